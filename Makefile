@@ -1,0 +1,57 @@
+# Build of the MI355X base64 byte-stream engine and its test oracle.
+#
+#   make            -> async_amd/libasync_b64.so  (product: HIP kernels + C ABI
+#                      + bytestream_1 stages + minimal loop/streams)
+#                      oracle/liboracle.so          (test infrastructure only)
+#                      tests/csrc/libstage_harness.so (test infrastructure only)
+#   make clean
+#
+# Everything is compiled for gfx950 only (no other offload targets, no
+# CUDA/HIP dual path).  Code object v5 keeps the library loadable by both
+# the ROCm 7.2 runtime of this image and the ROCm 7.0 runtime bundled with
+# the PyTorch wheel (the Python side imports torch first, see
+# async_amd/_lib.py).
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CC       ?= gcc
+ARCH     ?= gfx950
+HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC \
+            -Wall -Iinclude
+CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
+
+LIB      = async_amd/libasync_b64.so
+ORACLE   = oracle/liboracle.so
+HARNESS  = tests/csrc/libstage_harness.so
+OBJDIR   = build
+
+KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
+HOST_SRC   = async_amd/csrc/loop.c async_amd/csrc/streams.c async_amd/csrc/b64_stages.c
+HEADERS    = $(wildcard include/*.h)
+
+HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
+
+all: $(LIB) $(ORACLE) $(HARNESS)
+
+$(OBJDIR):
+	mkdir -p $(OBJDIR)
+
+$(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) | $(OBJDIR)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
+
+$(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h
+	$(CC) -O2 -std=c11 -fPIC -Wall -Wextra -shared -o $@ oracle/b64_oracle.c
+
+$(HARNESS): tests/csrc/stage_harness.c $(LIB) $(HEADERS)
+	$(CC) $(CFLAGS) -shared -o $@ tests/csrc/stage_harness.c \
+	    -Lasync_amd -lasync_b64 -Wl,-rpath,'$$ORIGIN/../../async_amd'
+
+clean:
+	rm -rf $(OBJDIR) $(LIB) $(ORACLE) $(HARNESS)
+
+.PHONY: all clean

@@ -1,0 +1,198 @@
+"""Host-side mirror of the base64 byte-stream engine over device tensors.
+
+Thin wrappers over the b64x C ABI (include/b64x.h): torch provides device
+memory and the stream, libasync_b64.so does the work.  The names follow the
+reference's operations (src/base64encoder.c ``base64_encode`` /
+src/base64decoder.c ``base64_decode``), applied to whole device-resident
+buffers and batches instead of a pull-model stream:
+
+    encode(x)                  one buffer      (b64x_encode_dev)
+    decode(x)                  one buffer      (b64x_decode_dev)
+    encode_strided / decode_strided            uniform batches
+    encode_batch / decode_batch                ragged batches (offsets)
+
+Every function raises (B64xError / RuntimeError) if the HIP library is
+missing or a call fails; nothing here computes base64 on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import B64xError, DecResult, alphabet  # noqa: F401
+
+HOLD_TAIL = 1  # B64X_DEC_HOLD_TAIL
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _u8(t: torch.Tensor, what: str) -> torch.Tensor:
+    if t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{what} must be a contiguous uint8 CUDA tensor")
+    return t
+
+
+def encoded_len(n: int, pad: bool = True) -> int:
+    return int(_lib.load().b64x_encoded_len(n, pad))
+
+
+def decoded_cap(nchars: int) -> int:
+    return int(_lib.load().b64x_decoded_cap(nchars))
+
+
+def workspace_size(nchars: int = 0) -> int:
+    return int(_lib.load().b64x_decode_workspace_size(nchars))
+
+
+def _abc(abc) -> _lib.Alphabet:
+    return abc if isinstance(abc, _lib.Alphabet) else alphabet(*abc) if abc else alphabet()
+
+
+def encode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
+           stream=None) -> torch.Tensor:
+    """Base64-encode a device buffer; returns the character tensor."""
+    lib = _lib.load()
+    a = _abc(abc)
+    _u8(x, "input")
+    n = x.numel()
+    m = encoded_len(n, a.pad)
+    if out is None:
+        out = torch.empty(max(m, 1), dtype=torch.uint8, device=x.device)
+    _u8(out, "output")
+    if out.numel() < m:
+        raise ValueError("output too small")
+    _lib.check("b64x_encode_dev", lib.b64x_encode_dev(
+        _ptr(x), n, _ptr(out), ctypes.byref(a), _stream(stream)))
+    return out[:m]
+
+
+@dataclass
+class Decoded:
+    out: torch.Tensor          # capacity-sized output buffer
+    result: torch.Tensor       # 24-byte b64x_dec_result on the device
+
+    def info(self) -> DecResult:
+        r = DecResult()
+        ctypes.memmove(ctypes.addressof(r), self.result.cpu().numpy().ctypes.data, 24)
+        return r
+
+    def bytes(self) -> torch.Tensor:
+        """The decoded bytes (synchronises to read the length)."""
+        return self.out[: self.info().out_len]
+
+
+def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
+           hold_tail: bool = False, workspace: torch.Tensor | None = None,
+           result: torch.Tensor | None = None, stream=None) -> Decoded:
+    """Leniently decode a device buffer of base64 characters."""
+    lib = _lib.load()
+    a = _abc(abc)
+    _u8(x, "input")
+    n = x.numel()
+    cap = decoded_cap(n)
+    if out is None:
+        out = torch.empty(max(cap, 1), dtype=torch.uint8, device=x.device)
+    _u8(out, "output")
+    if out.numel() < cap:
+        raise ValueError("output too small")
+    if result is None:
+        result = torch.zeros(24, dtype=torch.uint8, device=x.device)
+    if workspace is None:
+        workspace = torch.empty(workspace_size(n), dtype=torch.uint8, device=x.device)
+    _lib.check("b64x_decode_dev", lib.b64x_decode_dev(
+        _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a),
+        HOLD_TAIL if hold_tail else 0, _ptr(workspace), _stream(stream)))
+    return Decoded(out, result)
+
+
+def encode_strided(x: torch.Tensor, in_stride: int, length: int, nbuf: int,
+                   out: torch.Tensor, out_stride: int, abc=None, stream=None) -> None:
+    lib = _lib.load()
+    a = _abc(abc)
+    _u8(x, "input")
+    _u8(out, "output")
+    if nbuf and (x.numel() < (nbuf - 1) * in_stride + length or
+                 out.numel() < (nbuf - 1) * out_stride + encoded_len(length, a.pad)):
+        raise ValueError("buffers too small for the batch")
+    _lib.check("b64x_encode_strided", lib.b64x_encode_strided(
+        _ptr(x), in_stride, length, nbuf, _ptr(out), out_stride, ctypes.byref(a),
+        _stream(stream)))
+
+
+def decode_strided(x: torch.Tensor, in_stride: int, length: int, nbuf: int,
+                   out: torch.Tensor, out_stride: int, outlen: torch.Tensor,
+                   abc=None, stream=None) -> None:
+    lib = _lib.load()
+    a = _abc(abc)
+    _u8(x, "input")
+    _u8(out, "output")
+    if outlen.dtype != torch.int64 or outlen.numel() < nbuf or not outlen.is_cuda:
+        raise ValueError("outlen must be an int64 CUDA tensor with nbuf entries")
+    if nbuf and (x.numel() < (nbuf - 1) * in_stride + length or
+                 out.numel() < (nbuf - 1) * out_stride + decoded_cap(length)):
+        raise ValueError("buffers too small for the batch")
+    _lib.check("b64x_decode_strided", lib.b64x_decode_strided(
+        _ptr(x), in_stride, length, nbuf, _ptr(out), out_stride, _ptr(outlen),
+        ctypes.byref(a), _stream(stream)))
+
+
+def _offsets(t: torch.Tensor, n: int, what: str) -> torch.Tensor:
+    if t.dtype != torch.int64 or not t.is_cuda or t.numel() < n:
+        raise ValueError(f"{what} must be an int64 CUDA tensor of {n} entries")
+    return t
+
+
+def encode_batch(x: torch.Tensor, in_off: torch.Tensor, out: torch.Tensor,
+                 out_off: torch.Tensor, abc=None, stream=None) -> None:
+    """Ragged batch: buffer i = x[in_off[i]:in_off[i+1]] -> out[out_off[i]:]."""
+    lib = _lib.load()
+    a = _abc(abc)
+    nbuf = in_off.numel() - 1
+    _offsets(in_off, nbuf + 1, "in_off")
+    _offsets(out_off, nbuf, "out_off")
+    _lib.check("b64x_encode_batch", lib.b64x_encode_batch(
+        _ptr(_u8(x, "input")), _ptr(in_off), nbuf, _ptr(_u8(out, "output")),
+        _ptr(out_off), ctypes.byref(a), _stream(stream)))
+
+
+def decode_batch(x: torch.Tensor, in_off: torch.Tensor, out: torch.Tensor,
+                 out_off: torch.Tensor, outlen: torch.Tensor, abc=None,
+                 stream=None) -> None:
+    lib = _lib.load()
+    a = _abc(abc)
+    nbuf = in_off.numel() - 1
+    _offsets(in_off, nbuf + 1, "in_off")
+    _offsets(out_off, nbuf, "out_off")
+    _offsets(outlen, nbuf, "outlen")
+    _lib.check("b64x_decode_batch", lib.b64x_decode_batch(
+        _ptr(_u8(x, "input")), _ptr(in_off), nbuf, _ptr(_u8(out, "output")),
+        _ptr(out_off), _ptr(outlen), ctypes.byref(a), _stream(stream)))
+
+
+def fill_splitmix64(x: torch.Tensor, seed: int, stream=None) -> torch.Tensor:
+    """Fill a device buffer with the synthetic splitmix64 byte stream."""
+    lib = _lib.load()
+    _u8(x, "buffer")
+    _lib.check("b64x_fill_splitmix64", lib.b64x_fill_splitmix64(
+        _ptr(x), x.numel(), seed, _stream(stream)))
+    return x
+
+
+def device_check() -> None:
+    """Raise unless a gfx950 device is usable by the library."""
+    _lib.check("b64x_device_check", _lib.load().b64x_device_check())
+
+
+def build_info() -> str:
+    return _lib.load().b64x_build_info().decode()

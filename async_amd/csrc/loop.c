@@ -1,0 +1,308 @@
+/*
+ * loop.c -- minimal single-threaded event loop (include/async.h).
+ *
+ * Scope: only what the base64 stages and their test/bench topologies need
+ * (SURVEY.md §8(f) row f4).  The reference's loop (src/async.c) is an
+ * epoll/kqueue multiplexer with timers, immediate tasks, deferred frees
+ * and cross-thread notification; here:
+ *
+ *  - timers and immediate tasks share one binary min-heap ordered by
+ *    (expiry, sequence number); async_execute() is a timer that expires
+ *    at 0, so immediate tasks run in FIFO order before any timed one
+ *    (ref src/async.c:376-383);
+ *  - async_wound() queues the object and schedules a task that frees the
+ *    oldest wounded object, so a free happens only after every task that
+ *    was already scheduled (ref src/async.c:386-392);
+ *  - at most kBurst due tasks run before the loop polls file descriptors
+ *    (ref take_immediate_action, src/async.c:564-590, uses 20);
+ *  - async_register() watches a descriptor for readability with epoll;
+ *    the GPU completion eventfd of the stages goes through it.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdbool.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/epoll.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "async.h"
+
+enum { kBurst = 20, kMaxEvents = 16 };
+
+struct async_timer {
+    uint64_t expires;
+    uint64_t seq;
+    action_1 action;
+    size_t slot; /* index in the heap */
+};
+
+struct wounded {
+    void *object;
+    struct wounded *next;
+};
+
+struct fd_watch {
+    int fd;
+    action_1 action;
+    struct fd_watch *next;
+};
+
+struct async {
+    int epfd;
+    async_timer_t **heap;
+    size_t nheap, capheap;
+    uint64_t seq;
+    bool quit;
+    struct wounded *wound_head, *wound_tail;
+    struct fd_watch *watches;
+};
+
+uint64_t async_now(async_t *async)
+{
+    (void) async;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t) ts.tv_sec * 1000000000ull + (uint64_t) ts.tv_nsec;
+}
+
+static bool earlier(const async_timer_t *a, const async_timer_t *b)
+{
+    return a->expires < b->expires ||
+           (a->expires == b->expires && a->seq < b->seq);
+}
+
+static void heap_place(async_t *async, size_t i, async_timer_t *t)
+{
+    async->heap[i] = t;
+    t->slot = i;
+}
+
+static void sift_up(async_t *async, size_t i)
+{
+    async_timer_t *t = async->heap[i];
+    while (i > 0) {
+        size_t parent = (i - 1) / 2;
+        if (!earlier(t, async->heap[parent]))
+            break;
+        heap_place(async, i, async->heap[parent]);
+        i = parent;
+    }
+    heap_place(async, i, t);
+}
+
+static void sift_down(async_t *async, size_t i)
+{
+    async_timer_t *t = async->heap[i];
+    for (;;) {
+        size_t c = 2 * i + 1;
+        if (c >= async->nheap)
+            break;
+        if (c + 1 < async->nheap && earlier(async->heap[c + 1], async->heap[c]))
+            c++;
+        if (!earlier(async->heap[c], t))
+            break;
+        heap_place(async, i, async->heap[c]);
+        i = c;
+    }
+    heap_place(async, i, t);
+}
+
+static void heap_remove(async_t *async, size_t i)
+{
+    async_timer_t *last = async->heap[--async->nheap];
+    if (i == async->nheap)
+        return;
+    heap_place(async, i, last);
+    if (i > 0 && earlier(last, async->heap[(i - 1) / 2]))
+        sift_up(async, i);
+    else
+        sift_down(async, i);
+}
+
+async_t *make_async(void)
+{
+    async_t *async = calloc(1, sizeof *async);
+    if (!async)
+        return NULL;
+    async->epfd = epoll_create1(EPOLL_CLOEXEC);
+    if (async->epfd < 0) {
+        int e = errno;
+        free(async);
+        errno = e;
+        return NULL;
+    }
+    return async;
+}
+
+static void run_wound_task(async_t *async)
+{
+    struct wounded *w = async->wound_head;
+    if (!w)
+        return;
+    async->wound_head = w->next;
+    if (!async->wound_head)
+        async->wound_tail = NULL;
+    free(w->object);
+    free(w);
+}
+
+void destroy_async(async_t *async)
+{
+    if (!async)
+        return;
+    for (size_t i = 0; i < async->nheap; i++)
+        free(async->heap[i]);
+    free(async->heap);
+    while (async->wound_head)
+        run_wound_task(async);
+    while (async->watches) {
+        struct fd_watch *w = async->watches;
+        async->watches = w->next;
+        free(w);
+    }
+    close(async->epfd);
+    free(async);
+}
+
+async_timer_t *async_timer_start(async_t *async, uint64_t expires,
+                                 action_1 action)
+{
+    if (async->nheap == async->capheap) {
+        size_t cap = async->capheap ? 2 * async->capheap : 64;
+        async_timer_t **h = realloc(async->heap, cap * sizeof *h);
+        if (!h)
+            abort(); /* like fsalloc: allocation failure is fatal */
+        async->heap = h;
+        async->capheap = cap;
+    }
+    async_timer_t *t = malloc(sizeof *t);
+    if (!t)
+        abort();
+    t->expires = expires;
+    t->seq = async->seq++;
+    t->action = action;
+    heap_place(async, async->nheap++, t);
+    sift_up(async, async->nheap - 1);
+    return t;
+}
+
+void async_timer_cancel(async_t *async, async_timer_t *timer)
+{
+    heap_remove(async, timer->slot);
+    free(timer);
+}
+
+async_timer_t *async_execute(async_t *async, action_1 action)
+{
+    return async_timer_start(async, 0, action);
+}
+
+void async_wound(async_t *async, void *object)
+{
+    struct wounded *w = malloc(sizeof *w);
+    if (!w)
+        abort();
+    w->object = object;
+    w->next = NULL;
+    if (async->wound_tail)
+        async->wound_tail->next = w;
+    else
+        async->wound_head = w;
+    async->wound_tail = w;
+    async_execute(async, (action_1) { async, (act_1) run_wound_task });
+}
+
+void async_quit_loop(async_t *async)
+{
+    async->quit = true;
+}
+
+static struct fd_watch *find_watch(async_t *async, int fd)
+{
+    for (struct fd_watch *w = async->watches; w; w = w->next)
+        if (w->fd == fd)
+            return w;
+    return NULL;
+}
+
+int async_register(async_t *async, int fd, action_1 action)
+{
+    struct fd_watch *w = find_watch(async, fd);
+    if (w) {
+        w->action = action;
+        return 0;
+    }
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof ev);
+    ev.events = EPOLLIN;
+    ev.data.fd = fd;
+    if (epoll_ctl(async->epfd, EPOLL_CTL_ADD, fd, &ev) < 0)
+        return -1;
+    w = malloc(sizeof *w);
+    if (!w)
+        abort();
+    w->fd = fd;
+    w->action = action;
+    w->next = async->watches;
+    async->watches = w;
+    return 0;
+}
+
+int async_unregister(async_t *async, int fd)
+{
+    for (struct fd_watch **p = &async->watches; *p; p = &(*p)->next) {
+        if ((*p)->fd == fd) {
+            struct fd_watch *w = *p;
+            *p = w->next;
+            free(w);
+            return epoll_ctl(async->epfd, EPOLL_CTL_DEL, fd, NULL);
+        }
+    }
+    errno = ENOENT;
+    return -1;
+}
+
+int async_loop(async_t *async)
+{
+    async->quit = false;
+    while (!async->quit) {
+        uint64_t now = async_now(async);
+        for (int i = 0; i < kBurst && !async->quit && async->nheap; i++) {
+            async_timer_t *t = async->heap[0];
+            if (t->expires > now)
+                break;
+            heap_remove(async, 0);
+            action_1 a = t->action;
+            free(t);
+            action_1_perf(a);
+        }
+        if (async->quit)
+            break;
+        int timeout_ms = -1;
+        if (async->nheap) {
+            uint64_t exp = async->heap[0]->expires;
+            now = async_now(async);
+            timeout_ms = exp <= now ? 0 : (int) ((exp - now + 999999) / 1000000);
+        } else if (!async->watches) {
+            /* Nothing can ever happen again. */
+            errno = EDEADLK;
+            return -1;
+        }
+        struct epoll_event evs[kMaxEvents];
+        int n = epoll_wait(async->epfd, evs, kMaxEvents, timeout_ms);
+        if (n < 0) {
+            if (errno == EINTR)
+                continue;
+            return -1;
+        }
+        for (int i = 0; i < n && !async->quit; i++) {
+            struct fd_watch *w = find_watch(async, evs[i].data.fd);
+            if (w)
+                action_1_perf(w->action);
+        }
+    }
+    return 0;
+}

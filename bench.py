@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident base64 encode+decode throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s of base64 encode+decode, device-resident.
+A "step" = encode one 1 GiB buffer (BASELINE config 2: splitmix64 seed
+0x5EED, standard alphabet with padding) and decode the result back, both on
+the GPU, inputs already in HBM.  value = payload bytes (N per GPU per step)
+/ wall time of the K timed steps, summed over ranks (weak scaling: each
+rank owns its own 1 GiB buffer; the path shards by independent buffers and
+needs no collective on the data path).
+
+Also reported on the same JSON line:
+  roofline      the dominant kernel's algorithmic bytes per launch
+                (N + 4*ceil(N/3): read + write) / its average launch time
+                from HIP events over the timed region, against 8 TB/s;
+                `traffic` = HBM bytes per launch from the committed rocprofv3
+                PMC summary (profiles/pmc_<round>.json) when present;
+  cpu_baseline  the oracle's scalar C restatement of the reference
+                (oracle/, "port"), 1 thread, on a bounded sample of the same
+                data, rank 0 at N=1 only;
+  batch_cfg4    BASELINE config 4: 1,048,576 x 1 KiB buffers split across
+                the ranks by index range, strided encode + decode, plus the
+                one exchange step (allgather of per-rank output totals).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        (N > 1: launched by torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s base64 encode+decode, device-resident, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ROUND = "r01"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=1 << 30, help="bytes per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=512 << 20,
+                    help="bytes of the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-batch", action="store_true")
+    ap.add_argument("--batch-steps", type=int, default=20)
+    return ap.parse_args()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sync_all(world: int):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{ROUND}.json")
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+        return pmc["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def bench_single(args, world, rank, b64):
+    N = args.size
+    E = b64.encoded_len(N)
+    x = torch.empty(N, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    enc = torch.empty(E, dtype=torch.uint8, device="cuda")
+    dec = torch.empty(b64.decoded_cap(E), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(b64.workspace_size(E), dtype=torch.uint8, device="cuda")
+    res = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        b64.encode(x, out=enc, stream=stream)
+        b64.decode(enc, out=dec, workspace=ws, result=res, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness of the warmed-up result (bit-exact round trip)
+    info = b64.Decoded(dec, res).info()
+    ok = info.out_len == N and bool(torch.equal(dec[:N], x))
+    if not ok:
+        raise SystemExit(f"rank {rank}: round trip mismatch (out_len={info.out_len})")
+
+    K = args.steps
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    sync_all(world)
+    t0 = time.perf_counter()
+    for k in range(K):
+        evs[k][0].record(stream)
+        b64.encode(x, out=enc, stream=stream)
+        evs[k][1].record(stream)
+        b64.decode(enc, out=dec, workspace=ws, result=res, stream=stream)
+        evs[k][2].record(stream)
+    sync_all(world)
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, world)
+    enc_ms = [evs[k][0].elapsed_time(evs[k][1]) for k in range(K)]
+    dec_ms = [evs[k][1].elapsed_time(evs[k][2]) for k in range(K)]
+    return {"N": N, "E": E, "K": K, "wall": wall,
+            "enc_ms": statistics.mean(enc_ms), "dec_ms": statistics.mean(dec_ms),
+            "enc_ms_min": min(enc_ms), "dec_ms_min": min(dec_ms)}
+
+
+def bench_batch(args, world, rank, b64):
+    """BASELINE config 4: 1 M x 1 KiB, sharded across ranks by index."""
+    total_buf, L = 1 << 20, 1024
+    per = total_buf // world
+    lo = rank * per + min(rank, total_buf % world)
+    nbuf = per + (1 if rank < total_buf % world else 0)
+    Es = b64.encoded_len(L)
+    cap = b64.decoded_cap(Es)
+    x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED + lo)
+    enc = torch.empty(nbuf * Es, dtype=torch.uint8, device="cuda")
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device="cuda")
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    totals = torch.zeros(world, dtype=torch.int64, device="cuda")
+
+    def step():
+        b64.encode_strided(x, L, L, nbuf, enc, Es, stream=stream)
+        b64.decode_strided(enc, Es, Es, nbuf, dec, cap, outlen, stream=stream)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ok = bool((outlen == L).all()) and bool(torch.equal(dec.view(nbuf, cap)[:, :L],
+                                                        x.view(nbuf, L)))
+    if not ok:
+        raise SystemExit(f"rank {rank}: batch round trip mismatch")
+    K = args.batch_steps
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    sync_all(world)
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for _ in range(K):
+        b64.encode_strided(x, L, L, nbuf, enc, Es, stream=stream)
+    ev[1].record(stream)
+    for _ in range(K):
+        b64.decode_strided(enc, Es, Es, nbuf, dec, cap, outlen, stream=stream)
+    ev[2].record(stream)
+    # the one exchange step: every rank learns every rank's output total
+    mine = outlen.sum().reshape(1)
+    if world > 1:
+        dist.all_gather_into_tensor(totals, mine)
+    else:
+        totals.copy_(mine)
+    sync_all(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    assert int(totals.sum()) == total_buf * L
+    return {
+        "workload": "cfg4: 1,048,576 x 1 KiB buffers split across ranks, strided "
+                    "encode then decode, + allgather of per-rank output totals",
+        "buffers_per_rank": nbuf,
+        "value": total_buf * L * K / wall / 2**30,
+        "unit": "GiB/s",
+        "ms_per_step": wall / K * 1e3,
+        "encode_kernel_ms": ev[0].elapsed_time(ev[1]) / K,
+        "decode_kernel_ms": ev[1].elapsed_time(ev[2]) / K,
+        "roofline_frac": (2 * (nbuf * (L + Es))) /
+                         ((ev[0].elapsed_time(ev[2]) / K) * 1e-3) / (HBM_PEAK_GBS * 1e9),
+    }
+
+
+def cpu_baseline(args, b64):
+    import numpy as np
+
+    from oracle import pyoracle
+
+    n = args.cpu_sample
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    host = x.cpu().numpy()
+    t0 = time.perf_counter()
+    e = pyoracle.encode(host, as_array=True)
+    t1 = time.perf_counter()
+    d = pyoracle.decode(e, as_array=True)
+    t2 = time.perf_counter()
+    if not np.array_equal(d, host):
+        raise SystemExit("cpu baseline round trip mismatch")
+    return {
+        "value": n / (t2 - t0) / 2**30,
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {n >> 20} MiB of the cfg2 buffer: oracle/b64_oracle.c "
+                  f"(scalar restatement of src/base64encoder.c + src/base64decoder.c, "
+                  f"-O2, 1 thread), encode {n / (t1 - t0) / 2**30:.3f} GiB/s, "
+                  f"decode {n / (t2 - t1) / 2**30:.3f} GiB/s; host "
+                  f"{os.cpu_count()} logical CPUs",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from async_amd import b64
+
+    b64.device_check()
+    r = bench_single(args, world, rank, b64)
+    batch = None if args.no_batch else bench_batch(args, world, rank, b64)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, b64)
+
+    if rank == 0:
+        N, E, K = r["N"], r["E"], r["K"]
+        per_launch = N + E  # algorithmic bytes per launch (read + write)
+        dom = "encode" if r["enc_ms"] >= r["dec_ms"] else "decode"
+        dom_ms = max(r["enc_ms"], r["dec_ms"])
+        achieved = per_launch / (dom_ms * 1e-3) / 1e9
+        kname = "k_encode" if dom == "encode" else "k_decode_pass1"
+        out = {
+            "metric": METRIC,
+            "value": world * N * K / r["wall"] / 2**30,
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": r["wall"] / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: splitmix64(0x5EED) bytes generated in HBM; round trip "
+                    "verified bit-exact before timing",
+            "config": {
+                "workload": "cfg2: one 1 GiB buffer per GPU, encode (std alphabet, pad) "
+                            "then decode, device-resident",
+                "bytes_per_gpu": N,
+                "chars_per_gpu": E,
+                "parallelism": f"independent buffers x{world} (no data-path collective)",
+            },
+            "encode_ms": r["enc_ms"],
+            "decode_ms": r["dec_ms"],
+            "encode_GBps": per_launch / (r["enc_ms"] * 1e-3) / 1e9,
+            "decode_GBps": per_launch / (r["dec_ms"] * 1e-3) / 1e9,
+            "roundtrip_hbm_frac": 2 * per_launch / ((r["enc_ms"] + r["dec_ms"]) * 1e-3)
+                                  / (HBM_PEAK_GBS * 1e9),
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kname,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(kname),
+            },
+            "cpu_baseline": cpu,
+            "batch_cfg4": batch,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

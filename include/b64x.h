@@ -1,0 +1,173 @@
+/*
+ * b64x.h -- C ABI of the MI355X (gfx950) base64 engine.
+ *
+ * This is the thin shim between host code (the bytestream_1 stages in
+ * include/base64encoder.h / base64decoder.h, Python via ctypes, any FFI)
+ * and the hand-written HIP kernels in async_amd/csrc/b64x_kernels.hip.
+ * Only plain pointers, sizes and PODs cross it; no HIP or torch types.
+ *
+ * What each entry point replaces in the reference (all C, CPU only):
+ *
+ *   b64x_encode_dev / _strided / _batch
+ *       the per-byte bit-accumulator loop of do_read() + finalize(),
+ *       /root/reference/src/base64encoder.c:61-142, applied to a whole
+ *       device-resident buffer (or a batch of independent buffers -- one
+ *       encoder object per buffer in the reference).
+ *   b64x_decode_dev / _strided / _batch
+ *       the per-character loop of decoder_read() with map(),
+ *       /root/reference/src/base64decoder.c:38-80, including its
+ *       leniency (non-alphabet bytes skipped, bits carried across '=',
+ *       trailing partial bits dropped).
+ *   b64x_session_*
+ *       the host-memory leg of the bytestream_1 stages: pinned staging,
+ *       H2D, kernel, D2H.
+ *
+ * Error convention: 0 on success or a negative errno value (-EINVAL bad
+ * argument, -ENOMEM allocation, -ENODEV no usable GPU, -EIO any other
+ * HIP failure).  Nothing here aborts.
+ *
+ * All device pointers are HIP device (or host-pinned-mapped) pointers.
+ * `stream` is a hipStream_t passed as void * (NULL = the null stream).
+ * Device-side launches are asynchronous and capture-safe (no allocation
+ * or synchronisation inside) unless the comment says otherwise.
+ */
+#ifndef ASYNC_AMD_B64X_H
+#define ASYNC_AMD_B64X_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define B64X_ABI_VERSION 1
+
+/* Alphabet descriptor.  (char) -1 selects the reference's defaults,
+ * exactly like base64_encode()/base64_decode() (ref
+ * src/base64encoder.c:40-43, src/base64decoder.c:31-32).  `pad` and
+ * `padchar` are ignored by the decoder, which has no pad parameter. */
+typedef struct b64x_alphabet {
+    char pos62;
+    char pos63;
+    char padchar;
+    bool pad;
+} b64x_alphabet;
+
+/* Per-call decode result, written by the device. */
+typedef struct b64x_dec_result {
+    uint64_t out_len;  /* bytes written to the output */
+    uint64_t valid;    /* alphabet characters seen (V) */
+    uint32_t tail_n;   /* V mod 4 */
+    uint8_t tail[4];   /* the last tail_n sextet values (0..63) */
+} b64x_dec_result;
+
+/* Decode flags. */
+#define B64X_DEC_HOLD_TAIL 1u /* emit only whole 4-char groups (3 bytes
+                                 each); the V mod 4 trailing sextets are
+                                 reported in b64x_dec_result.tail and
+                                 produce no output.  Used by the streaming
+                                 stage, which carries them to its next
+                                 call. */
+
+/* ---- sizes ------------------------------------------------------------ */
+
+/* Characters produced for n input bytes: 4*ceil(n/3) with pad,
+ * ceil(4n/3) without. */
+uint64_t b64x_encoded_len(uint64_t n, bool pad);
+/* Output capacity the decoder needs for n input characters:
+ * 3*ceil(n/4).  Bytes beyond b64x_dec_result.out_len are unspecified
+ * (the reference likewise treats the caller's whole buffer as scratch,
+ * src/base64decoder.c:58). */
+uint64_t b64x_decoded_cap(uint64_t nchars);
+/* Device workspace bytes b64x_decode_dev() needs for nchars. */
+uint64_t b64x_decode_workspace_size(uint64_t nchars);
+
+/* ---- one device-resident buffer ----------------------------------------- */
+
+/* Encode n bytes at d_in into b64x_encoded_len(n, abc->pad) characters at
+ * d_out.  Any alignment is accepted; 4-byte aligned d_in and 16-byte
+ * aligned d_out take the fast path. */
+int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
+                    const b64x_alphabet *abc, void *stream);
+
+/* Decode nchars characters at d_in into d_out (capacity
+ * b64x_decoded_cap(nchars)); *d_res (device memory) receives the result.
+ * d_workspace: b64x_decode_workspace_size(nchars) bytes of device memory,
+ * or NULL to use a library-owned workspace (allocated on first use; not
+ * capture-safe on that first call, and not safe to share between
+ * concurrent streams). */
+int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
+                    b64x_dec_result *d_res, const b64x_alphabet *abc,
+                    unsigned flags, void *d_workspace, void *stream);
+
+/* ---- batches of independent buffers ----------------------------------- */
+
+/* nbuf buffers of `len` bytes at d_in + i*in_stride; buffer i's
+ * b64x_encoded_len(len, pad) characters go to d_out + i*out_stride. */
+int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
+                        uint32_t nbuf, void *d_out, uint64_t out_stride,
+                        const b64x_alphabet *abc, void *stream);
+
+/* nbuf buffers of `len` characters at d_in + i*in_stride, decoded to
+ * d_out + i*out_stride (capacity b64x_decoded_cap(len) each);
+ * d_outlen[i] (device) receives buffer i's byte count. */
+int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
+                        uint32_t nbuf, void *d_out, uint64_t out_stride,
+                        uint64_t *d_outlen, const b64x_alphabet *abc,
+                        void *stream);
+
+/* Ragged batch: buffer i is d_in[d_in_off[i] .. d_in_off[i+1]) (nbuf+1
+ * monotone offsets, device memory) and goes to d_out + d_out_off[i]. */
+int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off,
+                      uint32_t nbuf, void *d_out, const uint64_t *d_out_off,
+                      const b64x_alphabet *abc, void *stream);
+int b64x_decode_batch(const void *d_in, const uint64_t *d_in_off,
+                      uint32_t nbuf, void *d_out, const uint64_t *d_out_off,
+                      uint64_t *d_outlen, const b64x_alphabet *abc,
+                      void *stream);
+
+/* ---- host-memory sessions (used by the bytestream_1 stages) ----------- */
+
+typedef struct b64x_session b64x_session;
+
+/* A session owns a HIP stream, pinned host staging of `capacity` input
+ * bytes/characters and matching device buffers.  NULL + errno on
+ * failure (ENODEV when no GPU is usable). */
+b64x_session *b64x_session_open(uint64_t capacity);
+void b64x_session_close(b64x_session *s);
+uint64_t b64x_session_capacity(const b64x_session *s);
+/* Pinned host staging areas: fill host_in, read results from host_out. */
+uint8_t *b64x_session_host_in(b64x_session *s);
+uint8_t *b64x_session_host_out(b64x_session *s);
+
+/* Synchronous round trips host_in[0..n) -> GPU -> host_out.  The encoder
+ * leg encodes all n bytes (padding the final group iff `final` and
+ * abc->pad); the caller passes whole 3-byte groups unless `final`.  The
+ * decoder leg honours `flags` as b64x_decode_dev(). */
+int b64x_session_encode(b64x_session *s, uint64_t n,
+                        const b64x_alphabet *abc, uint64_t *out_len);
+int b64x_session_decode(b64x_session *s, uint64_t n,
+                        const b64x_alphabet *abc, unsigned flags,
+                        b64x_dec_result *res);
+
+/* ---- utilities ----------------------------------------------------------- */
+
+/* Fill n bytes with the splitmix64 stream used by every synthetic
+ * workload: 8 little-endian bytes per step,
+ * state = seed + k*0x9E3779B97F4A7C15 for k = 1, 2, ... */
+int b64x_fill_splitmix64(void *d_out, uint64_t n, uint64_t seed,
+                         void *stream);
+
+/* 0 if a gfx950 device is usable, -ENODEV otherwise. */
+int b64x_device_check(void);
+/* Static description of the compiled kernels (for logs). */
+const char *b64x_build_info(void);
+const char *b64x_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ASYNC_AMD_B64X_H */

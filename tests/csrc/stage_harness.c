@@ -1,0 +1,266 @@
+/*
+ * stage_harness.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Drives the product's bytestream_1 stages (libasync_b64.so) on the
+ * product's own event loop, the way the reference's test does
+ * (test/asynctest-base64encoder.c:86-151): a verify action reads from the
+ * outermost stream, re-schedules itself with async_execute() after data,
+ * waits for the registered callback after EAGAIN and quits at EOF.
+ * Python calls these through ctypes (tests/test_stages_gpu.py).
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "async.h"
+#include "base64decoder.h"
+#include "base64encoder.h"
+#include "blobstream.h"
+#include "nicestream.h"
+
+/* ---- counting source: test/asynctest-base64encoder.c:11-78 ------------ */
+
+typedef struct {
+    async_t *async;
+    size_t size, cursor;
+} counting_source;
+
+static ssize_t cs_read(void *obj, void *buf, size_t count)
+{
+    counting_source *s = obj;
+    size_t remaining = s->size - s->cursor;
+    if (remaining < count)
+        count = remaining;
+    uint8_t *p = buf;
+    for (size_t i = 0; i < count; i++)
+        *p++ = (uint8_t) s->cursor++;
+    return (ssize_t) count;
+}
+
+static void cs_close(void *obj)
+{
+    counting_source *s = obj;
+    async_wound(s->async, s);
+    s->async = NULL;
+}
+
+static void cs_reg(void *obj, action_1 a)
+{
+    (void) obj;
+    (void) a;
+}
+
+static void cs_unreg(void *obj)
+{
+    (void) obj;
+}
+
+static const struct bytestream_1_vt cs_vt = { cs_read, cs_close, cs_reg,
+                                              cs_unreg };
+
+/* ---- tap: copies what flows between two stages ------------------------ */
+
+typedef struct {
+    async_t *async;
+    bytestream_1 up;
+    uint8_t *copy;
+    size_t cap, len;
+    size_t *len_out; /* outlives the stream, which the loop frees */
+    int overflow;
+} tap_stream;
+
+static ssize_t tap_read(void *obj, void *buf, size_t count)
+{
+    tap_stream *t = obj;
+    ssize_t n = bytestream_1_read(t->up, buf, count);
+    if (n > 0) {
+        if (t->copy && t->len + (size_t) n <= t->cap)
+            memcpy(t->copy + t->len, buf, (size_t) n);
+        else if (t->copy)
+            t->overflow = 1;
+        t->len += (size_t) n;
+        if (t->len_out)
+            *t->len_out = t->len;
+    }
+    return n;
+}
+
+static void tap_close(void *obj)
+{
+    tap_stream *t = obj;
+    bytestream_1_close(t->up);
+    async_wound(t->async, t);
+    t->async = NULL;
+}
+
+static void tap_reg(void *obj, action_1 a)
+{
+    tap_stream *t = obj;
+    bytestream_1_register_callback(t->up, a);
+}
+
+static void tap_unreg(void *obj)
+{
+    tap_stream *t = obj;
+    bytestream_1_unregister_callback(t->up);
+}
+
+static const struct bytestream_1_vt tap_vt = { tap_read, tap_close, tap_reg,
+                                               tap_unreg };
+
+/* ---- the consumer ----------------------------------------------------- */
+
+typedef struct {
+    async_t *async;
+    bytestream_1 material;
+    size_t read_size;
+    uint8_t *out;
+    size_t cap, len;
+    int err;      /* errno of a failed read, 0 otherwise */
+    int done;
+    size_t eagains, reads;
+} consumer;
+
+static void consume(consumer *c)
+{
+    if (c->done)
+        return;
+    uint8_t *buf = malloc(c->read_size);
+    if (!buf)
+        abort();
+    ssize_t n = bytestream_1_read(c->material, buf, c->read_size);
+    c->reads++;
+    if (n < 0) {
+        free(buf);
+        if (errno == EAGAIN) {
+            c->eagains++;
+            return; /* the registered callback brings us back */
+        }
+        c->err = errno;
+        c->done = 1;
+        bytestream_1_close(c->material);
+        async_quit_loop(c->async);
+        return;
+    }
+    if (n == 0) {
+        free(buf);
+        c->done = 1;
+        bytestream_1_close(c->material);
+        async_quit_loop(c->async);
+        return;
+    }
+    if (c->len + (size_t) n > c->cap) {
+        free(buf);
+        c->err = ENOSPC;
+        c->done = 1;
+        bytestream_1_close(c->material);
+        async_quit_loop(c->async);
+        return;
+    }
+    memcpy(c->out + c->len, buf, (size_t) n);
+    c->len += (size_t) n;
+    free(buf);
+    async_execute(c->async, (action_1) { c, (act_1) consume });
+}
+
+static ssize_t run(async_t *async, bytestream_1 material, size_t read_size,
+                   uint8_t *out, size_t cap, int *err_out, size_t *eagains)
+{
+    consumer c;
+    memset(&c, 0, sizeof c);
+    c.async = async;
+    c.material = material;
+    c.read_size = read_size;
+    c.out = out;
+    c.cap = cap;
+    action_1 cb = { &c, (act_1) consume };
+    bytestream_1_register_callback(material, cb);
+    async_execute(async, cb);
+    int rc = async_loop(async);
+    if (err_out)
+        *err_out = rc < 0 ? errno : c.err;
+    if (eagains)
+        *eagains = c.eagains;
+    /* Let wounded objects be freed. */
+    destroy_async(async);
+    if (rc < 0 || c.err)
+        return -1;
+    return (ssize_t) c.len;
+}
+
+/* The reference topology, with the product's stages in the middle. */
+ssize_t h_reftest(size_t length, uint8_t *enc_out, size_t enc_cap,
+                  size_t *enc_len, uint8_t *dec_out, size_t dec_cap,
+                  int *err_out, size_t *eagains)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    counting_source *src = calloc(1, sizeof *src);
+    src->async = async;
+    src->size = length;
+    nicestream_t *n1 = make_nice(async, (bytestream_1) { src, &cs_vt }, 113);
+    base64encoder_t *enc = base64_encode(async, nicestream_as_bytestream_1(n1),
+                                         '.', '_', true, '-');
+    tap_stream *tap = calloc(1, sizeof *tap);
+    tap->async = async;
+    tap->up = base64encoder_as_bytestream_1(enc);
+    tap->copy = enc_out;
+    tap->cap = enc_cap;
+    if (enc_len)
+        *enc_len = 0;
+    tap->len_out = enc_len;
+    nicestream_t *n2 = make_nice(async, (bytestream_1) { tap, &tap_vt }, 91);
+    base64decoder_t *dec =
+        base64_decode(async, nicestream_as_bytestream_1(n2), '.', '_');
+    nicestream_t *n3 = make_nice(async, base64decoder_as_bytestream_1(dec), 97);
+    return run(async, nicestream_as_bytestream_1(n3), 200, dec_out, dec_cap,
+               err_out, eagains);
+}
+
+static bytestream_1 blob_chain(async_t *async, const uint8_t *in, size_t n,
+                               size_t burst)
+{
+    bytestream_1 s = blobstream_as_bytestream_1(open_blobstream(async, in, n));
+    if (burst)
+        s = nicestream_as_bytestream_1(make_nice(async, s, burst));
+    return s;
+}
+
+ssize_t h_encode_stream(const uint8_t *in, size_t n, size_t burst,
+                        size_t read_size, char pos62, char pos63, int pad,
+                        char padchar, uint8_t *out, size_t cap, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    base64encoder_t *enc = base64_encode(async, blob_chain(async, in, n, burst),
+                                         pos62, pos63, pad != 0, padchar);
+    return run(async, base64encoder_as_bytestream_1(enc), read_size, out, cap,
+               err_out, NULL);
+}
+
+ssize_t h_decode_stream(const uint8_t *in, size_t n, size_t burst,
+                        size_t read_size, char pos62, char pos63, uint8_t *out,
+                        size_t cap, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    base64decoder_t *dec =
+        base64_decode(async, blob_chain(async, in, n, burst), pos62, pos63);
+    return run(async, base64decoder_as_bytestream_1(dec), read_size, out, cap,
+               err_out, NULL);
+}
+
+/* Loop + streams only (no GPU): blob -> nice(burst) -> consumer. */
+ssize_t h_copy_stream(const uint8_t *in, size_t n, size_t burst,
+                      size_t read_size, uint8_t *out, size_t cap, int *err_out,
+                      size_t *eagains)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    return run(async, blob_chain(async, in, n, burst), read_size, out, cap,
+               err_out, eagains);
+}

@@ -1,0 +1,110 @@
+"""The C-ABI library loads and exports every declared symbol; host-only
+logic (loop, streams, stage error paths) works without a GPU.  CPU only:
+nothing here launches a kernel."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from async_amd import _lib
+from tests import util
+
+ROOT = util.ROOT
+
+
+def _declared(header: str):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"static inline[^{]*\{[^}]*\}", "", src)
+    # file-scope declarations start in column 0: "<type> [*]name(".
+    return set(re.findall(r"(?m)^(?:const\s+)?[a-z_]\w*[\s*]+([a-z_]\w*)\s*\(", src)) \
+        - {"void"}
+
+
+def _exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_library_built_in_tree():
+    assert os.path.exists(_lib.LIB_PATH), "run make / __graft_entry__.build()"
+
+
+def test_every_declared_symbol_is_exported():
+    exported = _exported()
+    headers = ["b64x.h", "base64encoder.h", "base64decoder.h", "async.h",
+               "bytestream_1.h", "blobstream.h", "nicestream.h"]
+    for h in headers:
+        for name in _declared(h):
+            assert name in exported, f"{h}: {name} not exported"
+    assert "NULL_ACTION_1" in exported
+    # and the Python binding covers all of b64x.h
+    assert _declared("b64x.h") == set(_lib.SIGNATURES)
+    for name in _lib.STAGE_SYMBOLS:
+        assert name in exported, name
+
+
+def test_binding_loads_and_sizes():
+    lib = _lib.load()
+    assert lib.b64x_encoded_len(0, True) == 0
+    assert lib.b64x_encoded_len(1, True) == 4 and lib.b64x_encoded_len(1, False) == 2
+    assert lib.b64x_encoded_len(2, False) == 3 and lib.b64x_encoded_len(3, False) == 4
+    assert lib.b64x_encoded_len(1 << 30, True) == 1431655768
+    assert lib.b64x_decoded_cap(1431655768) == 1073741826
+    assert lib.b64x_decode_workspace_size(1 << 30) > 0
+    assert b"gfx950" in lib.b64x_build_info()
+    assert lib.b64x_strerror(-22) == b"invalid argument"
+
+
+def test_no_gpu_fails_loudly():
+    """Without a usable gfx950 the ABI reports ENODEV; it never computes on
+    the CPU instead."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = _lib.load()
+    assert lib.b64x_device_check() == -19
+    buf = (ctypes.c_uint8 * 16)()
+    a = _lib.alphabet()
+    assert lib.b64x_encode_dev(ctypes.addressof(buf), 3, ctypes.addressof(buf),
+                               ctypes.byref(a), None) == -19
+    assert lib.b64x_session_open(1024) is None
+    # the bytestream_1 stages surface it as -1 / errno ENODEV on read()
+    out, err = util.stage_encode(b"hello world")
+    assert out is None and err == 19
+    out, err = util.stage_decode(b"aGVsbG8=")
+    assert out is None and err == 19
+
+
+def test_argument_validation():
+    lib = _lib.load()
+    a = _lib.alphabet()
+    assert lib.b64x_encode_dev(None, 5, None, ctypes.byref(a), None) == -22
+    assert lib.b64x_encode_dev(None, 0, None, ctypes.byref(a), None) == 0
+    assert lib.b64x_decode_dev(None, 4, None, None, ctypes.byref(a), 0, None, None) == -22
+    res = _lib.DecResult()
+    assert lib.b64x_decode_dev(None, 4, None, ctypes.byref(res), ctypes.byref(a),
+                               0x80, None, None) == -22
+
+
+@pytest.mark.parametrize("burst", [0, 1, 7, 113])
+@pytest.mark.parametrize("read_size", [1, 3, 200, 4096])
+def test_loop_and_streams_copy(burst, read_size):
+    """blobstream -> nicestream -> consumer on the product event loop: bytes
+    arrive intact and nicestream's EAGAIN/retry path is exercised."""
+    rng = np.random.default_rng(burst * 7 + read_size)
+    data = rng.integers(0, 256, 5000, dtype=np.uint8)
+    out = np.empty(6000, np.uint8)
+    err = ctypes.c_int(0)
+    eag = ctypes.c_size_t(0)
+    n = util.harness().h_copy_stream(data.ctypes.data, data.size, burst, read_size,
+                                     out.ctypes.data, out.size, ctypes.byref(err),
+                                     ctypes.byref(eag))
+    assert n == data.size and err.value == 0
+    assert (out[:n] == data).all()
+    if burst:
+        assert eag.value > 0

@@ -1,0 +1,285 @@
+"""GPU parity: the HIP kernels, called through the C ABI, against the
+oracle and the golden fixtures.  Bit-exact everywhere (integer/byte work).
+
+Sizes: oracle comparisons at sizes the oracle finishes in well under a
+second; full BASELINE sizes (1 GiB, 1 M x 1 KiB) through size-independent
+properties (digests recorded from the reference, round trips, lengths).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from async_amd import b64
+from oracle import pyoracle as orc
+from tests import util
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def dev(data) -> torch.Tensor:
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    if a.size == 0:
+        return torch.empty(0, dtype=torch.uint8, device=DEV)
+    return torch.from_numpy(a.copy()).to(DEV)
+
+
+def genc(data, pos62=-1, pos63=-1, pad=True, padchar=-1) -> bytes:
+    return b64.encode(dev(data), abc=(pos62, pos63, pad, padchar)).cpu().numpy().tobytes()
+
+
+def gdec(chars, pos62=-1, pos63=-1, hold=False):
+    d = b64.decode(dev(chars), abc=(pos62, pos63, True, -1), hold_tail=hold)
+    return d.bytes().cpu().numpy().tobytes(), d.info()
+
+
+def test_device_and_library():
+    b64.device_check()
+    assert "gfx950" in b64.build_info()
+
+
+def test_encode_kat():
+    for c in util.golden("kat_encode.json"):
+        data = (util.splitmix64(c["seed"], c["n"]).tobytes() if "gen" in c
+                else bytes.fromhex(c["in"]))
+        got = genc(data, c["pos62"], c["pos63"], c["pad"], c["padchar"])
+        if "out" in c:
+            assert got.hex() == c["out"], (c["mode"], len(data))
+        else:
+            assert hashlib.sha256(got).hexdigest() == c["out_sha256"], c["n"]
+
+
+def test_decode_kat():
+    for c in util.golden("kat_decode.json"):
+        got, _ = gdec(bytes.fromhex(c["in"]), c["pos62"], c["pos63"])
+        assert got.hex() == c["out"], (c["mode"], c["variant"])
+
+
+def test_leniency_table():
+    t = util.golden("leniency.json")
+    for c in t["decode"]:
+        got, _ = gdec(bytes.fromhex(c["in"]), c["pos62"], c["pos63"])
+        assert got.hex() == c["out"], c
+    for c in t["encode"]:
+        got = genc(bytes.fromhex(c["in"]), c["pos62"], c["pos63"], c["pad"], c["padchar"])
+        assert got.decode() == c["out"], c
+
+
+@pytest.mark.parametrize("abc", [(-1, -1, True, -1), (-1, -1, False, -1),
+                                 (".", "_", True, "-"), (0xE9, 0xE8, True, 0x80)])
+def test_encode_sizes_vs_oracle(abc):
+    rng = np.random.default_rng(1)
+    sizes = list(range(0, 100)) + [767, 768, 769, 3071, 3072, 3073, 12 * 1024 + 5,
+                                   65535, 65536, 65537, 1 << 20, (1 << 20) + 1]
+    sizes += list(rng.integers(100, 300000, 12))
+    for n in sizes:
+        host = rng.integers(0, 256, int(n), dtype=np.uint8)
+        assert genc(host, *abc) == orc.encode(host, *abc), n
+
+
+def test_encode_misaligned():
+    """Input and output views at every offset mod 16 (fallback paths)."""
+    rng = np.random.default_rng(2)
+    host = rng.integers(0, 256, 50000, dtype=np.uint8)
+    big = dev(host)
+    for off in range(16):
+        for n in (1, 11, 12, 13, 4097, 40000):
+            x = big[off:off + n]
+            out = torch.zeros(b64.encoded_len(n) + 32, dtype=torch.uint8, device=DEV)
+            o = out[(off * 7) % 16:]
+            got = b64.encode(x, out=o).cpu().numpy().tobytes()
+            assert got == orc.encode(host[off:off + n]), (off, n)
+
+
+def _junk(rng, chars: bytes, density: float, run_every=0, run_len=0) -> bytes:
+    a = np.frombuffer(chars, dtype=np.uint8)
+    junk_set = np.array([c for c in range(256) if not (chr(c).isalnum() and c < 128)
+                         and c not in b"+/"], dtype=np.uint8)
+    if density > 0:
+        k = max(1, int(len(a) * density))
+        pos = np.sort(rng.integers(0, len(a) + 1, k))
+        a = np.insert(a, pos, rng.choice(junk_set, k))
+    if run_every:
+        pieces = []
+        for i in range(0, len(a), run_every):
+            pieces.append(a[i:i + run_every])
+            pieces.append(rng.choice(junk_set, run_len))
+        a = np.concatenate(pieces) if pieces else a
+    return a.tobytes()
+
+
+@pytest.mark.parametrize("density", [0.0, 1e-5, 1e-3, 0.05, 0.5])
+def test_decode_dirty_vs_oracle(density):
+    """Junk anywhere, including across the kernel's range boundaries."""
+    rng = np.random.default_rng(int(density * 1e6) + 3)
+    for n in (0, 1, 5, 1000, 4096 * 3 + 17, 300000, 2_000_000):
+        host = rng.integers(0, 256, n, dtype=np.uint8)
+        chars = orc.encode(host)
+        dirty = _junk(rng, chars, density)
+        got, info = gdec(dirty)
+        want = orc.decode(dirty)
+        assert got == want, (n, density)
+        if density == 0.0:
+            assert got == host.tobytes()
+
+
+def test_decode_structured_junk():
+    rng = np.random.default_rng(4)
+    host = rng.integers(0, 256, 1_500_000, dtype=np.uint8)
+    chars = orc.encode(host)
+    cases = {
+        "crlf76": b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76)),
+        "pad_mid": chars[:100001] + b"==" + chars[100001:],
+        "long_runs": _junk(rng, chars, 0, run_every=700_001, run_len=300_000),
+        "lead_trail": b"\n" * 5000 + chars + b"=\n" * 9000,
+        "tiny_runs": _junk(rng, chars, 0, run_every=4093, run_len=3),
+    }
+    for name, dirty in cases.items():
+        got, info = gdec(dirty)
+        assert got == orc.decode(dirty), name
+    # all junk
+    junk = bytes(rng.integers(0x80, 0x100, 1_000_000, dtype=np.uint8))
+    got, info = gdec(junk)
+    assert got == b"" and info.valid == 0 and info.out_len == 0
+
+
+def test_decode_result_and_hold_tail():
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 3, 4, 5, 6, 7, 8, 100, 4096 * 5 + 1, 4096 * 5 + 2, 1 << 20):
+        host = rng.integers(0, 256, n, dtype=np.uint8)
+        chars = orc.encode(host, pad=False)
+        dirty = _junk(rng, chars, 0.01)
+        table = orc.decode_table()
+        alnum = [c for c in dirty if table[c] >= 0]
+        valid = len(alnum)
+        got, info = gdec(dirty)
+        assert info.valid == valid and info.out_len == valid * 6 // 8 == len(got)
+        assert info.tail_n == valid % 4
+        held, hinfo = gdec(dirty, hold=True)
+        assert hinfo.out_len == valid // 4 * 3 and held == got[: hinfo.out_len]
+        tail = [table[c] for c in alnum[len(alnum) - valid % 4:]] if valid % 4 else []
+        assert list(hinfo.tail[: hinfo.tail_n]) == tail
+
+
+@pytest.mark.parametrize("abc", [(".", "_"), ("A", "*"), ("*", "*"), (0xE9, 0xE8),
+                                 ("=", "\n")])
+def test_decode_alphabets_vs_oracle(abc):
+    rng = np.random.default_rng(6)
+    table = np.array(orc.decode_table(*abc))
+    for n in (10, 5000, 400_000):
+        # bytes drawn from the whole 0..255 range: alphabet, pos62/63, junk
+        raw = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        got, info = gdec(raw, *abc)
+        assert got == orc.decode(raw, *abc), (abc, n)
+        assert info.valid == int((table[np.frombuffer(raw, np.uint8)] >= 0).sum())
+
+
+def test_g1_g2_digests():
+    d = util.golden("digests.json")
+    g1 = genc(util.counting(1000001), ".", "_", True, "-")
+    assert hashlib.sha256(g1).hexdigest() == d["G1"]["out_sha256"]
+    g2 = genc(util.counting(1 << 20))
+    assert hashlib.sha256(g2).hexdigest() == d["G2"]["out_sha256"]
+
+
+@pytest.mark.slow
+def test_g3_1gib_roundtrip():
+    """BASELINE config 2 at full size: the recorded reference digest of the
+    1 GiB splitmix64 buffer, and decode(encode(x)) == x on the device."""
+    d = util.golden("digests.json")["G3"]
+    x = torch.empty(d["n"], dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, d["seed"])
+    assert hashlib.sha256(x.cpu().numpy()).hexdigest() == d["in_sha256"]
+    enc = b64.encode(x)
+    assert enc.numel() == d["out_len"]
+    assert hashlib.sha256(enc.cpu().numpy()).hexdigest() == d["out_sha256"]
+    dd = b64.decode(enc)
+    info = dd.info()
+    assert info.out_len == d["n"] and info.valid == d["out_len"] - 2
+    assert torch.equal(dd.out[: d["n"]], x)
+
+
+def _strided_check(nbuf, length, sample_idx, g4=None):
+    qstride_out = b64.encoded_len(length)
+    x = torch.empty(nbuf * length, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0x5EED)
+    enc = torch.empty(nbuf * qstride_out, dtype=torch.uint8, device=DEV)
+    b64.encode_strided(x, length, length, nbuf, enc, qstride_out)
+    host = x.cpu().numpy()
+    ehost = enc.cpu().numpy()
+    for i in sample_idx:
+        want = orc.encode(host[i * length:(i + 1) * length])
+        assert ehost[i * qstride_out:(i + 1) * qstride_out].tobytes() == want, i
+    if g4:
+        assert hashlib.sha256(ehost[:qstride_out].tobytes()).hexdigest().startswith(g4)
+    cap = b64.decoded_cap(qstride_out)
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(enc, qstride_out, qstride_out, nbuf, dec, cap, outlen)
+    assert int(outlen.min()) == length and int(outlen.max()) == length
+    assert torch.equal(dec.view(nbuf, cap)[:, :length], x.view(nbuf, length))
+
+
+def test_strided_small_shapes():
+    for nbuf, length in ((1, 1), (3, 2), (7, 3), (64, 12), (100, 1023), (33, 5000)):
+        _strided_check(nbuf, length, range(nbuf))
+
+
+@pytest.mark.slow
+def test_strided_cfg3_full():
+    """65,536 x 4 KiB (BASELINE config 3)."""
+    d = util.golden("digests.json")
+    _strided_check(65536, 4096, [0, 1, 2, 31337, 65535], d["G4_4096"]["out_sha256_prefix"])
+
+
+@pytest.mark.slow
+def test_strided_cfg4_full():
+    """1,048,576 x 1 KiB (BASELINE config 4, one GPU's worth)."""
+    d = util.golden("digests.json")
+    _strided_check(1 << 20, 1024, [0, 1, 777777, (1 << 20) - 1],
+                   d["G4_1024"]["out_sha256_prefix"])
+
+
+def test_ragged_batch_vs_oracle():
+    rng = np.random.default_rng(7)
+    lens = [0, 1, 2, 3, 4, 63, 64, 65, 1000, 4096, 12345, 70000] + \
+        list(rng.integers(0, 3000, 200))
+    host = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in lens]
+    in_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    elens = [b64.encoded_len(int(n)) for n in lens]
+    out_off = np.concatenate([[0], np.cumsum(elens)[:-1]]).astype(np.int64)
+    x = dev(np.concatenate(host))
+    enc = torch.zeros(int(sum(elens)) + 1, dtype=torch.uint8, device=DEV)
+    b64.encode_batch(x, torch.from_numpy(in_off).to(DEV), enc,
+                     torch.from_numpy(out_off).to(DEV))
+    eh = enc.cpu().numpy()
+    chunks = []
+    for i, h in enumerate(host):
+        got = eh[out_off[i]:out_off[i] + elens[i]].tobytes()
+        assert got == orc.encode(h), i
+        chunks.append(got)
+    # decode the same batch back, with junk in every third buffer
+    dchunks = [c if i % 3 else _junk(rng, c, 0.02) for i, c in enumerate(chunks)]
+    dlens = [len(c) for c in dchunks]
+    din_off = np.concatenate([[0], np.cumsum(dlens)]).astype(np.int64)
+    caps = [b64.decoded_cap(n) for n in dlens]
+    dout_off = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+    dec = torch.zeros(int(sum(caps)) + 1, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(len(lens), dtype=torch.int64, device=DEV)
+    b64.decode_batch(dev(b"".join(dchunks) or b"\0"), torch.from_numpy(din_off).to(DEV),
+                     dec, torch.from_numpy(dout_off).to(DEV), outlen)
+    dh = dec.cpu().numpy()
+    ol = outlen.cpu().numpy()
+    for i, h in enumerate(host):
+        assert ol[i] == len(h) and dh[dout_off[i]:dout_off[i] + ol[i]].tobytes() == h.tobytes()
+
+
+def test_fill_splitmix64():
+    d = util.golden("digests.json")
+    x = torch.empty(4099, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0x5EED)
+    assert np.array_equal(x.cpu().numpy(), util.splitmix64(0x5EED, 4099))
+    assert x[:16].cpu().numpy().tobytes().hex() == d["splitmix64_head"]["first16"]

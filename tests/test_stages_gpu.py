@@ -1,0 +1,58 @@
+"""The drop-in bytestream_1 stages (include/base64encoder.h,
+base64decoder.h) on the GPU, driven through the product's event loop by
+tests/csrc/stage_harness.c -- including the reference's own test topology
+(test/asynctest-base64encoder.c:123-151)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as orc
+from tests import util
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_topology_on_gpu_stages():
+    """1,000,001 counting bytes -> nice(113) -> GPU encoder('.', '_', '-')
+    -> nice(91) -> GPU decoder -> nice(97), read 200 at a time."""
+    d = util.golden("digests.json")["G1"]
+    res, err, eagains = util.stage_reftest(1000001)
+    assert err == 0 and res is not None
+    enc, dec = res
+    assert len(enc) == d["out_len"]
+    assert hashlib.sha256(enc).hexdigest() == d["out_sha256"]
+    assert dec == util.counting(1000001).tobytes()
+    assert eagains > 0  # the nicestreams did push back
+
+
+@pytest.mark.parametrize("read_size", [1, 3, 4, 5, 200, 4096, 1 << 20])
+@pytest.mark.parametrize("burst", [0, 113])
+def test_encoder_stage_any_read_size(read_size, burst):
+    """Same characters as the oracle for every read size -- including the
+    odd sizes the reference cannot serve (its assert, base64encoder.c:140)."""
+    rng = np.random.default_rng(read_size + burst)
+    for n, abc in ((0, (-1, -1, True, -1)), (1, (-1, -1, True, -1)),
+                   (2, (".", "_", True, "-")), (70001, (-1, -1, False, -1)),
+                   (300000, ("-", "_", True, "#"))):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        got, err = util.stage_encode(data, burst, read_size, *abc)
+        assert err == 0
+        assert got == orc.encode(data, *abc), (n, abc)
+
+
+@pytest.mark.parametrize("read_size", [1, 2, 3, 200, 65536])
+@pytest.mark.parametrize("burst", [0, 91])
+def test_decoder_stage_vs_oracle(read_size, burst):
+    rng = np.random.default_rng(read_size * 3 + burst)
+    for n in (0, 1, 2, 3, 1000, 250001):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        chars = orc.encode(data, pad=bool(n % 2))
+        dirty = b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76))
+        if n == 1000:
+            dirty = b"QQ==" + dirty + b"=QU"  # bits carried across '='
+        got, err = util.stage_decode(dirty, burst, read_size)
+        assert err == 0
+        assert got == orc.decode_stream(dirty, 0, 0, 200), n
+        if n not in (1000,):
+            assert got == data

@@ -1,0 +1,109 @@
+"""Shared test helpers (test infrastructure only)."""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+HARNESS = os.path.join(ROOT, "tests", "csrc", "libstage_harness.so")
+
+
+def golden(name: str):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def splitmix64(seed: int, n: int) -> np.ndarray:
+    """The synthetic byte stream of SURVEY.md §8(c) (numpy, vectorised)."""
+    n8 = (n + 7) // 8
+    with np.errstate(over="ignore"):
+        i = np.arange(1, n8 + 1, dtype=np.uint64)
+        z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").view(np.uint8)[:n]
+
+
+def counting(n: int) -> np.ndarray:
+    return (np.arange(n, dtype=np.uint64) & 0xFF).astype(np.uint8)
+
+
+_harness = None
+
+
+def harness() -> ctypes.CDLL:
+    """tests/csrc/libstage_harness.so (links the product library)."""
+    global _harness
+    if _harness is None:
+        try:
+            import torch  # noqa: F401  (one HIP runtime: see async_amd/_lib.py)
+        except ImportError:
+            pass
+        L = ctypes.CDLL(HARNESS)
+        sz, ssz, vp, ch, ip = (ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p,
+                               ctypes.c_char, ctypes.POINTER(ctypes.c_int))
+        L.h_reftest.argtypes = [sz, vp, sz, ctypes.POINTER(sz), vp, sz, ip,
+                                ctypes.POINTER(sz)]
+        L.h_reftest.restype = ssz
+        L.h_encode_stream.argtypes = [vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
+        L.h_encode_stream.restype = ssz
+        L.h_decode_stream.argtypes = [vp, sz, sz, sz, ch, ch, vp, sz, ip]
+        L.h_decode_stream.restype = ssz
+        L.h_copy_stream.argtypes = [vp, sz, sz, sz, vp, sz, ip, ctypes.POINTER(sz)]
+        L.h_copy_stream.restype = ssz
+        _harness = L
+    return _harness
+
+
+def cch(v) -> bytes:
+    if isinstance(v, str):
+        v = v.encode("latin-1")
+    if isinstance(v, (bytes, bytearray)):
+        return bytes(v[:1])
+    return bytes([v & 0xFF])
+
+
+def _buf(data: bytes):
+    a = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    return a, a.ctypes.data
+
+
+def stage_encode(data: bytes, burst=0, read_size=200, pos62=-1, pos63=-1, pad=True,
+                 padchar=-1):
+    """Product encoder stage on the product loop; returns (bytes|None, errno)."""
+    a, p = _buf(data)
+    cap = (len(data) + 2) // 3 * 4 + 16
+    out = np.empty(cap, np.uint8)
+    err = ctypes.c_int(0)
+    n = harness().h_encode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
+                                  int(bool(pad)), cch(padchar), out.ctypes.data, cap,
+                                  ctypes.byref(err))
+    return (None if n < 0 else out[:n].tobytes()), err.value
+
+
+def stage_decode(data: bytes, burst=0, read_size=200, pos62=-1, pos63=-1):
+    a, p = _buf(data)
+    cap = (len(data) + 3) // 4 * 3 + 16
+    out = np.empty(cap, np.uint8)
+    err = ctypes.c_int(0)
+    n = harness().h_decode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
+                                  out.ctypes.data, cap, ctypes.byref(err))
+    return (None if n < 0 else out[:n].tobytes()), err.value
+
+
+def stage_reftest(length=1000001):
+    ecap = (length + 2) // 3 * 4 + 16
+    enc = np.empty(ecap, np.uint8)
+    dec = np.empty(length + 16, np.uint8)
+    elen = ctypes.c_size_t(0)
+    err = ctypes.c_int(0)
+    eag = ctypes.c_size_t(0)
+    n = harness().h_reftest(length, enc.ctypes.data, ecap, ctypes.byref(elen),
+                            dec.ctypes.data, dec.size, ctypes.byref(err), ctypes.byref(eag))
+    return (None if n < 0 else (enc[: elen.value].tobytes(), dec[:n].tobytes())), \
+        err.value, eag.value
