@@ -83,9 +83,8 @@ class Decoded:
     result: torch.Tensor       # 24-byte b64x_dec_result on the device
 
     def info(self) -> DecResult:
-        r = DecResult()
-        ctypes.memmove(ctypes.addressof(r), self.result.cpu().numpy().ctypes.data, 24)
-        return r
+        host = self.result[:24].cpu().numpy()  # keep alive across the copy
+        return DecResult.from_buffer_copy(host.tobytes())
 
     def bytes(self) -> torch.Tensor:
         """The decoded bytes (synchronises to read the length)."""

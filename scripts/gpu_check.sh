@@ -3,15 +3,16 @@
 # Every GPU step has its own time limit; a crash/abort/timeout (exit code
 # other than 0 or 1) ends the script -- nothing more runs on the GPU.
 # Usage: scripts/gpu_check.sh [pytest -k expr] [bench args...]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
 mkdir -p gpurun_out
 K="${1:-not slow}"; shift || true
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   echo "== $name ($(date +%T))"
-  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$lim" "$@" > "$ROOT/gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  echo "== $name rc=$rc"; tail -n 25 "$ROOT/gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
@@ -20,5 +21,5 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 1200 python -m pytest tests -q -m gpu -k "$K" --timeout 600 -p no:cacheprovider
 step bench 600 python bench.py --steps 20 --warmup 3 "$@"
 cd /tmp && export TMPDIR=/tmp
-step rocprof 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu
+step rocprof 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu
 echo ALLDONE
