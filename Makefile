@@ -20,6 +20,9 @@ HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC 
 CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
 
 LIB      = async_amd/libasync_b64.so
+# Stages + kernels only (no event loop/streams): the drop-in for a build of
+# the reference library, which supplies async_wound() and the streams.
+CORE     = async_amd/libasync_b64_core.so
 ORACLE   = oracle/liboracle.so
 HARNESS  = tests/csrc/libstage_harness.so
 OBJDIR   = build
@@ -30,7 +33,7 @@ HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
 
-all: $(LIB) $(ORACLE) $(HARNESS)
+all: $(LIB) $(CORE) $(ORACLE) $(HARNESS)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -44,6 +47,9 @@ $(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) | $(OBJDIR)
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
 
+$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_stages.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64_core.so
+
 $(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h
 	$(CC) -O2 -std=c11 -fPIC -Wall -Wextra -shared -o $@ oracle/b64_oracle.c
 
@@ -52,6 +58,6 @@ $(HARNESS): tests/csrc/stage_harness.c $(LIB) $(HEADERS)
 	    -Lasync_amd -lasync_b64 -Wl,-rpath,'$$ORIGIN/../../async_amd'
 
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(ORACLE) $(HARNESS)
+	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS)
 
 .PHONY: all clean

@@ -107,8 +107,8 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
         raise ValueError("output too small")
     if result is None:
         result = torch.zeros(24, dtype=torch.uint8, device=x.device)
-    if workspace is None:
-        workspace = torch.empty(workspace_size(n), dtype=torch.uint8, device=x.device)
+    if workspace is None:  # must start zeroed; the library keeps it re-armed
+        workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
     _lib.check("b64x_decode_dev", lib.b64x_decode_dev(
         _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a),
         HOLD_TAIL if hold_tail else 0, _ptr(workspace), _stream(stream)))

@@ -54,8 +54,8 @@ constexpr int kThreads = 256;  // 4 waves of 64
 constexpr int kWavesPerBlock = kThreads / 64;
 constexpr int kChunk = 1024;            // characters per wave step
 constexpr int kSxBytes = 1088;          // per-wave sextet scratch in LDS
-constexpr uint32_t kMaxRanges = 8192;   // decode ranges (waves) per call
-constexpr uint64_t kMinRange = 4096;    // characters per range, at least
+constexpr uint32_t kMaxRanges = 1u << 20; // decode ranges (waves) per call
+constexpr uint64_t kRangeChunks = 2;    // default decode range: 2 KiB
 constexpr int kEncUnroll = 4;           // quads in flight per lane
 constexpr int kDecUnroll = 4;           // chunks in flight per wave
 
@@ -107,6 +107,78 @@ DEV void build_dec_table(uint8_t *tab, const DecAlpha &a)
 {
     for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x)
         tab[c] = (uint8_t) dec_value(c, a);
+}
+
+// ------------------------------------------------------- memory helpers --
+
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+// Store the first `nbytes` (0..12) bytes of {o0, o1, o2}: whole dwords when
+// `p` is dword aligned, then at most 3 single bytes.
+DEV void store_bytes12(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2,
+                       uint32_t nbytes)
+{
+    if ((((uintptr_t) p) & 3) == 0) {
+        const uint32_t nd = nbytes >> 2;
+        if (nd == 3) {
+            *(u32x3a4 *) p = u32x3a4{o0, o1, o2};
+            return;
+        }
+        if (nd == 2) *(u32x2a4 *) p = u32x2a4{o0, o1};
+        else if (nd == 1) *(uint32_t *) p = o0;
+        const uint32_t rem = nbytes & 3;
+        if (rem) {
+            const uint32_t w = nd == 0 ? o0 : nd == 1 ? o1 : o2;
+            uint8_t *q = p + 4 * nd;
+            q[0] = (uint8_t) w;
+            if (rem > 1) q[1] = (uint8_t) (w >> 8);
+            if (rem > 2) q[2] = (uint8_t) (w >> 16);
+        }
+        return;
+    }
+    uint32_t w[3] = {o0, o1, o2};
+#pragma unroll
+    for (uint32_t i = 0; i < 12; i++)
+        if (i < nbytes) p[i] = (uint8_t) (w[i >> 2] >> (8 * (i & 3)));
+}
+
+// Same for up to 16 bytes.
+DEV void store_bytes16(uint8_t *p, const uint32_t w[4], uint32_t nbytes)
+{
+    if (nbytes == 16 && (((uintptr_t) p) & 3) == 0) {
+        *(u32x4a4 *) p = u32x4a4{w[0], w[1], w[2], w[3]};
+        return;
+    }
+    if (nbytes > 12) {
+        store_bytes12(p, w[0], w[1], w[2], 12);
+        store_bytes12(p + 12, w[3], 0, 0, nbytes - 12);
+    } else {
+        store_bytes12(p, w[0], w[1], w[2], nbytes);
+    }
+}
+
+// True when the 16 bytes at p lie in one 4 KiB page.  A load of them is
+// then safe as soon as one of them belongs to a live buffer: memory is
+// mapped page-wise, so a window that shares a page with an in-range byte
+// cannot fault.  The extra bytes are never used (callers mask by count).
+DEV bool same_page16(const uint8_t *p)
+{
+    return (((uintptr_t) p) & 4095) <= 4096 - 16;
+}
+
+// Up to 16 characters at `p`, `nin` (>= 1) of which are inside the range;
+// the others are unspecified (callers mask them out by position).
+DEV uint4 load_chars(const uint8_t *p, uint32_t nin)
+{
+    if ((((uintptr_t) p) & 3) == 0 && (nin == 16 || same_page16(p))) {
+        u32x4a4 v = *(const u32x4a4 *) p;
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+        if (i < nin) w[i >> 2] |= (uint32_t) p[i] << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ----------------------------------------------------------- encode core --
@@ -166,6 +238,51 @@ DEV uint32_t enc_bytes(const uint8_t *tab, const uint8_t *src, uint32_t r,
         }
     }
     return o;
+}
+
+// The final r (1..11) bytes of a buffer at a dword-aligned `src`: loaded as
+// one 12-byte window when it stays in the page of its first byte (else
+// bytewise), encoded like a quad with the missing bytes zeroed, the partial
+// group's padding (finalize(), src/base64encoder.c:61-99) merged in, and
+// stored as whole dwords plus at most 3 bytes.
+DEV void enc_tail(const uint8_t *tab, const uint8_t *src, uint32_t r, uint8_t *dst,
+                  const EncAlpha &a)
+{
+    uint32_t x, y, z;
+    if ((((uintptr_t) src) & 4095) <= 4096 - 12) {
+        u32x3a4 v = *(const u32x3a4 *) src;
+        x = v.x;
+        y = v.y;
+        z = v.z;
+    } else {
+        uint32_t w[3] = {0, 0, 0};
+        for (uint32_t i = 0; i < r; i++) w[i >> 2] |= (uint32_t) src[i] << (8 * (i & 3));
+        x = w[0];
+        y = w[1];
+        z = w[2];
+    }
+    // zero the bytes at and past r
+    x &= r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1;
+    y &= r >= 8 ? 0xFFFFFFFFu : r <= 4 ? 0u : (1u << (8 * (r - 4))) - 1;
+    z &= r <= 8 ? 0u : (1u << (8 * (r - 8))) - 1;
+    const uint4 o = enc_quad(tab, x, y, z);
+    uint32_t dw[4] = {o.x, o.y, o.z, o.w};
+    const uint32_t ng = r / 3, rem = r % 3;
+    uint32_t m = 4 * ng;
+    if (rem) {
+        const uint32_t keep = rem + 1;  // characters of the partial group
+        if (a.pad) {
+            const uint32_t mask = keep == 2 ? 0xFFFFu : 0xFFFFFFu;
+            const uint32_t pads = a.padc * 0x01010101u;
+#pragma unroll
+            for (uint32_t g = 0; g < 4; g++)
+                if (g == ng) dw[g] = (dw[g] & mask) | (pads & ~mask);
+            m += 4;
+        } else {
+            m += keep;
+        }
+    }
+    store_bytes16(dst, dw, m);
 }
 
 // Encode one quad slot: full 12-byte quads with dword-aligned source and
@@ -252,6 +369,173 @@ __global__ __launch_bounds__(kThreads) void k_encode(
     }
 }
 
+// Runtime tuning knobs (scripts/bench_variants.py; not part of the public
+// ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant.
+int g_tune[4] = {0, 0, 0, 0};
+
+template <bool NT>
+DEV void store16(uint8_t *p, uint4 o)
+{
+    if (NT) {
+        __builtin_nontemporal_store(u32x4a4{o.x, o.y, o.z, o.w}, (u32x4a4 *) p);
+    } else {
+        *(u32x4a4 *) p = u32x4a4{o.x, o.y, o.z, o.w};
+    }
+}
+
+// One dword-aligned device buffer (the BASELINE config-2 hot path).  The
+// n/12 full quads form tiles of U quads per lane (U x 768 B in per wave);
+// blocks take whole tiles grid-stride with no per-lane guards, so loads
+// and stores are never exec-masked and the compiler can wait on loads with
+// counted vmcnt instead of draining the stores (vmcnt counts both).  With
+// PIPE the next tile's loads are issued before this tile's compute; LNT/NT
+// make loads/stores non-temporal.  Launched with one block per tile (a
+// non-persistent grid streams fastest here: tests/tools/copy_sweep.hip).  The
+// last, partial tile and the final n mod 12 bytes (with padding) are done
+// by the last block.
+template <bool NT>
+DEV u32x3a4 ld12(const uint8_t *p)
+{
+    if (NT) return __builtin_nontemporal_load((const u32x3a4 *) p);
+    return *(const u32x3a4 *) p;
+}
+
+template <int U, bool PIPE, bool LNT, bool NT>
+__global__ __launch_bounds__(kThreads) void k_encode_flat(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
+{
+    __shared__ uint8_t tab[64];
+    build_enc_table(tab, a);
+    __syncthreads();
+    const uint64_t nq = n / 12;
+    const uint64_t tile = (uint64_t) kThreads * U;
+    const uint64_t full = nq / tile;
+    const uint32_t tid = threadIdx.x;
+    uint64_t t = blockIdx.x;
+    if (t < full) {
+        u32x3a4 cur[U];
+        const uint8_t *src = in + (t * tile + tid) * 12;
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = ld12<LNT>(src + u * kThreads * 12);
+        for (;;) {
+            const uint64_t tn = t + gridDim.x;
+            u32x3a4 nxt[U];
+            if (PIPE) {
+                // unconditional (re-reads this tile on the last trip) so
+                // the compute below waits on exactly the older loads
+                const uint64_t tl = tn < full ? tn : t;
+                const uint8_t *nsrc = in + (tl * tile + tid) * 12;
+#pragma unroll
+                for (int u = 0; u < U; u++) nxt[u] = ld12<LNT>(nsrc + u * kThreads * 12);
+            }
+            uint8_t *dst = out + (t * tile + tid) * 16;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                store16<NT>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
+            if (tn >= full) break;
+            t = tn;
+            const uint8_t *src2 = in + (t * tile + tid) * 12;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                cur[u] = PIPE ? nxt[u] : ld12<LNT>(src2 + u * kThreads * 12);
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        for (uint64_t q = full * tile + tid; q < nq; q += kThreads)
+            store16<NT>(out + q * 16, enc_quad(tab, ((const u32x3a4 *) (in + q * 12))->x,
+                                                ((const u32x3a4 *) (in + q * 12))->y,
+                                                ((const u32x3a4 *) (in + q * 12))->z));
+        if (tid == 0 && n % 12)
+            enc_bytes(tab, in + nq * 12, (uint32_t) (n % 12), out + nq * 16, true, a);
+    }
+}
+
+// Calibration probe: a pure stream with a kernel's access widths --
+// RD bytes loaded and WR bytes stored per lane per slot (12 or 16), U slots
+// per lane per tile, whole tiles grid-stride -- to measure the HBM rate the
+// same traffic shape reaches without any base64 work.
+template <int RD, int WR, bool NT>
+__global__ __launch_bounds__(kThreads) void k_copy_probe(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t slots)
+{
+    constexpr int U = 4;
+    const uint64_t tile = (uint64_t) kThreads * U;
+    const uint64_t full = slots / tile;
+    for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
+        const uint64_t s0 = t * tile + threadIdx.x;
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint8_t *p = in + (s0 + u * kThreads) * RD;
+            if (RD == 16) {
+                v[u] = *(const uint4 *) p;
+            } else {
+                u32x3a4 x = *(const u32x3a4 *) p;
+                v[u] = make_uint4(x.x, x.y, x.z, x.x ^ x.y);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint8_t *q = out + (s0 + u * kThreads) * WR;
+            if (WR == 16) {
+                store16<NT>(q, v[u]);
+            } else if (NT) {
+                __builtin_nontemporal_store(u32x3a4{v[u].x, v[u].y, v[u].z ^ v[u].w}, (u32x3a4 *) q);
+            } else {
+                *(u32x3a4 *) q = u32x3a4{v[u].x, v[u].y, v[u].z ^ v[u].w};
+            }
+        }
+    }
+}
+
+// Uniform-stride batch encode: slot t = (buffer t / Q, quad t mod Q), Q =
+// quads per buffer; one tile of U slots per lane per block (non-persistent
+// grid), non-temporal loads and stores on whole, dword-aligned quads, the
+// buffer tails (and misaligned buffers) bytewise.
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_encode_strided(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
+    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
+    uint32_t qpb, uint32_t total_slots, EncAlpha a)
+{
+    __shared__ uint8_t tab[64];
+    build_enc_table(tab, a);
+    __syncthreads();
+    u32x3a4 v[U];
+    const uint8_t *srcs[U];
+    uint8_t *dsts[U];
+    uint64_t avails[U];
+    bool fast[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t t = (blockIdx.x * U + u) * kThreads + threadIdx.x;
+        fast[u] = false;
+        avails[u] = 0;
+        srcs[u] = in;
+        dsts[u] = out;
+        if (t < total_slots) {
+            const uint32_t b = t / qpb, q = t - b * qpb;
+            srcs[u] = in + (uint64_t) b * in_stride + (uint64_t) q * 12;
+            dsts[u] = out + (uint64_t) b * out_stride + (uint64_t) q * 16;
+            avails[u] = len - (uint64_t) q * 12;
+            fast[u] = avails[u] >= 12 && ((((uintptr_t) srcs[u]) | ((uintptr_t) dsts[u])) & 3) == 0;
+            if (fast[u]) v[u] = ld12<true>(srcs[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        if (fast[u]) {
+            store16<true>(dsts[u], enc_quad(tab, v[u].x, v[u].y, v[u].z));
+        } else if (avails[u]) {
+            const uint32_t r = avails[u] < 12 ? (uint32_t) avails[u] : 12;
+            if (avails[u] < 12 && (((uintptr_t) srcs[u]) & 3) == 0)
+                enc_tail(tab, srcs[u], r, dsts[u], a);
+            else
+                enc_bytes(tab, srcs[u], r, dsts[u], avails[u] <= 12, a);
+        }
+    }
+}
+
 // Ragged batch: one block per buffer.
 __global__ __launch_bounds__(kThreads) void k_encode_ragged(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
@@ -320,54 +604,65 @@ DEV void groups_to_bytes(uint32_t G0, uint32_t G1, uint32_t G2, uint32_t G3,
     o2 = __builtin_amdgcn_perm(G3, G2, 0x04050600u);  // G2.b0 G3.b2 G3.b1 G3.b0
 }
 
-DEV void store_bytes12(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2,
-                       uint32_t nbytes)
+// Hot-path mapping: 16 table lookups folded straight into the four 24-bit
+// groups of the lane (3 v_lshl_or per group) plus an OR accumulator;
+// `bad` is nonzero unless all 16 characters are present and in the
+// alphabet (then G is exact).
+DEV void map_fast(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t G[4], uint32_t &bad)
 {
-    if (nbytes == 12 && (((uintptr_t) p) & 3) == 0) {
-        *(u32x3a4 *) p = u32x3a4{o0, o1, o2};
-        return;
-    }
-    uint32_t w[3] = {o0, o1, o2};
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+    uint32_t acc = nin < 16 ? 0x80u : 0u;
 #pragma unroll
-    for (uint32_t i = 0; i < 12; i++)
-        if (i < nbytes) p[i] = (uint8_t) (w[i >> 2] >> (8 * (i & 3)));
+    for (int g = 0; g < 4; g++) {
+        uint32_t t0 = tab[dw[g] & 0xFFu];
+        uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
+        uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
+        uint32_t t3 = tab[dw[g] >> 24];
+        G[g] = (t0 << 18) | (t1 << 12) | (t2 << 6) | t3;
+        acc |= t0 | t1 | t2 | t3;
+    }
+    bad = acc & ~63u;
 }
 
-// Up to 16 characters at `p`, `nin` of which are inside the range.
-// Missing characters read as 0, which is never in the alphabet; callers
-// mask them out by position anyway.
-DEV uint4 load_chars(const uint8_t *p, uint32_t nin)
+// Slow-path view of a lane's 16 characters: groups with every absent or
+// non-alphabet character's sextet zeroed, and the alphabet bit mask.
+DEV uint4 load16_a4(const uint8_t *p)
 {
-    if (nin == 16) {
-        if ((((uintptr_t) p) & 15) == 0) return *(const uint4 *) p;
-        if ((((uintptr_t) p) & 3) == 0) {
-            u32x4a4 v = *(const u32x4a4 *) p;
-            return make_uint4(v.x, v.y, v.z, v.w);
-        }
-    }
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t i = 0; i < 16; i++)
-        if (i < nin) w[i >> 2] |= (uint32_t) p[i] << (8 * (i & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    u32x4a4 v = *(const u32x4a4 *) p;
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 struct LaneChunk {
-    uint32_t t[16];  // table values (0..63, or 0xFF)
+    uint32_t G[4];
     uint32_t vmask;  // bit k: character k present and in the alphabet
 };
 
-DEV void map_chunk(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
+DEV void map_chunk(const uint8_t *tab_, uint4 w, uint32_t nin, LaneChunk &lc)
 {
+    // Re-read the table (volatile): sharing the hot path's lookups would keep
+    // all 16 per-character values of every in-flight chunk alive.
+    const volatile uint8_t *tab = tab_;
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
     uint32_t m = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        uint32_t c = (dw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-        lc.t[k] = tab[c];
-        m |= (lc.t[k] < 64u ? 1u : 0u) << k;
+    for (int g = 0; g < 4; g++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = 4 * g + j;
+            uint32_t t = tab[(dw[g] >> (8 * j)) & 0xFFu];
+            bool ok = t < 64u && (uint32_t) k < nin;
+            v |= (ok ? t : 0u) << (18 - 6 * j);
+            m |= (ok ? 1u : 0u) << k;
+        }
+        lc.G[g] = v;
     }
-    lc.vmask = m & (nin >= 16 ? 0xFFFFu : ((1u << nin) - 1u));
+    lc.vmask = m;
+}
+
+DEV uint32_t sextet(const LaneChunk &lc, int k)
+{
+    return (lc.G[k >> 2] >> (18 - 6 * (k & 3))) & 63u;
 }
 
 struct RangeState {
@@ -386,7 +681,7 @@ DEV void exact_chunk(uint8_t *sx, uint8_t *out, const LaneChunk &lc, RangeState 
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         if ((lc.vmask >> k) & 1u) {
-            if (idx >= 0) sx[idx] = (uint8_t) lc.t[k];
+            if (idx >= 0) sx[idx] = (uint8_t) sextet(lc, k);
             idx++;
         }
     }
@@ -430,20 +725,73 @@ DEV void emit_partial(uint8_t *sx, uint8_t *dst, int r)
     }
 }
 
-// Decode characters [rb, re) of the stream in[0..n).  The first `skip`
-// (0..3) alphabet characters complete a group owned by the previous range
-// and are not emitted here.  `out` receives this range's first owned
-// group.  If the range is not the last, the final group is completed with
-// up to 3 alphabet characters read past `re` (lookahead).  With `hold`
-// the stream's final incomplete group is not emitted.
-// Returns the number of alphabet characters in [rb, re).
+// Fast path (a): a lane's 16 alphabet characters, as 4 groups, to 12 bytes.
+DEV void emit_full(const uint32_t G[4], uint8_t *out)
+{
+    uint32_t o0, o1, o2;
+    groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+    store_bytes12(out + 12 * lane_id(), o0, o1, o2, 12);
+}
+
+// Hot-path form: `out` is known dword aligned (checked once, uniformly, by
+// the caller), so the store is one unmasked dwordx3.
+template <bool NT>
+DEV void emit_full_a4(const uint32_t G[4], uint8_t *out)
+{
+    uint32_t o0, o1, o2;
+    groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+    u32x3a4 *p = (u32x3a4 *) (out + 12 * lane_id());
+    if (NT)
+        __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, p);
+    else
+        *p = u32x3a4{o0, o1, o2};
+}
+
+// Fast path (b), for the stream's final chunk when it starts on a group
+// boundary: if its alphabet characters form a prefix -- lanes 0..f-1 full,
+// lane f a prefix of its 16, no alphabet character after that (the shape
+// of every padded or unaligned stream end) -- emit them, lane f including
+// the final partial group (floor(6r/8) bytes, src/base64decoder.c:71-76)
+// unless `hold`.  Returns the characters consumed, or -1 if the shape does
+// not apply.  Wave-uniform.
+DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t m = lc.vmask;
+    if (!__all((m & (m + 1)) == 0)) return -1;
+    const uint64_t F = __ballot(m == 0xFFFFu);
+    const uint64_t NZ = __ballot(m != 0);
+    const uint32_t f = __popcll(F);
+    if (f == 64) {
+        emit_full(lc.G, out);
+        return kChunk;
+    }
+    if (F != ((1ull << f) - 1)) return -1;
+    if (f < 63 && (NZ >> (f + 1))) return -1;
+    const uint32_t k = __popc(m);
+    const uint32_t nbytes = 3 * (k >> 2) + (hold ? 0u : (6 * (k & 3)) >> 3);
+    if (nbytes) {
+        uint32_t o0, o1, o2;
+        groups_to_bytes(lc.G[0], lc.G[1], lc.G[2], lc.G[3], o0, o1, o2);
+        store_bytes12(out + 12 * lane, o0, o1, o2, nbytes);
+    }
+    return (int) (16 * f + __shfl(k, (int) f, 64));
+}
+
+// Exact decode of characters [start, re) of the stream in[0..n).  The
+// first `skip` (0..3) alphabet characters complete a group owned by an
+// earlier range and are not emitted.  `out` receives the first group owned
+// here.  Unless `is_last`, the final group is completed with up to 3
+// alphabet characters read past `re` (lookahead).  With `hold` the
+// stream's final incomplete group is not emitted.
+// Returns the number of alphabet characters in [start, re).
 DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
-                          uint64_t n, uint64_t rb, uint64_t re, int skip,
+                          uint64_t n, uint64_t start, uint64_t re, int skip,
                           uint8_t *out, bool is_last, bool hold)
 {
     const uint32_t lane = lane_id();
     RangeState st{-skip, 0, 0};
-    for (uint64_t pos = rb; pos < re; pos += (uint64_t) kChunk * kDecUnroll) {
+    for (uint64_t pos = start; pos < re; pos += (uint64_t) kChunk * kDecUnroll) {
         uint4 w[kDecUnroll];
         uint32_t nin[kDecUnroll];
 #pragma unroll
@@ -456,23 +804,26 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
         for (int u = 0; u < kDecUnroll; u++) {
             const uint64_t cpos = pos + (uint64_t) u * kChunk;
             if (cpos >= re) break;
+            if (st.carry == 0) {
+                uint32_t G[4], bad;
+                map_fast(tab, w[u], nin[u], G, bad);
+                if (__all(bad == 0)) {
+                    emit_full(G, out + 3 * st.groups);
+                    st.groups += kChunk / 4;
+                    st.valid += kChunk;
+                    continue;
+                }
+            }
             LaneChunk lc;
             map_chunk(tab, w[u], nin[u], lc);
-            if (st.carry == 0 && __all(lc.vmask == 0xFFFFu)) {
-                // Fast path: 1024 alphabet characters, group aligned.
-                uint32_t G[4];
-#pragma unroll
-                for (int g = 0; g < 4; g++)
-                    G[g] = (lc.t[4 * g] << 18) | (lc.t[4 * g + 1] << 12) |
-                           (lc.t[4 * g + 2] << 6) | lc.t[4 * g + 3];
-                uint32_t o0, o1, o2;
-                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-                store_bytes12(out + 3 * st.groups + 12 * lane, o0, o1, o2, 12);
-                st.groups += kChunk / 4;
-                st.valid += kChunk;
-            } else {
-                exact_chunk(sx, out, lc, st);
+            if (st.carry == 0 && is_last && cpos + kChunk >= re) {
+                int got = fast_prefix(lc, hold, out + 3 * st.groups);
+                if (got >= 0) {
+                    st.valid += (uint32_t) got;
+                    continue;  // the stream ends here
+                }
             }
+            exact_chunk(sx, out, lc, st);
         }
     }
     int r = st.carry;
@@ -507,168 +858,478 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
     return st.valid;
 }
 
+// Decode workspace: b64x_decode_workspace_size() bytes, zero-filled before
+// its first use; every call leaves it re-armed for the next.
+//   fd      ~((range << 32) | offset) of the first chunk pass 1 could not
+//           take on a fast path, combined with atomicMax over the waves that
+//           hit one; 0 = none.  The scan moves it to fd_cur and zeroes it.
+//   counts  alphabet characters per range (pass 1, every range)
+//   bases   exclusive prefix of counts (scan, dirty calls only)
 struct DecodeWs {
-    uint32_t *counts;  // [kMaxRanges] valid characters per range
-    uint64_t *bases;   // [kMaxRanges] exclusive prefix of counts
-    uint32_t *first_dirty;
+    uint64_t *fd;
+    uint64_t *fd_cur;
+    uint32_t *counts;
+    uint64_t *bases;
 };
 
 DEV DecodeWs ws_view(void *ws)
 {
     DecodeWs w;
-    w.counts = (uint32_t *) ws;
-    w.bases = (uint64_t *) ((uint8_t *) ws + kMaxRanges * sizeof(uint32_t));
-    w.first_dirty = (uint32_t *) ((uint8_t *) ws + kMaxRanges * 12);
+    uint8_t *p = (uint8_t *) ws;
+    w.fd = (uint64_t *) p;
+    w.fd_cur = (uint64_t *) (p + 8);
+    w.counts = (uint32_t *) (p + 64);
+    w.bases = (uint64_t *) (p + 64 + (uint64_t) kMaxRanges * 4);
     return w;
 }
 
-// Pass 1: every range assumes all earlier ranges were all-alphabet.
+DEV uint32_t wave_sum(uint32_t x)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+template <bool NT>
+DEV uint4 ld16(const uint8_t *p)
+{
+    if (NT) {
+        u32x4a4 v = __builtin_nontemporal_load((const u32x4a4 *) p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return load16_a4(p);
+}
+
+constexpr uint32_t kNoDirty = 0xFFFFFFFFu;
+
+// Pass 1 (fast paths only), one wave per range; each range assumes every
+// earlier range was all alphabet.  The hot loop takes groups of U full
+// chunks while every chunk is all alphabet (no per-lane guards, scalar loop
+// control; NT = non-temporal loads and stores, the policy that lets a plain
+// stream reach ~6.3 TB/s on this part).  The first exception drops to a
+// one-chunk loop that still emits fast-path chunks until one does not fit;
+// that chunk is published (atomicMax of the complemented (range, offset))
+// and the range only counts from then on.
+template <int U, bool PIPE, bool NT>
 __global__ __launch_bounds__(kThreads) void k_decode_pass1(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
 {
-    __shared__ DecSmem sm;
-    build_dec_table(sm.tab, a);
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
     __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t r = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t lane = lane_id();
+    // wave-uniform, and provably so (scalar loop control, no exec masking)
+    const uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (r >= nranges) return;
     const uint64_t rb = (uint64_t) r * R;
     const uint64_t re = rb + R < n ? rb + R : n;
-    uint64_t v = decode_range(sm.tab, sm.sx[wv], in, n, rb, re, 0,
-                              out + rb / 4 * 3, r + 1 == nranges, hold != 0);
-    if (lane_id() == 0) ws_view(ws).counts[r] = (uint32_t) v;
+    const bool last = r + 1 == nranges;
+    uint8_t *o = out + rb / 4 * 3;
+    uint32_t cnt = 0;  // per lane; summed over the wave at the end
+    uint64_t pos = rb;
+    const uint64_t hot_end = re - (re - rb) % ((uint64_t) kChunk * U);
+    if (((((uintptr_t) in) | ((uintptr_t) o)) & 3) == 0 && pos < hot_end) {
+        uint4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            cur[u] = ld16<NT>(in + pos + (uint64_t) u * kChunk + 16 * lane);
+        for (;;) {
+            const uint64_t np = pos + (uint64_t) kChunk * U;
+            uint4 nxt[U];
+            if (PIPE) {
+                const uint64_t lp = np < hot_end ? np : pos;  // unconditional load
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    nxt[u] = ld16<NT>(in + lp + (uint64_t) u * kChunk + 16 * lane);
+            }
+            int u = 0;
+#pragma unroll
+            for (; u < U; u++) {
+                uint32_t G[4], bad;
+                map_fast(tab, cur[u], 16, G, bad);
+                if (!__all(bad == 0)) break;
+                emit_full_a4<NT>(G, o + (pos + (uint64_t) u * kChunk - rb) / 4 * 3);
+            }
+            cnt += 16 * u;
+            if (u < U) {
+                pos += (uint64_t) u * kChunk;
+                break;
+            }
+            pos = np;
+            if (pos >= hot_end) break;
+#pragma unroll
+            for (int v = 0; v < U; v++)
+                cur[v] = PIPE ? nxt[v] : ld16<NT>(in + pos + (uint64_t) v * kChunk + 16 * lane);
+        }
+    }
+    uint32_t dirty = kNoDirty;
+    for (; pos < re; pos += kChunk) {
+        const uint64_t p = pos + 16 * lane;
+        const uint32_t nin = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+        const uint4 w = nin ? load_chars(in + p, nin) : make_uint4(0, 0, 0, 0);
+        if (dirty == kNoDirty) {
+            uint32_t G[4], bad;
+            map_fast(tab, w, nin, G, bad);
+            if (__all(bad == 0)) {
+                cnt += 16;
+                emit_full(G, o + (pos - rb) / 4 * 3);
+                continue;
+            }
+        }
+        LaneChunk lc;
+        map_chunk(tab, w, nin, lc);
+        cnt += __popc(lc.vmask);
+        if (dirty == kNoDirty) {
+            const bool final = last && pos + kChunk >= re;
+            if (!final || fast_prefix(lc, hold != 0, o + (pos - rb) / 4 * 3) < 0)
+                dirty = (uint32_t) (pos - rb);
+        }
+    }
+    cnt = wave_sum(cnt);
+    if (lane == 0) {
+        DecodeWs v = ws_view(ws);
+        v.counts[r] = cnt;
+        if (dirty != kNoDirty)
+            atomicMax((unsigned long long *) v.fd,
+                      (unsigned long long) ~(((uint64_t) r << 32) | dirty));
+    }
 }
 
-// One block: find the first range whose valid count fell short of its
-// length, prefix-sum the counts, fill the result, and collect the stream's
-// last V mod 4 sextets (for B64X_DEC_HOLD_TAIL callers).
+// One block: take (and re-arm) the first-dirty record, compute V and the
+// result record; on a dirty call also the true base of every range from
+// the first dirty one on.  Then the stream's last V mod 4 sextets (for
+// B64X_DEC_HOLD_TAIL callers), scanning backwards.
 __global__ __launch_bounds__(1024) void k_decode_scan(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
     DecAlpha a, void *ws, b64x_dec_result *res, uint32_t hold)
 {
     __shared__ uint8_t tab[256];
-    __shared__ uint64_t part[1024];
-    __shared__ uint32_t first_dirty;
+    __shared__ uint64_t wtot[16];
     build_dec_table(tab, a);
-    if (threadIdx.x == 0) first_dirty = nranges;
-    __syncthreads();
     DecodeWs w = ws_view(ws);
-    const uint32_t per = (nranges + 1023) / 1024;
-    const uint32_t r0 = threadIdx.x * per;
-    uint64_t sum = 0;
-    uint32_t fd = nranges;
-    for (uint32_t i = 0; i < per; i++) {
-        uint32_t r = r0 + i;
-        if (r >= nranges) break;
-        uint64_t rb = (uint64_t) r * R, re = rb + R < n ? rb + R : n;
-        uint32_t c = w.counts[r];
-        if (c != re - rb && fd == nranges) fd = r;
-        sum += c;
-    }
-    if (fd != nranges) atomicMin(&first_dirty, fd);
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over the 1024 partial sums.
-    for (int d = 1; d < 1024; d <<= 1) {
-        uint64_t y = threadIdx.x >= (uint32_t) d ? part[threadIdx.x - d] : 0;
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    const uint64_t packed = *w.fd;
+    __syncthreads();  // every thread has read fd before it is re-armed
+    uint64_t V;
+    if (packed == 0) {
+        // all ranges but the last were all alphabet
+        V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
+    } else {
+        const uint32_t r0 = (uint32_t) (~packed >> 32);
+        const uint32_t span = nranges - r0;
+        const uint32_t per = (span + 1023) / 1024;
+        const uint32_t q0 = r0 + threadIdx.x * per;
+        uint64_t sum = 0;
+        for (uint32_t i = 0; i < per; i++)
+            if (q0 + i < nranges) sum += w.counts[q0 + i];
+        uint64_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t) d) x += y;
+        }
+        if (lane == 63) wtot[wave] = x;
         __syncthreads();
-        part[threadIdx.x] += y;
-        __syncthreads();
+        uint64_t before = 0, tot = 0;
+        for (uint32_t i = 0; i < 16; i++) {
+            if (i < wave) before += wtot[i];
+            tot += wtot[i];
+        }
+        uint64_t run = (uint64_t) r0 * R + before + x - sum;
+        for (uint32_t i = 0; i < per; i++) {
+            if (q0 + i >= nranges) break;
+            w.bases[q0 + i] = run;
+            run += w.counts[q0 + i];
+        }
+        V = (uint64_t) r0 * R + tot;
     }
-    uint64_t run = part[threadIdx.x] - sum;
-    for (uint32_t i = 0; i < per; i++) {
-        uint32_t r = r0 + i;
-        if (r >= nranges) break;
-        w.bases[r] = run;
-        run += w.counts[r];
-    }
-    const uint64_t V = part[1023];
     if (threadIdx.x == 0) {
-        *w.first_dirty = first_dirty;
+        *w.fd_cur = packed;
+        *w.fd = 0;
         res->valid = V;
         res->tail_n = (uint32_t) (V & 3);
         res->out_len = hold ? V / 4 * 3 : V * 6 / 8;
     }
-    // Last V mod 4 alphabet characters, scanning backwards (wave 0).
-    if (threadIdx.x < 64) {
+    if (wave == 0) {
         int need = (int) (V & 3);
         uint8_t got[4] = {0, 0, 0, 0};
         uint64_t end = n;
         while (need > 0 && end > 0) {
             uint64_t beg = end >= 64 ? end - 64 : 0;
-            uint64_t p = beg + threadIdx.x;
+            uint64_t p = beg + lane;
             uint32_t t = p < end ? tab[in[p]] : 0xFFu;
-            uint64_t m = __ballot(t < 64u);
-            while (need > 0 && m) {
-                int hi = 63 - __clzll(m);
+            uint64_t bm = __ballot(t < 64u);
+            while (need > 0 && bm) {
+                int hi = 63 - __clzll(bm);
                 got[--need] = (uint8_t) __shfl(t, hi, 64);
-                m &= ~(1ull << hi);
+                bm &= ~(1ull << hi);
             }
             end = beg;
         }
-        if (threadIdx.x == 0)
+        if (lane == 0)
             for (int j = 0; j < 4; j++) res->tail[j] = got[j];
     }
 }
 
-// Pass 2: re-run the ranges after the first dirty one with true bases.
+// Pass 2: exact decode from the first dirty chunk on (grid-stride over
+// ranges; returns at once on a clean call).  The first dirty range resumes
+// at its dirty chunk -- everything before it was alphabet and is already
+// final; every later range re-runs with its true base.
 __global__ __launch_bounds__(kThreads) void k_decode_pass2(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
 {
     DecodeWs w = ws_view(ws);
-    const uint32_t fd = *w.first_dirty;
-    if (blockIdx.x * kWavesPerBlock + kWavesPerBlock - 1 <= fd) return;
+    const uint64_t packed = *w.fd_cur;
+    if (packed == 0) return;
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t off0 = (uint32_t) ~packed;
     __shared__ DecSmem sm;
     build_dec_table(sm.tab, a);
     __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t r = blockIdx.x * kWavesPerBlock + wv;
-    if (r >= nranges || r <= fd) return;
-    const uint64_t rb = (uint64_t) r * R;
-    const uint64_t re = rb + R < n ? rb + R : n;
-    const uint64_t B = w.bases[r];
-    const int skip = (int) ((4 - (B & 3)) & 3);
-    decode_range(sm.tab, sm.sx[wv], in, n, rb, re, skip, out + (B + 3) / 4 * 3,
-                 r + 1 == nranges, hold != 0);
-}
-
-// Uniform-stride batch decode: one wave per buffer.
-__global__ __launch_bounds__(kThreads) void k_decode_strided(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
-    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
-    uint64_t *__restrict__ outlen, DecAlpha a)
-{
-    __shared__ DecSmem sm;
-    build_dec_table(sm.tab, a);
-    __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t b = blockIdx.x * kWavesPerBlock + wv; b < nbuf; b += nw) {
-        const uint8_t *src = in + (uint64_t) b * in_stride;
-        uint64_t v = decode_range(sm.tab, sm.sx[wv], src, len, 0, len, 0,
-                                  out + (uint64_t) b * out_stride, true, false);
-        if (lane_id() == 0) outlen[b] = v * 6 / 8;
+    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const uint64_t B = w.bases[r];
+        const bool last = r + 1 == nranges;
+        if (r == r0) {
+            decode_range(sm.tab, sm.sx[wv], in, n, rb + off0, re, 0,
+                         out + (B + off0) / 4 * 3, last, hold != 0);
+        } else {
+            const int skip = (int) ((4 - (B & 3)) & 3);
+            decode_range(sm.tab, sm.sx[wv], in, n, rb, re, skip, out + (B + 3) / 4 * 3,
+                         last, hold != 0);
+        }
     }
 }
 
-// Ragged batch decode: one wave per buffer.
-__global__ __launch_bounds__(kThreads) void k_decode_ragged(
-    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-    uint32_t nbuf, uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off,
-    uint64_t *__restrict__ outlen, DecAlpha a)
+// Batches: buffer b is in[ioff(b) .. +len(b)) -> out + ooff(b).
+struct BatchLayout {
+    const uint64_t *in_off;   // nbuf+1 offsets, or null for a uniform stride
+    const uint64_t *out_off;  // nbuf offsets, or null
+    uint64_t in_stride, out_stride, len;
+};
+
+DEV void batch_buf(const BatchLayout &L, uint32_t b, uint64_t &beg, uint64_t &len,
+                   uint64_t &obeg)
+{
+    if (L.in_off) {
+        beg = L.in_off[b];
+        len = L.in_off[b + 1] - beg;
+        obeg = L.out_off[b];
+    } else {
+        beg = (uint64_t) b * L.in_stride;
+        len = L.len;
+        obeg = (uint64_t) b * L.out_stride;
+    }
+}
+
+constexpr uint64_t kNeedsExact = ~0ull;
+
+// Up to 16 characters of a lane from src[p..] within [0, len): one
+// dwordx4 (non-temporal) when the lane's 16 are present and dword aligned.
+DEV uint4 load_lane(const uint8_t *src, uint64_t p, uint64_t len, bool aligned, uint32_t &nin)
+{
+    nin = p >= len ? 0u : (len - p >= 16 ? 16u : (uint32_t) (len - p));
+    if (nin == 16 && aligned) return ld16<true>(src + p);
+    return nin ? load_chars(src + p, nin) : make_uint4(0, 0, 0, 0);
+}
+
+// Batch decode, fast paths only.  Persistent waves walk buffers b, b+W,
+// ... two chunks ("a pair") at a time; the loads of the next pair -- of
+// this buffer, or the first pair of the next one -- are issued before the
+// current pair is decoded, so small buffers do not each pay a full memory
+// latency.  A buffer any of whose chunks needs the exact path is marked in
+// outlen[] for the fix-up.
+__global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
+    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (b >= nbuf) return;
+    uint64_t beg, len, obeg;
+    batch_buf(L, b, beg, len, obeg);
+    bool aligned = ((((uintptr_t) (in + beg)) | ((uintptr_t) (out + obeg))) & 3) == 0;
+    uint32_t nin[2];
+    uint4 w[2];
+    w[0] = load_lane(in + beg, 16 * lane, len, aligned, nin[0]);
+    w[1] = load_lane(in + beg, kChunk + 16 * lane, len, aligned, nin[1]);
+    uint64_t pos = 0, V = 0;
+    bool ok = true;
+    for (;;) {
+        // issue the next pair's loads
+        const bool more_here = pos + 2 * kChunk < len;
+        const uint32_t bn = b + nw;
+        uint64_t nbeg = beg, nlen = len, nobeg = obeg, npos = pos + 2 * kChunk;
+        if (!more_here && bn < nbuf) {
+            batch_buf(L, bn, nbeg, nlen, nobeg);
+            npos = 0;
+        }
+        const bool naligned = ((((uintptr_t) (in + nbeg)) | ((uintptr_t) (out + nobeg))) & 3) == 0;
+        uint32_t nnin[2] = {0, 0};
+        uint4 nw4[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if (more_here || bn < nbuf) {
+            nw4[0] = load_lane(in + nbeg, npos + 16 * lane, nlen, naligned, nnin[0]);
+            nw4[1] = load_lane(in + nbeg, npos + kChunk + 16 * lane, nlen, naligned, nnin[1]);
+        }
+        // decode the current pair of buffer b
+        uint8_t *dst = out + obeg;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t cpos = pos + (uint64_t) u * kChunk;
+            if (!ok || cpos >= len) break;
+            uint32_t G[4], bad;
+            map_fast(tab, w[u], nin[u], G, bad);
+            if (__all(bad == 0)) {
+                if (aligned) emit_full_a4<true>(G, dst + cpos / 4 * 3);
+                else emit_full(G, dst + cpos / 4 * 3);
+                V += kChunk;
+                continue;
+            }
+            LaneChunk lc;
+            map_chunk(tab, w[u], nin[u], lc);
+            int got = cpos + kChunk >= len ? fast_prefix(lc, false, dst + cpos / 4 * 3) : -1;
+            if (got < 0) ok = false;
+            else V += (uint32_t) got;
+        }
+        if (more_here && ok) {
+            pos = npos;
+        } else {
+            if (lane == 0) outlen[b] = ok ? V * 6 / 8 : kNeedsExact;
+            if (bn >= nbuf) break;
+            bool fresh_aligned = naligned;
+            if (more_here) {
+                // buffer b was abandoned early (marked): what was loaded is
+                // its next pair, not the next buffer's first pair
+                batch_buf(L, bn, nbeg, nlen, nobeg);
+                fresh_aligned = ((((uintptr_t) (in + nbeg)) | ((uintptr_t) (out + nobeg))) & 3) == 0;
+                nw4[0] = load_lane(in + nbeg, 16 * lane, nlen, fresh_aligned, nnin[0]);
+                nw4[1] = load_lane(in + nbeg, kChunk + 16 * lane, nlen, fresh_aligned, nnin[1]);
+            }
+            b = bn;
+            beg = nbeg;
+            len = nlen;
+            obeg = nobeg;
+            aligned = fresh_aligned;
+            pos = 0;
+            V = 0;
+            ok = true;
+        }
+        w[0] = nw4[0];
+        w[1] = nw4[1];
+        nin[0] = nnin[0];
+        nin[1] = nnin[1];
+    }
+}
+
+// Uniform-stride batch decode, flattened: lane slot t = (buffer t / S,
+// 16-character slot t mod S), S = slots per buffer.  Interior slots must
+// be all alphabet (12 bytes out); the last slot of a buffer takes the
+// prefix shape of a padded or unaligned end (fast_prefix's rule, per lane)
+// and publishes the buffer's length.  Any other slot marks the buffer.
+// Both go through atomicMax on outlen[] (zeroed by the launcher), so a mark
+// always wins; the fix-up then decodes marked buffers exactly.
+template <int U, bool PLAIN>
+__global__ __launch_bounds__(kThreads) void k_decode_slots(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
+    uint8_t *__restrict__ out, uint64_t out_stride,
+    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t total_slots, DecAlpha a)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    uint4 w[U];
+    uint32_t nin[U], bq[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t t = (blockIdx.x * U + u) * kThreads + threadIdx.x;
+        nin[u] = 0;
+        bq[u][0] = bq[u][1] = 0;
+        w[u] = make_uint4(0, 0, 0, 0);
+        if (t < total_slots) {
+            const uint32_t b = t / S, q = t - b * S;
+            bq[u][0] = b;
+            bq[u][1] = q;
+            const uint8_t *src = in + (uint64_t) b * in_stride + (uint64_t) q * 16;
+            const uint64_t avail = len - (uint64_t) q * 16;
+            nin[u] = avail >= 16 ? 16u : (uint32_t) avail;
+            if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<true>(src);
+            else w[u] = load_chars(src, nin[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        if (!nin[u]) continue;
+        const uint32_t b = bq[u][0], q = bq[u][1];
+        uint8_t *dst = out + (uint64_t) b * out_stride + (uint64_t) q * 12;
+        uint32_t G[4], bad;
+        map_fast(tab, w[u], nin[u], G, bad);
+        uint32_t nbytes = 12, k = 16;
+        bool ok = bad == 0;
+        if (!ok && q == S - 1) {
+            LaneChunk lc;
+            map_chunk(tab, w[u], nin[u], lc);
+            const uint32_t m = lc.vmask;
+            ok = (m & (m + 1)) == 0;  // alphabet characters form a prefix
+            k = __popc(m);
+            nbytes = 3 * (k >> 2) + ((6 * (k & 3)) >> 3);
+#pragma unroll
+            for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+        }
+        if (ok) {
+            uint32_t o0, o1, o2;
+            groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+            if (nbytes == 12 && (((uintptr_t) dst) & 3) == 0) {
+                __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+            } else if (nbytes) {
+                store_bytes12(dst, o0, o1, o2, nbytes);
+            }
+            if (q == S - 1) {
+                if (PLAIN) outlen[b] = (16ull * q + k) * 6 / 8;
+                else atomicMax(&outlen[b], (unsigned long long) ((16ull * q + k) * 6 / 8));
+            }
+        } else {
+            if (PLAIN) outlen[b] = kNeedsExact;
+            else atomicMax(&outlen[b], (unsigned long long) kNeedsExact);
+        }
+    }
+}
+
+// Batch fix-up: exact decode of the buffers the fast kernel marked.  Each
+// wave checks 64 outlen[] words at a time (one coalesced load + ballot) and
+// decodes the marked ones, so a clean batch costs one read of outlen[].
+__global__ __launch_bounds__(kThreads) void k_decode_batch_fix(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
+    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
 {
     __shared__ DecSmem sm;
     build_dec_table(sm.tab, a);
     __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t b = blockIdx.x * kWavesPerBlock + wv; b < nbuf; b += nw) {
-        const uint64_t beg = in_off[b], len = in_off[b + 1] - beg;
-        uint64_t v = decode_range(sm.tab, sm.sx[wv], in + beg, len, 0, len, 0,
-                                  out + out_off[b], true, false);
-        if (lane_id() == 0) outlen[b] = v * 6 / 8;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
+    for (uint64_t base = ((uint64_t) blockIdx.x * kWavesPerBlock + wv) * 64; base < nbuf;
+         base += nw * 64) {
+        const uint64_t bl = base + lane;
+        uint64_t m = __ballot(bl < nbuf && outlen[bl] == kNeedsExact);
+        while (m) {
+            const uint32_t i = __ffsll((unsigned long long) m) - 1;
+            m &= m - 1;
+            const uint32_t b = (uint32_t) (base + i);
+            uint64_t beg, len, obeg;
+            batch_buf(L, b, beg, len, obeg);
+            uint64_t v = decode_range(sm.tab, sm.sx[wv], in + beg, len, 0, len, 0,
+                                      out + obeg, true, false);
+            if (lane == 0) outlen[b] = v * 6 / 8;
+        }
     }
 }
 
@@ -717,7 +1378,7 @@ DeviceInfo query_device()
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_encode, kThreads, 0) == hipSuccess && nb > 0)
         d.enc_blocks_per_cu = nb;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_pass1, kThreads, 0) == hipSuccess && nb > 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_batch_fast, kThreads, 0) == hipSuccess && nb > 0)
         d.dec_blocks_per_cu = nb;
     d.ok = true;
     return d;
@@ -787,20 +1448,96 @@ struct RangePlan {
     uint32_t nranges;
 };
 
-RangePlan plan_ranges(uint64_t n, const DeviceInfo &d)
+// Ranges of kRangeChunks chunks (g_tune[2] overrides), at most kMaxRanges
+// of them: many short ranges, one wave each, launched as a non-persistent
+// grid -- the shape that streams fastest -- and enough parallelism for the
+// exact pass 2 on dirty input.
+RangePlan plan_ranges(uint64_t n)
 {
-    uint64_t resident = (uint64_t) d.cus * d.dec_blocks_per_cu * kWavesPerBlock;
-    if (resident > kMaxRanges) resident = kMaxRanges;
-    uint64_t want = (n + kMinRange - 1) / kMinRange;
-    if (want > resident) want = resident;
-    if (want < 1) want = 1;
-    uint64_t R = (n + want - 1) / want;
-    R = (R + kChunk - 1) / kChunk * kChunk;
+    uint64_t chunks = g_tune[2] > 0 ? (uint64_t) g_tune[2] : kRangeChunks;
+    uint64_t R = chunks * kChunk;
+    if ((n + R - 1) / R > kMaxRanges) {
+        R = (n + kMaxRanges - 1) / kMaxRanges;
+        R = (R + kChunk - 1) / kChunk * kChunk;
+    }
     RangePlan p;
     p.R = R;
     p.nranges = (uint32_t) ((n + R - 1) / R);
     if (p.nranges == 0) p.nranges = 1;
     return p;
+}
+
+template <typename K>
+int occupancy_of(K kernel)
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kThreads, 0) != hipSuccess || nb < 1)
+        nb = 1;
+    return nb;
+}
+
+template <int U, bool P, bool LNT, bool NT>
+int launch_encode_flat(const DeviceInfo &d, const uint8_t *in, uint64_t n, uint8_t *out,
+                       EncAlpha a, hipStream_t s, bool persistent)
+{
+    static const int occ = occupancy_of(k_encode_flat<U, P, LNT, NT>);
+    const uint64_t nq = n / 12, tile = (uint64_t) kThreads * U;
+    const uint64_t cap = persistent ? (uint64_t) d.cus * occ : (uint64_t) 1 << 31;
+    uint32_t grid = cap_grid(nq / tile, cap);
+    hipLaunchKernelGGL((k_encode_flat<U, P, LNT, NT>), dim3(grid), dim3(kThreads), 0, s, in,
+                       n, out, a);
+    return launch_status();
+}
+
+// Variant 0 is the shipped configuration (fastest in the interleaved A/B of
+// scripts/bench_variants.py, profiles/r01_variants*.json); the others stay
+// selectable for re-tuning.
+int encode_flat(int variant, const DeviceInfo &d, const uint8_t *in, uint64_t n,
+                uint8_t *out, EncAlpha a, hipStream_t s)
+{
+    switch (variant) {
+    case 1: return launch_encode_flat<4, false, false, true>(d, in, n, out, a, s, false);
+    case 2: return launch_encode_flat<4, false, false, true>(d, in, n, out, a, s, true);
+    case 3: return launch_encode_flat<8, false, true, true>(d, in, n, out, a, s, false);
+    case 4: return launch_encode_flat<4, false, true, true>(d, in, n, out, a, s, false);
+    case 5: return launch_encode_flat<4, true, true, true>(d, in, n, out, a, s, true);
+    case 6: return launch_encode_flat<1, false, true, true>(d, in, n, out, a, s, false);
+    default: return launch_encode_flat<2, false, true, true>(d, in, n, out, a, s, false);
+    }
+}
+
+struct Pass1Launch {
+    int blocks_per_cu;
+    void (*launch)(dim3, hipStream_t, const uint8_t *, uint64_t, uint8_t *, uint64_t,
+                   uint32_t, DecAlpha, void *, uint32_t);
+};
+
+template <int U, bool P, bool NT>
+void pass1_launcher(dim3 g, hipStream_t s, const uint8_t *in, uint64_t n, uint8_t *out,
+                    uint64_t R, uint32_t nr, DecAlpha a, void *ws, uint32_t hold)
+{
+    hipLaunchKernelGGL((k_decode_pass1<U, P, NT>), g, dim3(kThreads), 0, s, in, n, out, R,
+                       nr, a, ws, hold);
+}
+
+template <int U, bool P, bool NT>
+Pass1Launch pass1_of()
+{
+    static const int occ = occupancy_of(k_decode_pass1<U, P, NT>);
+    return Pass1Launch{occ, pass1_launcher<U, P, NT>};
+}
+
+Pass1Launch pass1_variant(int variant)
+{
+    switch (variant) {
+    case 1: return pass1_of<4, false, false>();
+    case 2: return pass1_of<2, true, true>();
+    case 3: return pass1_of<8, false, true>();
+    case 4: return pass1_of<4, false, true>();
+    case 5: return pass1_of<4, true, true>();
+    case 6: return pass1_of<1, false, true>();
+    default: return pass1_of<2, false, true>();
+    }
 }
 
 }  // namespace
@@ -819,7 +1556,7 @@ uint64_t b64x_decoded_cap(uint64_t nchars) { return (nchars + 3) / 4 * 3; }
 uint64_t b64x_decode_workspace_size(uint64_t nchars)
 {
     (void) nchars;
-    return (uint64_t) kMaxRanges * 12 + 64;
+    return 64 + (uint64_t) kMaxRanges * 12;
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
@@ -831,6 +1568,11 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
     if (!d_in || !d_out) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
+    const int variant = g_tune[0];
+    if (variant != 99 && ((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 3) == 0)
+        return encode_flat(variant, *d, (const uint8_t *) d_in, n, (uint8_t *) d_out,
+                           enc_alpha(abc), (hipStream_t) stream);
+    // Misaligned buffers: the generic slot kernel (bytewise where needed).
     const uint64_t slots = (n + 11) / 12;
     const uint64_t per_block = (uint64_t) kThreads * kEncUnroll;
     uint32_t grid = cap_grid((slots + per_block - 1) / per_block,
@@ -847,19 +1589,20 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
 {
     if (nbuf == 0 || len == 0) return 0;
     if (!d_in || !d_out) return -EINVAL;
-    if (nbuf > 1 && (in_stride < len || out_stride < b64x_encoded_len(len, enc_alpha(abc).pad)))
+    if (nbuf == 1) return b64x_encode_dev(d_in, len, d_out, abc, stream);
+    if (in_stride < len || out_stride < b64x_encoded_len(len, enc_alpha(abc).pad))
         return -EINVAL;
     const uint64_t qpb = (len + 11) / 12;
     const uint64_t slots = qpb * nbuf;
-    if (nbuf > 1 && slots > 0xFFFFFFFFull) return -EINVAL;
+    if (slots > 0xFFFFFFFFull - 4096) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-    const uint64_t per_block = (uint64_t) kThreads * kEncUnroll;
-    uint32_t grid = cap_grid((slots + per_block - 1) / per_block,
-                             (uint64_t) d->cus * d->enc_blocks_per_cu);
-    hipLaunchKernelGGL(k_encode, dim3(grid), dim3(kThreads), 0, (hipStream_t) stream,
-                       (const uint8_t *) d_in, in_stride, len, nbuf, (uint8_t *) d_out,
-                       out_stride, qpb, slots, enc_alpha(abc));
+    constexpr int U = 2;
+    const uint64_t per_block = (uint64_t) kThreads * U;
+    hipLaunchKernelGGL(k_encode_strided<U>, dim3((uint32_t) ((slots + per_block - 1) / per_block)),
+                       dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
+                       in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
+                       (uint32_t) slots, enc_alpha(abc));
     return launch_status();
 }
 
@@ -889,6 +1632,7 @@ static void *library_workspace(int *err)
     if (!g_ws[dev]) {
         void *p = nullptr;
         hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
+        if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
         if (e != hipSuccess) {
             *err = hip_err(e);
             return nullptr;
@@ -914,24 +1658,46 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     int err = 0;
     void *ws = d_workspace ? d_workspace : library_workspace(&err);
     if (!ws) return err;
-    const RangePlan p = plan_ranges(nchars, *d);
+    const Pass1Launch p1 = pass1_variant(g_tune[1]);
+    const RangePlan p = plan_ranges(nchars);
     const uint32_t blocks = (p.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const DecAlpha a = dec_alpha(abc);
     const uint32_t hold = flags & B64X_DEC_HOLD_TAIL;
-    hipLaunchKernelGGL(k_decode_pass1, dim3(blocks), dim3(kThreads), 0, s,
-                       (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
-                       p.nranges, a, ws, hold);
+    p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
+              p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
     hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
                        nchars, p.R, p.nranges, a, ws, d_res, hold);
     if ((err = launch_status())) return err;
-    if (p.nranges > 1) {
-        hipLaunchKernelGGL(k_decode_pass2, dim3(blocks), dim3(kThreads), 0, s,
-                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
-                           p.nranges, a, ws, hold);
-        if ((err = launch_status())) return err;
-    }
-    return 0;
+    const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 4);
+    hipLaunchKernelGGL(k_decode_pass2, dim3(b2), dim3(kThreads), 0, s,
+                       (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+                       a, ws, hold);
+    return launch_status();
+}
+
+static int launch_batch_decode(const void *d_in, const BatchLayout &L, uint32_t nbuf,
+                               void *d_out, uint64_t *d_outlen,
+                               const b64x_alphabet *abc, void *stream)
+{
+    const DeviceInfo *d = device_info();
+    if (!d) return -ENODEV;
+    hipStream_t s = (hipStream_t) stream;
+    const DecAlpha a = dec_alpha(abc);
+    static const int occ = occupancy_of(k_decode_batch_fast);
+    uint32_t grid = cap_grid((nbuf + kWavesPerBlock - 1) / kWavesPerBlock,
+                             (uint64_t) d->cus * occ);
+    hipLaunchKernelGGL(k_decode_batch_fast, dim3(grid), dim3(kThreads), 0, s,
+                       (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
+    int err = launch_status();
+    if (err) return err;
+    // The fix-up scans outlen[] 64 words per wave; on clean input that is
+    // all it does.
+    uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
+                              (uint64_t) d->cus * 8);
+    hipLaunchKernelGGL(k_decode_batch_fix, dim3(fgrid), dim3(kThreads), 0, s,
+                       (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
+    return launch_status();
 }
 
 int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
@@ -941,13 +1707,37 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (nbuf == 0) return 0;
     if (!d_in || !d_out || !d_outlen) return -EINVAL;
     if (nbuf > 1 && (in_stride < len || out_stride < b64x_decoded_cap(len))) return -EINVAL;
+    const uint64_t S = (len + 15) / 16;
+    const uint64_t slots = S * nbuf;
+    BatchLayout L{nullptr, nullptr, in_stride, out_stride, len};
+    if (slots > 0xFFFFFFFFull - 4096 || len > 0xFFFFFFFFull)
+        return launch_batch_decode(d_in, L, nbuf, d_out, d_outlen, abc, stream);
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-    uint32_t grid = cap_grid((nbuf + kWavesPerBlock - 1) / kWavesPerBlock,
-                             (uint64_t) d->cus * d->dec_blocks_per_cu * 16);
-    hipLaunchKernelGGL(k_decode_strided, dim3(grid), dim3(kThreads), 0, (hipStream_t) stream,
-                       (const uint8_t *) d_in, in_stride, len, nbuf, (uint8_t *) d_out,
-                       out_stride, d_outlen, dec_alpha(abc));
+    hipStream_t s = (hipStream_t) stream;
+    const DecAlpha a = dec_alpha(abc);
+    int err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s));
+    if (err) return err;
+    if (slots) {
+        constexpr int U = 2;
+        const uint64_t per_block = (uint64_t) kThreads * U;
+        const dim3 g((uint32_t) ((slots + per_block - 1) / per_block));
+        if (g_tune[3] == 1)  // benchmark-only: racy plain stores (prices the atomics)
+            hipLaunchKernelGGL((k_decode_slots<U, true>), g, dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
+                               (uint32_t) slots, a);
+        else
+            hipLaunchKernelGGL((k_decode_slots<U, false>), g, dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
+                               (uint32_t) slots, a);
+        if ((err = launch_status())) return err;
+    }
+    uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
+                              (uint64_t) d->cus * 8);
+    hipLaunchKernelGGL(k_decode_batch_fix, dim3(fgrid), dim3(kThreads), 0, s,
+                       (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }
 
@@ -957,14 +1747,8 @@ int b64x_decode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
 {
     if (nbuf == 0) return 0;
     if (!d_in || !d_in_off || !d_out || !d_out_off || !d_outlen) return -EINVAL;
-    const DeviceInfo *d = device_info();
-    if (!d) return -ENODEV;
-    uint32_t grid = cap_grid((nbuf + kWavesPerBlock - 1) / kWavesPerBlock,
-                             (uint64_t) d->cus * d->dec_blocks_per_cu * 16);
-    hipLaunchKernelGGL(k_decode_ragged, dim3(grid), dim3(kThreads), 0, (hipStream_t) stream,
-                       (const uint8_t *) d_in, d_in_off, nbuf, (uint8_t *) d_out,
-                       d_out_off, d_outlen, dec_alpha(abc));
-    return launch_status();
+    BatchLayout L{d_in_off, d_out_off, 0, 0, 0};
+    return launch_batch_decode(d_in, L, nbuf, d_out, d_outlen, abc, stream);
 }
 
 int b64x_fill_splitmix64(void *d_out, uint64_t n, uint64_t seed, void *stream)
@@ -1020,7 +1804,8 @@ b64x_session *b64x_session_open(uint64_t capacity)
               hipMalloc((void **) &s->d_in, capacity) == hipSuccess &&
               hipMalloc((void **) &s->d_out, ocap) == hipSuccess &&
               hipMalloc((void **) &s->d_res, sizeof(b64x_dec_result)) == hipSuccess &&
-              hipMalloc(&s->d_ws, b64x_decode_workspace_size(capacity)) == hipSuccess;
+              hipMalloc(&s->d_ws, b64x_decode_workspace_size(capacity)) == hipSuccess &&
+              hipMemset(s->d_ws, 0, b64x_decode_workspace_size(capacity)) == hipSuccess;
     if (!ok) {
         b64x_session_close(s);
         errno = ENOMEM;
@@ -1086,6 +1871,40 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
     if ((err = hip_err(hipStreamSynchronize(s->stream)))) return err;
     *res = *s->h_res;
     return 0;
+}
+
+// Tuning and calibration hooks for scripts/bench_variants.py (exported,
+// deliberately not declared in include/b64x.h).
+int b64x__tune(int idx, int value)
+{
+    if (idx < 0 || idx >= 4) return -EINVAL;
+    int old = g_tune[idx];
+    g_tune[idx] = value;
+    return old;
+}
+
+// kind: 0 = 16 B in / 16 B out, 1 = 12 in / 16 out (encode shape),
+// 2 = 16 in / 12 out (decode shape); +8 = non-temporal stores.  `slots`
+// lanes' worth of data are streamed.
+int b64x__probe_copy(const void *d_in, void *d_out, uint64_t slots, int kind, void *stream)
+{
+    const DeviceInfo *d = device_info();
+    if (!d) return -ENODEV;
+    if ((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 15) return -EINVAL;
+    hipStream_t s = (hipStream_t) stream;
+    uint32_t grid = cap_grid(slots / (kThreads * 4), (uint64_t) d->cus * 8);
+    const uint8_t *i = (const uint8_t *) d_in;
+    uint8_t *o = (uint8_t *) d_out;
+    switch (kind) {
+    case 0: hipLaunchKernelGGL((k_copy_probe<16, 16, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    case 1: hipLaunchKernelGGL((k_copy_probe<12, 16, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    case 2: hipLaunchKernelGGL((k_copy_probe<16, 12, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    case 8: hipLaunchKernelGGL((k_copy_probe<16, 16, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    case 9: hipLaunchKernelGGL((k_copy_probe<12, 16, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    case 10: hipLaunchKernelGGL((k_copy_probe<16, 12, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
+    default: return -EINVAL;
+    }
+    return launch_status();
 }
 
 const char *b64x_build_info(void)

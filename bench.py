@@ -92,7 +92,7 @@ def bench_single(args, world, rank, b64):
     b64.fill_splitmix64(x, 0x5EED)
     enc = torch.empty(E, dtype=torch.uint8, device="cuda")
     dec = torch.empty(b64.decoded_cap(E), dtype=torch.uint8, device="cuda")
-    ws = torch.empty(b64.workspace_size(E), dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(b64.workspace_size(E), dtype=torch.uint8, device="cuda")
     res = torch.zeros(24, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
@@ -136,7 +136,7 @@ def bench_batch(args, world, rank, b64):
     lo = rank * per + min(rank, total_buf % world)
     nbuf = per + (1 if rank < total_buf % world else 0)
     Es = b64.encoded_len(L)
-    cap = b64.decoded_cap(Es)
+    cap = (b64.decoded_cap(Es) + 15) // 16 * 16  # decode stride: capacity, 16-B rows
     x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
     b64.fill_splitmix64(x, 0x5EED + lo)
     enc = torch.empty(nbuf * Es, dtype=torch.uint8, device="cuda")

@@ -95,9 +95,10 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
 /* Decode nchars characters at d_in into d_out (capacity
  * b64x_decoded_cap(nchars)); *d_res (device memory) receives the result.
  * d_workspace: b64x_decode_workspace_size(nchars) bytes of device memory,
- * or NULL to use a library-owned workspace (allocated on first use; not
- * capture-safe on that first call, and not safe to share between
- * concurrent streams). */
+ * zero-filled before its first use (each call leaves it ready for the
+ * next; one workspace per stream), or NULL to use a library-owned one
+ * (allocated on first use: not capture-safe on that first call, and not
+ * safe to share between concurrent streams). */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);

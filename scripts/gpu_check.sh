@@ -6,7 +6,7 @@
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 mkdir -p gpurun_out
-K="${1:-not slow}"; shift || true
+K="${1-not slow}"; shift || true
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   echo "== $name ($(date +%T))"
