@@ -56,13 +56,20 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-batch", action="store_true")
     ap.add_argument("--batch-steps", type=int, default=20)
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; "
+                         "gloo only to rehearse the multi-rank logic on one GPU)")
     return ap.parse_args()
+
+
+def coll_device():
+    return "cpu" if dist.is_initialized() and dist.get_backend() == "gloo" else "cuda"
 
 
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -74,13 +81,23 @@ def sync_all(world: int):
     torch.cuda.synchronize()
 
 
-def load_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary."""
+def load_traffic(kernels):
+    """HBM bytes per launch of `kernels` (summed) from the committed PMC
+    summary (scripts/pmc_traffic.sh + scripts/summarize_pmc.py)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{ROUND}.json")
     try:
         with open(path) as f:
-            pmc = json.load(f)
-        return pmc["kernels"][kernel]["hbm_bytes_per_launch"]
+            pmc = json.load(f)["kernels"]
+        total = 0.0
+        for k in kernels:
+            if k in pmc:
+                total += pmc[k]["hbm_bytes_per_launch"]
+            else:  # grid-qualified entries
+                hits = [v for n, v in pmc.items() if n.startswith(k + "@")]
+                if not hits:
+                    return None
+                total += max(h["hbm_bytes_per_launch"] for h in hits)
+        return total
     except (OSError, KeyError, ValueError):
         return None
 
@@ -131,10 +148,10 @@ def bench_single(args, world, rank, b64):
 
 def bench_batch(args, world, rank, b64):
     """BASELINE config 4: 1 M x 1 KiB, sharded across ranks by index."""
+    from async_amd import shard
+
     total_buf, L = 1 << 20, 1024
-    per = total_buf // world
-    lo = rank * per + min(rank, total_buf % world)
-    nbuf = per + (1 if rank < total_buf % world else 0)
+    lo, nbuf = shard.by_index(total_buf, world, rank)
     Es = b64.encoded_len(L)
     cap = (b64.decoded_cap(Es) + 15) // 16 * 16  # decode stride: capacity, 16-B rows
     x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
@@ -168,11 +185,8 @@ def bench_batch(args, world, rank, b64):
         b64.decode_strided(enc, Es, Es, nbuf, dec, cap, outlen, stream=stream)
     ev[2].record(stream)
     # the one exchange step: every rank learns every rank's output total
-    mine = outlen.sum().reshape(1)
-    if world > 1:
-        dist.all_gather_into_tensor(totals, mine)
-    else:
-        totals.copy_(mine)
+    _, tot_list = shard.exchange_totals(int(outlen.sum()), device=coll_device())
+    totals.copy_(torch.tensor(tot_list, dtype=torch.int64))
     sync_all(world)
     wall = max_over_ranks(time.perf_counter() - t0, world)
     assert int(totals.sum()) == total_buf * L
@@ -226,9 +240,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     from async_amd import b64
 
     b64.device_check()
@@ -244,7 +261,8 @@ def main():
         dom = "encode" if r["enc_ms"] >= r["dec_ms"] else "decode"
         dom_ms = max(r["enc_ms"], r["dec_ms"])
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
-        kname = "k_encode" if dom == "encode" else "k_decode_pass1"
+        knames = ["k_encode_flat"] if dom == "encode" else \
+            ["k_decode_pass1", "k_decode_scan", "k_decode_pass2"]
         out = {
             "metric": METRIC,
             "value": world * N * K / r["wall"] / 2**30,
@@ -274,12 +292,14 @@ def main():
                                   / (HBM_PEAK_GBS * 1e9),
             "roofline": {
                 "bound": "hbm",
-                "kernel": kname,
+                "kernel": "+".join(knames),
+                "timing": "HIP events around the b64x call on its stream, mean over the "
+                          "timed steps",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(kname),
+                "traffic": load_traffic(knames),
             },
             "cpu_baseline": cpu,
             "batch_cfg4": batch,

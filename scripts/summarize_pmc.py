@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.sh)
+into profiles/pmc_<round>.json, the file bench.py reads `roofline.traffic`
+from.  Corrections per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide streaming
+read, so it is doubled; WRITE_SIZE is taken as is."""
+import collections
+import csv
+import json
+import os
+import statistics
+import sys
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out", "pmc_traffic")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+vals = collections.defaultdict(dict)
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    per = collections.defaultdict(list)
+    with open(os.path.join(src, c, "run_counter_collection.csv")) as f:
+        for r in csv.DictReader(f):
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            name = name.replace("void ", "").split("<")[0]
+            key = f"{name}@grid{r['Grid_Size']}"
+            per[key].append(float(r["Counter_Value"]))
+    for k, v in per.items():
+        vals[k][c] = statistics.median(v)
+        vals[k]["dispatches"] = len(v)
+kernels = {}
+for k, v in vals.items():
+    if "FETCH_SIZE" not in v or "WRITE_SIZE" not in v:
+        continue
+    fetch = 2 * v["FETCH_SIZE"] * 1024
+    write = v["WRITE_SIZE"] * 1024
+    kernels[k] = {"fetch_bytes": fetch, "write_bytes": write,
+                  "hbm_bytes_per_launch": fetch + write,
+                  "raw_FETCH_SIZE_KiB": v["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": v["WRITE_SIZE"]}
+# short aliases for the config-2 kernels bench.py names
+for alias in ("k_encode_flat", "k_decode_pass1"):
+    cands = sorted((k for k in kernels if k.startswith(alias + "@")),
+                   key=lambda k: -kernels[k]["hbm_bytes_per_launch"])
+    if cands:
+        kernels[alias] = kernels[cands[0]]
+out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
+                 "`bench.py --steps 5 --warmup 1 --no-cpu --batch-steps 3`",
+       "corrections": "fetch = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB",
+       "kernels": kernels}
+dst = os.path.join(root, "profiles", f"pmc_{rnd}.json")
+with open(dst, "w") as f:
+    json.dump(out, f, indent=1)
+for k, v in sorted(kernels.items()):
+    print(f"{k:45s} fetch {v['fetch_bytes']/1e9:8.4f} GB  write {v['write_bytes']/1e9:8.4f} GB")
