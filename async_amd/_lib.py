@@ -81,6 +81,10 @@ SIGNATURES = {
     "b64x_session_host_out": (_vp, [_vp]),
     "b64x_session_encode": (_int, [_vp, _u64, _ap, ctypes.POINTER(_u64)]),
     "b64x_session_decode": (_int, [_vp, _u64, _ap, ctypes.c_uint, ctypes.POINTER(DecResult)]),
+    "b64x_session_encode_async": (_int, [_vp, _u64, _ap, _vp, _vp]),
+    "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp, _vp]),
+    "b64x_session_result": (ctypes.POINTER(DecResult), [_vp]),
+    "b64x_session_wait": (_int, [_vp]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),
     "b64x_build_info": (ctypes.c_char_p, []),

@@ -5,48 +5,96 @@
  *
  * Reference: src/base64encoder.c and src/base64decoder.c.  The reference
  * transforms in place inside the caller's buffer, one byte per loop trip
- * (encoder :101-142, decoder :52-80).  Here each stage pulls a large block
- * from its upstream into pinned staging, runs one GPU round trip
- * (b64x_session_*), and serves reads from the staged result:
+ * (encoder :101-142, decoder :52-80), synchronously inside read().  Here a
+ * stage is a small pipeline of two slots, each a b64x session (pinned host
+ * staging + device buffers + a HIP stream):
  *
+ *   read() --> serve the oldest finished slot
+ *          --> top up: pull upstream into an idle slot's pinned buffer and
+ *              queue H2D + kernels + D2H on its stream (read-ahead: both
+ *              slots can be in flight while the consumer drains a third
+ *              block's worth of output)
+ *          --> nothing finished yet: -1 / EAGAIN.
+ *
+ *   GPU completion: a HIP host function marks the slot finished and writes
+ *   the stage's eventfd; the eventfd is registered with async_register(),
+ *   so the loop calls the stage, which calls the consumer's registered
+ *   callback -- the same "EAGAIN now, callback later" contract every
+ *   bytestream_1 in the reference follows.
+ *
+ * Group carries:
  *  - encoder: whole 3-byte groups are encoded; the 0-2 leftover bytes are
- *    carried to the next pull, and encoded with the final padding once
- *    upstream reports EOF (the reference's finalize(), :61-99);
- *  - decoder: whole 4-character groups are decoded (B64X_DEC_HOLD_TAIL);
- *    the 0-3 leftover sextets are carried (re-spelled as alphabet
- *    characters) to the next pull, and flushed at EOF with the
- *    reference's truncation rule (floor(6V/8) bytes overall).
+ *    carried on the host into the next block, and encoded with the final
+ *    padding once upstream reports EOF (the reference's finalize(),
+ *    :61-99);
+ *  - decoder: blocks are decoded with B64X_DEC_HOLD_TAIL; the 0-3 sextets
+ *    a block leaves over are device-determined, so the next block is
+ *    chained on the device (b64x_session_decode_async(carry_from)) instead
+ *    of waiting for the result on the host; at EOF the last block (or an
+ *    empty flush) is decoded without HOLD_TAIL, giving the reference's
+ *    floor(6V/8) bytes overall.
  *
- * The character/byte stream each stage produces is the reference's, byte
- * for byte.  Per-call return counts may differ (a stage returns what it
- * has staged; it never returns 0 before EOF), errno from upstream (EAGAIN
- * included) is passed through with all state kept, and count == 0
- * returns 0 (ref :103-104, :54-55).  The reference's assert at
- * src/base64encoder.c:140 (read counts not divisible by 4) has no
- * counterpart: any count works.
+ * The byte stream each stage produces is the reference's, byte for byte.
+ * Per-call counts differ: a stage returns what it has finished, and
+ * returns -1/EAGAIN while the GPU is busy (a consumer written for the
+ * reference already handles EAGAIN from any stream).  Upstream errors are
+ * passed through with all state kept when nothing is in flight; count ==
+ * 0 returns 0 (ref :103-104, :54-55).  The reference's assert at
+ * src/base64encoder.c:140 (counts not divisible by 4) has no counterpart.
+ * With no usable GPU the first read fails with ENODEV: there is no CPU
+ * path.
  *
  * Tuning (environment, read when a stage is created):
- *   ASYNC_B64_STAGE_CAPACITY  staging bytes per stage (default 1 MiB)
- *   ASYNC_B64_MIN_PULL        smallest upstream request (default 64 KiB)
+ *   ASYNC_B64_STAGE_CAPACITY  staging bytes per slot (default 1 MiB)
+ *   ASYNC_B64_MIN_PULL        gather at least this much from upstream
+ *                             before launching, unless it runs dry
+ *                             (default 64 KiB)
  */
+#define _GNU_SOURCE
 #include <errno.h>
+#include <stdatomic.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
 
+#include "async.h"
 #include "b64x.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
 
-enum stage_state { STAGE_OPEN, STAGE_DONE, STAGE_FAILED };
+enum { NSLOTS = 2 };
+
+typedef struct stage stage;
 
 typedef struct {
+    stage *owner;
     b64x_session *sess;
-    int err;            /* errno to report when sess is NULL / failed */
-    size_t min_pull;
-    const uint8_t *out; /* staged output, inside the session's host_out */
+    atomic_int done;  /* set by the HIP host function */
     size_t out_pos, out_len;
-    enum stage_state state;
-} stage_common;
+} slot;
+
+typedef enum { DIR_ENCODE, DIR_DECODE } direction;
+
+struct stage {
+    async_t *async;
+    bytestream_1 up;
+    action_1 cb;        /* the consumer's callback, or NULL_ACTION_1 */
+    direction dir;
+    b64x_alphabet abc;
+    size_t cap, min_pull;
+    int efd;            /* GPU completion -> loop */
+    bool started;       /* sessions + eventfd exist */
+    int err;            /* sticky failure errno, 0 while healthy */
+    slot slots[NSLOTS];
+    unsigned head;      /* oldest busy slot */
+    unsigned nbusy;     /* launched, output not fully served */
+    bool final_queued;  /* the last block (or nothing) has been launched */
+    bool launched_any;
+    uint8_t carry[2];   /* encoder: bytes of the incomplete group */
+    size_t ncarry;
+};
 
 static size_t env_size(const char *name, size_t dflt, size_t lo)
 {
@@ -60,139 +108,310 @@ static size_t env_size(const char *name, size_t dflt, size_t lo)
     return (size_t) x;
 }
 
-static void stage_init(stage_common *c)
+static void stage_init(stage *st, async_t *async, bytestream_1 up,
+                       direction dir, b64x_alphabet abc)
 {
-    size_t cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
-    c->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
-    c->sess = b64x_session_open(cap);
-    c->err = c->sess ? 0 : (errno ? errno : ENODEV);
-    c->state = c->sess ? STAGE_OPEN : STAGE_FAILED;
+    memset(st, 0, sizeof *st);
+    st->async = async;
+    st->up = up;
+    st->cb = NULL_ACTION_1;
+    st->dir = dir;
+    st->abc = abc;
+    st->cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
+    st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
+    st->efd = -1;
+    for (int i = 0; i < NSLOTS; i++)
+        st->slots[i].owner = st;
 }
 
-static ssize_t stage_fail(stage_common *c, int negerr)
+static ssize_t stage_fail(stage *st, int negerr)
 {
-    c->state = STAGE_FAILED;
-    c->err = negerr < 0 ? -negerr : EIO;
-    errno = c->err;
+    st->err = negerr < 0 ? -negerr : EIO;
+    errno = st->err;
     return -1;
 }
 
-/* Serve from the staged result; -2 when nothing is staged. */
-static ssize_t stage_serve(stage_common *c, void *buf, size_t count)
+/* Loop side of the completion eventfd. */
+static void stage_wake(stage *st)
 {
-    size_t avail = c->out_len - c->out_pos;
-    if (!avail)
-        return -2;
-    size_t n = avail < count ? avail : count;
-    memcpy(buf, c->out + c->out_pos, n);
-    c->out_pos += n;
-    return (ssize_t) n;
+    uint64_t v;
+    while (read(st->efd, &v, sizeof v) == (ssize_t) sizeof v)
+        ;
+    action_1_perf(st->cb);
 }
 
-static size_t pull_size(const stage_common *c, size_t want, size_t held)
+/* HIP runtime thread: publish, then signal. */
+static void slot_done(void *arg)
 {
-    size_t cap = b64x_session_capacity(c->sess) - held;
-    if (want < c->min_pull)
-        want = c->min_pull;
-    return want < cap ? want : cap;
+    slot *sl = arg;
+    atomic_store_explicit(&sl->done, 1, memory_order_release);
+    uint64_t one = 1;
+    ssize_t rc = write(sl->owner->efd, &one, sizeof one);
+    (void) rc; /* EAGAIN only when the counter is saturated: still readable */
+}
+
+static int stage_start(stage *st)
+{
+    if (st->started)
+        return 0;
+    st->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (st->efd < 0)
+        return -errno;
+    if (async_register(st->async, st->efd,
+                       (action_1) { st, (act_1) stage_wake }) < 0) {
+        int e = errno ? errno : EIO;
+        close(st->efd);
+        st->efd = -1;
+        return -e;
+    }
+    for (int i = 0; i < NSLOTS; i++) {
+        st->slots[i].sess = b64x_session_open(st->cap);
+        if (!st->slots[i].sess)
+            return -(errno ? errno : ENODEV);
+    }
+    st->started = true;
+    return 0;
+}
+
+static void stage_stop(stage *st)
+{
+    for (int i = 0; i < NSLOTS; i++) {
+        if (st->slots[i].sess) {
+            (void) b64x_session_wait(st->slots[i].sess);
+            b64x_session_close(st->slots[i].sess);
+            st->slots[i].sess = NULL;
+        }
+    }
+    if (st->efd >= 0) {
+        (void) async_unregister(st->async, st->efd);
+        close(st->efd);
+        st->efd = -1;
+    }
+    st->started = false;
+}
+
+/* Pull from upstream into dst until `want` bytes, EOF, EAGAIN or an
+ * error.  Returns bytes gathered; *eof / *err report why it stopped. */
+static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
+                     int *err)
+{
+    size_t got = 0;
+    size_t want = st->min_pull < room ? st->min_pull : room;
+    *eof = false;
+    *err = 0;
+    while (got < want) {
+        ssize_t n = bytestream_1_read(st->up, dst + got, room - got);
+        if (n < 0) {
+            *err = errno ? errno : EIO;
+            break;
+        }
+        if (n == 0) {
+            *eof = true;
+            break;
+        }
+        got += (size_t) n;
+    }
+    return got;
+}
+
+static slot *next_launch_slot(stage *st)
+{
+    if (st->nbusy >= NSLOTS || st->final_queued)
+        return NULL;
+    return &st->slots[(st->head + st->nbusy) % NSLOTS];
+}
+
+static void slot_arm(stage *st, slot *sl)
+{
+    atomic_store_explicit(&sl->done, 0, memory_order_relaxed);
+    sl->out_pos = sl->out_len = 0;
+    st->nbusy++;
+}
+
+/* Launch as many blocks as slots and upstream allow.  Returns 0, or a
+ * positive errno from upstream (EAGAIN included) that stopped it, or a
+ * negative errno from the GPU side. */
+static int top_up_encoder(stage *st)
+{
+    slot *sl;
+    while ((sl = next_launch_slot(st))) {
+        uint8_t *in = b64x_session_host_in(sl->sess);
+        memcpy(in, st->carry, st->ncarry);
+        bool eof;
+        int uerr;
+        size_t got = gather(st, in + st->ncarry, st->cap - st->ncarry, &eof,
+                            &uerr);
+        size_t total = st->ncarry + got;
+        size_t n;
+        if (eof) {
+            st->final_queued = true;
+            st->ncarry = 0;
+            if (total == 0)
+                return 0;
+            n = total; /* finalize(): partial group + padding */
+        } else {
+            n = total - total % 3;
+            st->ncarry = total - n;
+            memcpy(st->carry, in + n, st->ncarry);
+            if (n == 0)
+                return uerr ? uerr : EAGAIN;
+        }
+        slot_arm(st, sl);
+        int rc = b64x_session_encode_async(sl->sess, n, &st->abc, slot_done,
+                                           sl);
+        if (rc)
+            return rc;
+        sl->out_len = (size_t) b64x_encoded_len(n, eof && st->abc.pad);
+        /* Non-final blocks are whole groups: no padding either way. */
+        if (uerr)
+            return uerr;
+    }
+    return 0;
+}
+
+static int top_up_decoder(stage *st)
+{
+    slot *sl;
+    while ((sl = next_launch_slot(st))) {
+        slot *prev = st->launched_any
+                         ? &st->slots[(st->head + st->nbusy + NSLOTS - 1) %
+                                      NSLOTS]
+                         : NULL;
+        bool eof;
+        int uerr;
+        size_t got = gather(st, b64x_session_host_in(sl->sess), st->cap, &eof,
+                            &uerr);
+        unsigned flags = B64X_DEC_HOLD_TAIL;
+        if (eof) {
+            st->final_queued = true;
+            if (!st->launched_any && got == 0)
+                return 0;
+            flags = 0; /* last block, or a flush of the carried sextets */
+        } else if (got == 0) {
+            return uerr ? uerr : EAGAIN;
+        }
+        slot_arm(st, sl);
+        int rc = b64x_session_decode_async(sl->sess, got, &st->abc, flags,
+                                           prev ? prev->sess : NULL, slot_done,
+                                           sl);
+        if (rc)
+            return rc;
+        st->launched_any = true;
+        if (uerr)
+            return uerr;
+    }
+    return 0;
+}
+
+static ssize_t stage_read(stage *st, void *buf, size_t count)
+{
+    if (!count)
+        return 0;
+    if (st->err) {
+        errno = st->err;
+        return -1;
+    }
+    int rc = stage_start(st);
+    if (rc)
+        return stage_fail(st, rc);
+    for (;;) {
+        slot *h = &st->slots[st->head];
+        if (st->nbusy &&
+            atomic_load_explicit(&h->done, memory_order_acquire)) {
+            if (st->dir == DIR_DECODE && h->out_len == 0 && h->out_pos == 0)
+                h->out_len = (size_t) b64x_session_result(h->sess)->out_len;
+            size_t avail = h->out_len - h->out_pos;
+            size_t n = avail < count ? avail : count;
+            if (n) {
+                memcpy(buf, b64x_session_host_out(h->sess) + h->out_pos, n);
+                h->out_pos += n;
+            }
+            if (h->out_pos == h->out_len) {
+                st->nbusy--;
+                st->head = (st->head + 1) % NSLOTS;
+            }
+            if (n) {
+                /* Keep the GPU busy while the consumer works. */
+                rc = st->dir == DIR_ENCODE ? top_up_encoder(st)
+                                           : top_up_decoder(st);
+                if (rc < 0)
+                    return stage_fail(st, rc);
+                return (ssize_t) n;
+            }
+            continue; /* an empty block: look at the next one */
+        }
+        rc = st->dir == DIR_ENCODE ? top_up_encoder(st) : top_up_decoder(st);
+        if (rc < 0)
+            return stage_fail(st, rc);
+        if (st->nbusy) {
+            if (atomic_load_explicit(&st->slots[st->head].done,
+                                     memory_order_acquire))
+                continue;
+            errno = EAGAIN; /* the eventfd brings the consumer back */
+            return -1;
+        }
+        if (st->final_queued)
+            return 0;
+        errno = rc ? rc : EAGAIN;
+        return -1;
+    }
+}
+
+static void stage_close(stage *st)
+{
+    stage_stop(st);
+    bytestream_1_close(st->up);
+    async_wound(st->async, st);
+    st->async = NULL;
+}
+
+static void stage_register(stage *st, action_1 action)
+{
+    st->cb = action;
+    bytestream_1_register_callback(st->up, action);
+}
+
+static void stage_unregister(stage *st)
+{
+    st->cb = NULL_ACTION_1;
+    bytestream_1_unregister_callback(st->up);
 }
 
 /* ================================================================ encoder */
 
 struct base64encoder {
-    async_t *async;
-    bytestream_1 stream;
-    b64x_alphabet abc;
-    stage_common c;
-    uint8_t carry[2];
-    size_t ncarry;
+    stage st; /* first member: the object pointer is the stage */
 };
 
 base64encoder_t *base64_encode(async_t *async, bytestream_1 stream, char pos62,
                                char pos63, bool pad, char padchar)
 {
-    base64encoder_t *e = calloc(1, sizeof *e);
+    base64encoder_t *e = malloc(sizeof *e);
     if (!e)
         abort();
-    e->async = async;
-    e->stream = stream;
-    e->abc.pos62 = pos62;
-    e->abc.pos63 = pos63;
-    e->abc.padchar = padchar;
-    e->abc.pad = pad;
-    stage_init(&e->c);
+    b64x_alphabet abc = { pos62, pos63, padchar, pad };
+    stage_init(&e->st, async, stream, DIR_ENCODE, abc);
     return e;
 }
 
 ssize_t base64encoder_read(base64encoder_t *e, void *buf, size_t count)
 {
-    if (!count)
-        return 0;
-    for (;;) {
-        ssize_t n = stage_serve(&e->c, buf, count);
-        if (n != -2)
-            return n;
-        if (e->c.state == STAGE_DONE)
-            return 0;
-        if (e->c.state == STAGE_FAILED) {
-            errno = e->c.err;
-            return -1;
-        }
-        uint8_t *in = b64x_session_host_in(e->c.sess);
-        memcpy(in, e->carry, e->ncarry);
-        /* The reference asks upstream for ceil(6*count/8)-ish bytes
-         * (src/base64encoder.c:124); ask for at least min_pull. */
-        size_t want = pull_size(&e->c, (count * 6 + 7) / 8, e->ncarry);
-        ssize_t got = bytestream_1_read(e->stream, in + e->ncarry, want);
-        if (got < 0)
-            return -1; /* errno from upstream; carry kept */
-        size_t total = e->ncarry + (size_t) got;
-        uint64_t m = 0;
-        int rc;
-        if (got == 0) {
-            e->c.state = STAGE_DONE;
-            e->ncarry = 0;
-            if (total == 0)
-                return 0;
-            rc = b64x_session_encode(e->c.sess, total, &e->abc, &m);
-            if (rc)
-                return stage_fail(&e->c, rc);
-        } else {
-            size_t whole = total - total % 3;
-            size_t rest = total - whole;
-            uint8_t keep[2];
-            memcpy(keep, in + whole, rest);
-            if (whole) {
-                rc = b64x_session_encode(e->c.sess, whole, &e->abc, &m);
-                if (rc)
-                    return stage_fail(&e->c, rc);
-            }
-            memcpy(e->carry, keep, rest);
-            e->ncarry = rest;
-        }
-        e->c.out = b64x_session_host_out(e->c.sess);
-        e->c.out_pos = 0;
-        e->c.out_len = (size_t) m;
-    }
+    return stage_read(&e->st, buf, count);
 }
 
 void base64encoder_close(base64encoder_t *e)
 {
-    bytestream_1_close(e->stream);
-    b64x_session_close(e->c.sess);
-    e->c.sess = NULL;
-    async_wound(e->async, e);
-    e->async = NULL;
+    stage_close(&e->st);
 }
 
 void base64encoder_register_callback(base64encoder_t *e, action_1 action)
 {
-    bytestream_1_register_callback(e->stream, action);
+    stage_register(&e->st, action);
 }
 
 void base64encoder_unregister_callback(base64encoder_t *e)
 {
-    bytestream_1_unregister_callback(e->stream);
+    stage_unregister(&e->st);
 }
 
 static ssize_t enc_read_vt(void *o, void *buf, size_t count)
@@ -224,111 +443,38 @@ bytestream_1 base64encoder_as_bytestream_1(base64encoder_t *e)
 /* ================================================================ decoder */
 
 struct base64decoder {
-    async_t *async;
-    bytestream_1 stream;
-    b64x_alphabet abc;
-    stage_common c;
-    uint8_t carry[4]; /* alphabet characters of the incomplete group */
-    size_t ncarry;
+    stage st;
 };
 
 base64decoder_t *base64_decode(async_t *async, bytestream_1 stream, char pos62,
                                char pos63)
 {
-    base64decoder_t *d = calloc(1, sizeof *d);
+    base64decoder_t *d = malloc(sizeof *d);
     if (!d)
         abort();
-    d->async = async;
-    d->stream = stream;
-    d->abc.pos62 = pos62;
-    d->abc.pos63 = pos63;
-    d->abc.padchar = (char) -1;
-    d->abc.pad = false;
-    stage_init(&d->c);
+    b64x_alphabet abc = { pos62, pos63, (char) -1, false };
+    stage_init(&d->st, async, stream, DIR_DECODE, abc);
     return d;
-}
-
-/* A character that decodes to sextet v under this alphabet.  Only values
- * the device actually produced are asked for, so 62/63 always have a
- * matching pos62/pos63 (ref map(), src/base64decoder.c:38-48). */
-static uint8_t spell_sextet(const b64x_alphabet *abc, unsigned v)
-{
-    if (v < 26)
-        return (uint8_t) ('A' + v);
-    if (v < 52)
-        return (uint8_t) ('a' + v - 26);
-    if (v < 62)
-        return (uint8_t) ('0' + v - 52);
-    char p = v == 62 ? abc->pos62 : abc->pos63;
-    if (p == (char) -1)
-        p = v == 62 ? '+' : '/';
-    return (uint8_t) p;
 }
 
 ssize_t base64decoder_read(base64decoder_t *d, void *buf, size_t count)
 {
-    if (!count)
-        return 0;
-    for (;;) {
-        ssize_t n = stage_serve(&d->c, buf, count);
-        if (n != -2)
-            return n;
-        if (d->c.state == STAGE_DONE)
-            return 0;
-        if (d->c.state == STAGE_FAILED) {
-            errno = d->c.err;
-            return -1;
-        }
-        uint8_t *in = b64x_session_host_in(d->c.sess);
-        memcpy(in, d->carry, d->ncarry);
-        size_t want = pull_size(&d->c, count, d->ncarry);
-        ssize_t got = bytestream_1_read(d->stream, in + d->ncarry, want);
-        if (got < 0)
-            return -1; /* errno from upstream; carry kept */
-        size_t total = d->ncarry + (size_t) got;
-        b64x_dec_result res;
-        memset(&res, 0, sizeof res);
-        int rc;
-        if (got == 0) {
-            d->c.state = STAGE_DONE;
-            d->ncarry = 0;
-            if (total == 0)
-                return 0;
-            rc = b64x_session_decode(d->c.sess, total, &d->abc, 0, &res);
-            if (rc)
-                return stage_fail(&d->c, rc);
-        } else {
-            rc = b64x_session_decode(d->c.sess, total, &d->abc,
-                                     B64X_DEC_HOLD_TAIL, &res);
-            if (rc)
-                return stage_fail(&d->c, rc);
-            d->ncarry = res.tail_n;
-            for (unsigned i = 0; i < res.tail_n; i++)
-                d->carry[i] = spell_sextet(&d->abc, res.tail[i]);
-        }
-        d->c.out = b64x_session_host_out(d->c.sess);
-        d->c.out_pos = 0;
-        d->c.out_len = (size_t) res.out_len;
-    }
+    return stage_read(&d->st, buf, count);
 }
 
 void base64decoder_close(base64decoder_t *d)
 {
-    bytestream_1_close(d->stream);
-    b64x_session_close(d->c.sess);
-    d->c.sess = NULL;
-    async_wound(d->async, d);
-    d->async = NULL;
+    stage_close(&d->st);
 }
 
 void base64decoder_register_callback(base64decoder_t *d, action_1 action)
 {
-    bytestream_1_register_callback(d->stream, action);
+    stage_register(&d->st, action);
 }
 
 void base64decoder_unregister_callback(base64decoder_t *d)
 {
-    bytestream_1_unregister_callback(d->stream);
+    stage_unregister(&d->st);
 }
 
 static ssize_t dec_read_vt(void *o, void *buf, size_t count)

@@ -872,14 +872,15 @@ struct DecodeWs {
     uint64_t *bases;
 };
 
-DEV DecodeWs ws_view(void *ws)
+// Layout for `nranges` ranges: 64-byte header, counts, bases.
+DEV DecodeWs ws_view(void *ws, uint32_t nranges)
 {
     DecodeWs w;
     uint8_t *p = (uint8_t *) ws;
     w.fd = (uint64_t *) p;
     w.fd_cur = (uint64_t *) (p + 8);
     w.counts = (uint32_t *) (p + 64);
-    w.bases = (uint64_t *) (p + 64 + (uint64_t) kMaxRanges * 4);
+    w.bases = (uint64_t *) (p + 64 + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     return w;
 }
 
@@ -988,7 +989,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
     }
     cnt = wave_sum(cnt);
     if (lane == 0) {
-        DecodeWs v = ws_view(ws);
+        DecodeWs v = ws_view(ws, nranges);
         v.counts[r] = cnt;
         if (dirty != kNoDirty)
             atomicMax((unsigned long long *) v.fd,
@@ -1007,7 +1008,7 @@ __global__ __launch_bounds__(1024) void k_decode_scan(
     __shared__ uint8_t tab[256];
     __shared__ uint64_t wtot[16];
     build_dec_table(tab, a);
-    DecodeWs w = ws_view(ws);
+    DecodeWs w = ws_view(ws, nranges);
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     const uint64_t packed = *w.fd;
     __syncthreads();  // every thread has read fd before it is re-armed
@@ -1080,7 +1081,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
 {
-    DecodeWs w = ws_view(ws);
+    DecodeWs w = ws_view(ws, nranges);
     const uint64_t packed = *w.fd_cur;
     if (packed == 0) return;
     const uint32_t r0 = (uint32_t) (~packed >> 32);
@@ -1555,8 +1556,11 @@ uint64_t b64x_decoded_cap(uint64_t nchars) { return (nchars + 3) / 4 * 3; }
 
 uint64_t b64x_decode_workspace_size(uint64_t nchars)
 {
-    (void) nchars;
-    return 64 + (uint64_t) kMaxRanges * 12;
+    // header + counts + bases for as many ranges as any plan can use for
+    // nchars (ranges are at least one chunk; 0 = the largest input)
+    uint64_t nr = nchars ? (nchars + kChunk - 1) / kChunk : kMaxRanges;
+    if (nr > kMaxRanges) nr = kMaxRanges;
+    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8;
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
@@ -1769,12 +1773,40 @@ int b64x_fill_splitmix64(void *d_out, uint64_t n, uint64_t seed, void *stream)
 struct b64x_session {
     int device;
     hipStream_t stream;
+    hipEvent_t decoded;  // recorded after each decode's kernels
     uint64_t cap;
     uint8_t *h_in, *h_out;
+    uint8_t *d_base;     // d_in - kSessionHead
     uint8_t *d_in, *d_out;
     void *d_ws;
     b64x_dec_result *d_res, *h_res;
 };
+
+// Device headroom in front of d_in: a chained decode writes the carried
+// sextets (re-spelled as characters, right-aligned, padded on the left with
+// a character the alphabet skips) into the last kCarryHead bytes of it.
+constexpr uint64_t kSessionHead = 256;
+constexpr uint32_t kCarryHead = 16;
+
+// One wave: writes the kCarryHead-byte prefix for a decode chained after
+// the HOLD_TAIL decode whose result is *prev (ref base64decoder.c:64-76 --
+// the reference keeps those bits in decoder->bits across reads).
+__global__ void __launch_bounds__(64)
+k_spell_carry(const b64x_dec_result *__restrict__ prev, uint8_t *__restrict__ head,
+              char pos62, char pos63, uint8_t skip)
+{
+    const uint32_t i = threadIdx.x;
+    if (i >= kCarryHead) return;
+    const uint32_t n = prev->tail_n < 4 ? prev->tail_n : 0;
+    const uint32_t first = kCarryHead - n;
+    uint8_t c = skip;
+    if (i >= first) {
+        const uint32_t v = prev->tail[i - first] & 63;
+        c = v < 26 ? 'A' + v : v < 52 ? 'a' + (v - 26) : v < 62 ? '0' + (v - 52)
+          : (uint8_t) (v == 62 ? pos62 : pos63);
+    }
+    head[i] = c;
+}
 
 static uint64_t session_out_cap(uint64_t cap)
 {
@@ -1796,21 +1828,25 @@ b64x_session *b64x_session_open(uint64_t capacity)
     if (!s) return nullptr;
     s->cap = capacity;
     (void) hipGetDevice(&s->device);
-    const uint64_t ocap = session_out_cap(capacity);
+    // Decodes may carry kCarryHead extra characters in front of host_in.
+    const uint64_t ocap = session_out_cap(capacity + kCarryHead);
+    const uint64_t wsz = b64x_decode_workspace_size(capacity + kCarryHead);
     bool ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
               hipHostMalloc((void **) &s->h_in, capacity, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void **) &s->h_out, ocap, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void **) &s->h_res, sizeof(b64x_dec_result), hipHostMallocDefault) == hipSuccess &&
-              hipMalloc((void **) &s->d_in, capacity) == hipSuccess &&
+              hipEventCreateWithFlags(&s->decoded, hipEventDisableTiming) == hipSuccess &&
+              hipMalloc((void **) &s->d_base, kSessionHead + capacity) == hipSuccess &&
               hipMalloc((void **) &s->d_out, ocap) == hipSuccess &&
               hipMalloc((void **) &s->d_res, sizeof(b64x_dec_result)) == hipSuccess &&
-              hipMalloc(&s->d_ws, b64x_decode_workspace_size(capacity)) == hipSuccess &&
-              hipMemset(s->d_ws, 0, b64x_decode_workspace_size(capacity)) == hipSuccess;
+              hipMalloc(&s->d_ws, wsz) == hipSuccess &&
+              hipMemset(s->d_ws, 0, wsz) == hipSuccess;
     if (!ok) {
         b64x_session_close(s);
         errno = ENOMEM;
         return nullptr;
     }
+    s->d_in = s->d_base + kSessionHead;
     return s;
 }
 
@@ -1824,7 +1860,8 @@ void b64x_session_close(b64x_session *s)
     if (s->h_in) (void) hipHostFree(s->h_in);
     if (s->h_out) (void) hipHostFree(s->h_out);
     if (s->h_res) (void) hipHostFree(s->h_res);
-    if (s->d_in) (void) hipFree(s->d_in);
+    if (s->d_base) (void) hipFree(s->d_base);
+    if (s->decoded) (void) hipEventDestroy(s->decoded);
     if (s->d_out) (void) hipFree(s->d_out);
     if (s->d_res) (void) hipFree(s->d_res);
     if (s->d_ws) (void) hipFree(s->d_ws);
@@ -1842,15 +1879,10 @@ int b64x_session_encode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
 {
     if (!s || n > s->cap || !out_len) return -EINVAL;
     *out_len = 0;
-    if (n == 0) return 0;
     int err;
-    const uint64_t m = b64x_encoded_len(n, enc_alpha(abc).pad);
-    if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream)))) return err;
-    if ((err = b64x_encode_dev(s->d_in, n, s->d_out, abc, s->stream))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, m, hipMemcpyDeviceToHost, s->stream)))) return err;
-    if ((err = hip_err(hipStreamSynchronize(s->stream)))) return err;
-    *out_len = m;
+    if ((err = b64x_session_encode_async(s, n, abc, nullptr, nullptr))) return err;
+    if ((err = b64x_session_wait(s))) return err;
+    *out_len = n ? b64x_encoded_len(n, enc_alpha(abc).pad) : 0;
     return 0;
 }
 
@@ -1859,18 +1891,87 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
 {
     if (!s || n > s->cap || !res) return -EINVAL;
     memset(res, 0, sizeof(*res));
-    if (n == 0) return 0;
     int err;
-    if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream)))) return err;
-    if ((err = b64x_decode_dev(s->d_in, n, s->d_out, s->d_res, abc, flags, s->d_ws, s->stream))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->h_res, s->d_res, sizeof(b64x_dec_result),
-                                      hipMemcpyDeviceToHost, s->stream)))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(n),
-                                      hipMemcpyDeviceToHost, s->stream)))) return err;
-    if ((err = hip_err(hipStreamSynchronize(s->stream)))) return err;
+    if ((err = b64x_session_decode_async(s, n, abc, flags, nullptr, nullptr, nullptr))) return err;
+    if ((err = b64x_session_wait(s))) return err;
     *res = *s->h_res;
     return 0;
+}
+
+int b64x_session_encode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
+                              b64x_done_fn done, void *arg)
+{
+    if (!s || n > s->cap) return -EINVAL;
+    int err;
+    if ((err = hip_err(hipSetDevice(s->device)))) return err;
+    if (n) {
+        const uint64_t m = b64x_encoded_len(n, enc_alpha(abc).pad);
+        if ((err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream)))) return err;
+        if ((err = b64x_encode_dev(s->d_in, n, s->d_out, abc, s->stream))) return err;
+        if ((err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, m, hipMemcpyDeviceToHost, s->stream)))) return err;
+    }
+    if (done) return hip_err(hipLaunchHostFunc(s->stream, done, arg));
+    return 0;
+}
+
+// A character the decoder skips under this alphabet (ref map(),
+// base64decoder.c:38-48: not alphanumeric, not pos62/pos63).
+static uint8_t skip_char(const b64x_alphabet *abc)
+{
+    const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
+    const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
+    for (char c : {'\n', '\r', ' '})
+        if (c != p62 && c != p63) return (uint8_t) c;
+    return '\n';  // unreachable: two characters cannot shadow three
+}
+
+int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
+                              unsigned flags, const b64x_session *carry_from,
+                              b64x_done_fn done, void *arg)
+{
+    if (!s || n > s->cap || carry_from == s) return -EINVAL;
+    if (carry_from && carry_from->device != s->device) return -EINVAL;
+    int err;
+    if ((err = hip_err(hipSetDevice(s->device)))) return err;
+    const uint8_t *src = s->d_in;
+    uint64_t len = n;
+    if (n && (err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice,
+                                           s->stream))))
+        return err;
+    if (carry_from) {
+        // The H2D above overlaps carry_from's kernels; the prefix waits.
+        if ((err = hip_err(hipStreamWaitEvent(s->stream, carry_from->decoded, 0)))) return err;
+        const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
+        const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
+        hipLaunchKernelGGL(k_spell_carry, dim3(1), dim3(64), 0, s->stream,
+                           carry_from->d_res, s->d_in - kCarryHead, p62, p63, skip_char(abc));
+        if ((err = launch_status())) return err;
+        src -= kCarryHead;
+        len += kCarryHead;
+    }
+    if ((err = b64x_decode_dev(src, len, s->d_out, s->d_res, abc, flags, s->d_ws, s->stream)))
+        return err;
+    if ((err = hip_err(hipEventRecord(s->decoded, s->stream)))) return err;
+    if ((err = hip_err(hipMemcpyAsync(s->h_res, s->d_res, sizeof(b64x_dec_result),
+                                      hipMemcpyDeviceToHost, s->stream))))
+        return err;
+    // The output length is device-determined: copy the capacity bound.
+    if (len && (err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(len),
+                                             hipMemcpyDeviceToHost, s->stream))))
+        return err;
+    if (done) return hip_err(hipLaunchHostFunc(s->stream, done, arg));
+    return 0;
+}
+
+const b64x_dec_result *b64x_session_result(const b64x_session *s)
+{
+    return s ? s->h_res : nullptr;
+}
+
+int b64x_session_wait(b64x_session *s)
+{
+    if (!s) return -EINVAL;
+    return hip_err(hipStreamSynchronize(s->stream));
 }
 
 // Tuning and calibration hooks for scripts/bench_variants.py (exported,

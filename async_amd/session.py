@@ -1,0 +1,108 @@
+"""Host-memory sessions: pinned staging + H2D + GPU kernels + D2H.
+
+Python view of the ``b64x_session_*`` entry points (include/b64x.h), the
+host-memory leg the bytestream_1 stages in async_amd/csrc/b64_stages.c are
+built on.  Used by the tests and by
+scripts/bench_host_pipeline.py, which measures the PCIe-inclusive rate.
+
+    s = Session(1 << 20)
+    s.host_in[:n] = data
+    s.encode_async(n); s.wait(); chars = s.host_out[:encoded_len(n)]
+
+Chained decoding (``decode_async(..., carry_from=other)``) prepends on the
+device the sextets the other session's last HOLD_TAIL decode held back, so
+a stream of blocks can be queued without a host round trip per block.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import B64xError, DecResult, alphabet
+
+HOLD_TAIL = 1
+
+
+def _abc(abc) -> _lib.Alphabet:
+    return abc if isinstance(abc, _lib.Alphabet) else alphabet(*abc) if abc else alphabet()
+
+
+class Session:
+    """One b64x_session: a HIP stream, pinned host_in/host_out, device
+    buffers and a decode workspace, all sized for ``capacity``."""
+
+    def __init__(self, capacity: int):
+        self._L = _lib.load()
+        ctypes.set_errno(0)
+        h = self._L.b64x_session_open(capacity)
+        if not h:
+            raise B64xError("b64x_session_open", -(ctypes.get_errno() or 19))
+        self._h = ctypes.c_void_p(h)
+        self.capacity = int(self._L.b64x_session_capacity(self._h))
+        out_cap = max(4 * ((self.capacity + 16 + 2) // 3), 3 * ((self.capacity + 16 + 3) // 4))
+        self.host_in = np.ctypeslib.as_array(
+            ctypes.cast(self._L.b64x_session_host_in(self._h),
+                        ctypes.POINTER(ctypes.c_uint8)), (self.capacity,))
+        self.host_out = np.ctypeslib.as_array(
+            ctypes.cast(self._L.b64x_session_host_out(self._h),
+                        ctypes.POINTER(ctypes.c_uint8)), (out_cap,))
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            self._L.b64x_session_close(self._h)
+            self._h = None
+            self.host_in = self.host_out = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- synchronous ------------------------------------------------------
+    def encode(self, n: int, abc=None) -> int:
+        out = ctypes.c_uint64(0)
+        _lib.check("b64x_session_encode",
+                   self._L.b64x_session_encode(self._h, n, ctypes.byref(_abc(abc)),
+                                               ctypes.byref(out)))
+        return int(out.value)
+
+    def decode(self, n: int, abc=None, flags: int = 0) -> DecResult:
+        res = DecResult()
+        _lib.check("b64x_session_decode",
+                   self._L.b64x_session_decode(self._h, n, ctypes.byref(_abc(abc)), flags,
+                                               ctypes.byref(res)))
+        return res
+
+    # -- asynchronous -----------------------------------------------------
+    def encode_async(self, n: int, abc=None) -> None:
+        _lib.check("b64x_session_encode_async",
+                   self._L.b64x_session_encode_async(self._h, n, ctypes.byref(_abc(abc)),
+                                                     None, None))
+
+    def decode_async(self, n: int, abc=None, flags: int = 0,
+                     carry_from: "Session | None" = None) -> None:
+        prev = carry_from.handle if carry_from is not None else None
+        _lib.check("b64x_session_decode_async",
+                   self._L.b64x_session_decode_async(self._h, n, ctypes.byref(_abc(abc)),
+                                                     flags, prev, None, None))
+
+    def wait(self) -> None:
+        _lib.check("b64x_session_wait", self._L.b64x_session_wait(self._h))
+
+    def result(self) -> DecResult:
+        """Copy of the last completed decode's result (call after wait())."""
+        p = self._L.b64x_session_result(self._h)
+        return DecResult.from_buffer_copy(ctypes.string_at(p, ctypes.sizeof(DecResult)))

@@ -153,6 +153,34 @@ int b64x_session_decode(b64x_session *s, uint64_t n,
                         const b64x_alphabet *abc, unsigned flags,
                         b64x_dec_result *res);
 
+/* Completion callback of the asynchronous session calls.  It runs on a HIP
+ * runtime thread and must not call HIP; it should only signal (set a flag,
+ * write an eventfd). */
+typedef void (*b64x_done_fn)(void *arg);
+
+/* Asynchronous forms of b64x_session_encode/_decode: enqueue H2D, kernels
+ * and D2H on the session's stream and return at once.  `done(arg)` (may be
+ * NULL) runs once host_out -- and, for decode, b64x_session_result() -- hold
+ * the results.  One call in flight per session. */
+int b64x_session_encode_async(b64x_session *s, uint64_t n,
+                              const b64x_alphabet *abc, b64x_done_fn done,
+                              void *arg);
+/* carry_from (NULL = none): another session on the same device whose last
+ * call was a decode with B64X_DEC_HOLD_TAIL.  The sextets it held back are
+ * prepended on the device, ordered by a HIP event, so a stream of blocks
+ * can be queued before the previous block's result reaches the host.
+ * Alternate two sessions (A, B, A, ...) each naming the other: a session's
+ * next call is then ordered after the chained call that read its result.
+ * n == 0 with carry_from flushes the carried sextets alone. */
+int b64x_session_decode_async(b64x_session *s, uint64_t n,
+                              const b64x_alphabet *abc, unsigned flags,
+                              const b64x_session *carry_from,
+                              b64x_done_fn done, void *arg);
+/* The decode result of the last completed call (host memory). */
+const b64x_dec_result *b64x_session_result(const b64x_session *s);
+/* Wait for everything queued on the session. */
+int b64x_session_wait(b64x_session *s);
+
 /* ---- utilities ----------------------------------------------------------- */
 
 /* Fill n bytes with the splitmix64 stream used by every synthetic

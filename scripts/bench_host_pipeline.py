@@ -1,0 +1,151 @@
+"""PCIe-inclusive rates of the host-memory path.
+
+Two measurements, both bit-checked against the device-resident result:
+
+  sessions  K sessions round-robin over a host buffer of TOTAL bytes:
+            memcpy into pinned host_in, H2D, kernels, D2H into pinned
+            host_out (+ memcpy out), with up to K blocks in flight.  This is
+            what a caller holding host buffers gets per GPU.
+  stages    the drop-in bytestream_1 stages on the product event loop:
+            blobstream -> base64 encoder stage -> consumer (1 MiB reads), and
+            blobstream -> decoder stage -> consumer, timed end to end.
+
+Prints one JSON line per measurement.  Usage:
+    python scripts/bench_host_pipeline.py [--total MiB] [--block MiB] [--k K]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from async_amd.session import HOLD_TAIL, Session  # noqa: E402
+
+
+def splitmix(n, seed=1):
+    k = np.arange(1, (n + 7) // 8 + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.view(np.uint8)[:n]
+
+
+def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
+    """Stream src through k sessions; returns (seconds, out_len)."""
+    sess = [Session(block) for _ in range(k)]
+    step = block // 3 * 3 if op == "encode" else block
+    try:
+        # warm up every session once (allocations, code objects)
+        for s in sess:
+            s.host_in[:step] = src[:step]
+            if op == "encode":
+                s.encode(step)
+            else:
+                s.decode(step)
+        live = []  # (session, out_len or None)
+        opos = 0
+        prev = None
+        t0 = time.perf_counter()
+        pos, i = 0, 0
+        while pos < len(src) or live:
+            if pos < len(src) and len(live) < k:
+                s = sess[i % k]
+                n = min(step, len(src) - pos)
+                s.host_in[:n] = src[pos:pos + n]
+                last = pos + n == len(src)
+                if op == "encode":
+                    s.encode_async(n)
+                    m = (n + 2) // 3 * 4 if last else n // 3 * 4
+                else:
+                    s.decode_async(n, None, 0 if last else HOLD_TAIL, carry_from=prev)
+                    m = None
+                live.append((s, m))
+                prev = s
+                pos += n
+                i += 1
+                continue
+            s, m = live.pop(0)
+            s.wait()
+            if m is None:
+                m = s.result().out_len
+            out[opos:opos + m] = s.host_out[:m]
+            opos += m
+        dt = time.perf_counter() - t0
+    finally:
+        for s in sess:
+            s.close()
+    return dt, opos
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--total", type=int, default=1024, help="MiB of input bytes")
+    ap.add_argument("--block", type=int, default=32, help="MiB per session block")
+    ap.add_argument("--k", type=int, default=4, help="sessions in flight")
+    ap.add_argument("--stage-total", type=int, default=256, help="MiB through the stages")
+    args = ap.parse_args()
+
+    import torch
+    from async_amd import b64
+
+    total = args.total << 20
+    block = args.block << 20
+    src = splitmix(total)
+    # Device-resident reference result for the bit check.
+    ref_chars = b64.encode(torch.from_numpy(src).cuda()).cpu().numpy()
+    chars = np.empty(len(ref_chars), np.uint8)
+    dt, m = run_sessions(src, block, args.k, "encode", chars)
+    ok = m == len(ref_chars) and np.array_equal(chars, ref_chars)
+    print(json.dumps({"measure": "sessions_encode", "bytes": total, "block": block,
+                      "k": args.k, "seconds": dt, "GiB_s": total / dt / 2**30,
+                      "exact": bool(ok)}), flush=True)
+    back = np.empty(total + 16, np.uint8)
+    dt, m = run_sessions(ref_chars, block, args.k, "decode", back)
+    ok = m == total and np.array_equal(back[:m], src)
+    print(json.dumps({"measure": "sessions_decode", "chars": len(ref_chars), "bytes": m,
+                      "block": block, "k": args.k, "seconds": dt,
+                      "GiB_s": m / dt / 2**30, "exact": bool(ok)}), flush=True)
+
+    # The bytestream_1 stages on the product loop (tests/csrc harness).
+    from tests import util
+    st_total = args.stage_total << 20
+    data = src[:st_total]
+    raw = data.tobytes()
+    st_chars = b64.encode(torch.from_numpy(data).cuda()).cpu().numpy()
+    L = util.harness()
+    ecap = (st_total + 2) // 3 * 4 + 16
+    out = np.empty(ecap, np.uint8)
+    err = ctypes.c_int(0)
+    for rs in (1 << 20, 64 << 10):
+        t0 = time.perf_counter()
+        n = L.h_encode_stream(raw, st_total, 0, rs, b"\xff", b"\xff", 1, b"\xff",
+                              out.ctypes.data, ecap, ctypes.byref(err))
+        dt = time.perf_counter() - t0
+        ok = n == len(st_chars) and np.array_equal(out[:n], st_chars)
+        print(json.dumps({"measure": "stage_encode", "bytes": st_total, "read_size": rs,
+                          "capacity": int(os.environ.get("ASYNC_B64_STAGE_CAPACITY", 1 << 20)),
+                          "seconds": dt, "GiB_s": st_total / dt / 2**30,
+                          "exact": bool(ok), "err": err.value}), flush=True)
+        enc = out[:n].tobytes()
+        dout = np.empty(st_total + 16, np.uint8)
+        t0 = time.perf_counter()
+        n2 = L.h_decode_stream(enc, len(enc), 0, rs, b"\xff", b"\xff",
+                               dout.ctypes.data, dout.size, ctypes.byref(err))
+        dt = time.perf_counter() - t0
+        ok = n2 == st_total and np.array_equal(dout[:n2], data)
+        print(json.dumps({"measure": "stage_decode", "bytes": st_total, "read_size": rs,
+                          "seconds": dt, "GiB_s": st_total / dt / 2**30,
+                          "exact": bool(ok), "err": err.value}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,138 @@
+"""Host-memory sessions (include/b64x.h b64x_session_*) and the pipelined
+stages built on them: asynchronous calls,
+device-chained decode carries, and stages forced through many small
+blocks so every carry length crosses a block seam."""
+import numpy as np
+import pytest
+
+from async_amd.session import HOLD_TAIL, Session
+from oracle import pyoracle as orc
+from tests import util
+
+pytestmark = pytest.mark.gpu
+
+
+def _dirty(rng, n, pad=True, abc=(-1, -1)):
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    chars = orc.encode(data, abc[0], abc[1], pad)
+    sep = b"  " if "\n" in abc else b"\r\n"  # junk for this alphabet
+    return sep.join(chars[i:i + 76] for i in range(0, len(chars), 76))
+
+
+def _chained_decode(blocks, abc=(-1, -1), cap=None):
+    """Decode `blocks` through two alternating sessions, queueing each block
+    before the previous one's result is back on the host."""
+    cap = cap or max(64, max((len(b) for b in blocks), default=0))
+    out = []
+    with Session(cap) as a, Session(cap) as b:
+        ss = (a, b)
+        pending = []
+        prev = None
+        for i, blk in enumerate(blocks + [b""]):
+            s = ss[i % 2]
+            if pending and pending[0] is s:  # refilling s: wait for its last call
+                s.wait()
+                out.append(bytes(s.host_out[:s.result().out_len]))
+                pending.pop(0)
+            s.host_in[:len(blk)] = np.frombuffer(blk, np.uint8)
+            last = i == len(blocks)
+            s.decode_async(len(blk), abc + (True, -1), 0 if last else HOLD_TAIL,
+                           carry_from=prev)
+            pending.append(s)
+            prev = s
+        for s in pending:
+            s.wait()
+            out.append(bytes(s.host_out[:s.result().out_len]))
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_chained_decode_matches_oracle(seed):
+    rng = np.random.default_rng(seed)
+    abc = [(-1, -1), ("-", "_"), ("\n", "\r"), (".", "_")][seed % 4]
+    stream = _dirty(rng, int(rng.integers(0, 200000)), bool(seed % 2), abc)
+    if seed == 3:
+        stream = b"QQ=" + stream + b"==Q"
+    cuts = np.sort(rng.integers(0, len(stream) + 1, int(rng.integers(1, 40))))
+    blocks = [stream[i:j] for i, j in zip([0, *cuts], [*cuts, len(stream)])]
+    assert _chained_decode(blocks, abc) == orc.decode(stream, *abc)
+
+
+def test_chained_decode_every_carry_length():
+    """Blocks of 1..7 characters: every tail_n value, empty blocks, and
+    carries that pass through blocks holding only junk."""
+    rng = np.random.default_rng(7)
+    stream = _dirty(rng, 3000)
+    pos, blocks = 0, []
+    while pos < len(stream):
+        k = int(rng.integers(0, 8))
+        blocks.append(stream[pos:pos + k])
+        pos += k
+    blocks.insert(3, b"\r\n\r\n")
+    assert _chained_decode(blocks, cap=64) == orc.decode(stream)
+
+
+def test_encode_async_blocks():
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, 500001, dtype=np.uint8).tobytes()
+    abc = ("-", "_", True, "#")
+    out = []
+    with Session(1 << 17) as a, Session(1 << 17) as b:
+        ss, pos, i, live = (a, b), 0, 0, []
+        while pos < len(data):
+            s = ss[i % 2]
+            if live and live[0][0] is s:
+                _, m = live.pop(0)
+                s.wait()
+                out.append(bytes(s.host_out[:m]))
+            n = min(len(data) - pos, (1 << 17) // 3 * 3)
+            s.host_in[:n] = np.frombuffer(data[pos:pos + n], np.uint8)
+            s.encode_async(n, abc)
+            m = (n + 2) // 3 * 4 if pos + n == len(data) else n // 3 * 4
+            live.append((s, m))
+            pos += n
+            i += 1
+        for s, m in live:
+            s.wait()
+            out.append(bytes(s.host_out[:m]))
+    assert b"".join(out) == orc.encode(data, *abc)
+
+
+def test_session_sync_roundtrip_and_capacity():
+    with Session(4096) as s:
+        data = bytes(range(256)) * 12
+        s.host_in[:3072] = np.frombuffer(data, np.uint8)
+        m = s.encode(3072)
+        assert bytes(s.host_out[:m]) == orc.encode(data)
+        chars = bytes(s.host_out[:m])
+        s.host_in[:m] = np.frombuffer(chars, np.uint8)
+        r = s.decode(m)
+        assert r.out_len == 3072 and bytes(s.host_out[:3072]) == data
+        with pytest.raises(Exception):
+            s.encode(4097)
+
+
+@pytest.mark.parametrize("cap", [64, 100, 1000])
+@pytest.mark.parametrize("read_size", [1, 7, 200])
+def test_stages_many_small_blocks(monkeypatch, cap, read_size):
+    """Stages with tiny slots: thousands of chained blocks, both slots in
+    flight, carries across every seam."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    monkeypatch.setenv("ASYNC_B64_MIN_PULL", "1")
+    rng = np.random.default_rng(cap + read_size)
+    data = rng.integers(0, 256, 20011, dtype=np.uint8).tobytes()
+    got, err = util.stage_encode(data, 37, read_size, ".", "_", True, "-")
+    assert err == 0 and got == orc.encode(data, ".", "_", True, "-")
+    dirty = b"\r\n".join(got[i:i + 61] for i in range(0, len(got), 61))
+    back, err = util.stage_decode(dirty, 29, read_size, ".", "_")
+    assert err == 0 and back == data
+
+
+def test_reference_topology_small_slots(monkeypatch):
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", "4096")
+    monkeypatch.setenv("ASYNC_B64_MIN_PULL", "1")
+    res, err, eagains = util.stage_reftest(100003)
+    assert err == 0 and res is not None
+    enc, dec = res
+    assert enc == orc.encode(util.counting(100003).tobytes(), ".", "_", True, "-")
+    assert dec == util.counting(100003).tobytes()
