@@ -28,7 +28,8 @@ HARNESS  = tests/csrc/libstage_harness.so
 OBJDIR   = build
 
 KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
-HOST_SRC   = async_amd/csrc/loop.c async_amd/csrc/streams.c async_amd/csrc/b64_stages.c
+HOST_SRC   = async_amd/csrc/loop.c async_amd/csrc/streams.c async_amd/csrc/framing.c \
+             async_amd/csrc/b64_hub.c async_amd/csrc/b64_stages.c
 HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
@@ -41,13 +42,13 @@ $(OBJDIR):
 $(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) | $(OBJDIR)
+$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h | $(OBJDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
 
-$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_stages.o
+$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_hub.o $(OBJDIR)/b64_stages.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64_core.so
 
 $(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h

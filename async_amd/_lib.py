@@ -85,6 +85,12 @@ SIGNATURES = {
     "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp, _vp]),
     "b64x_session_result": (ctypes.POINTER(DecResult), [_vp]),
     "b64x_session_wait": (_int, [_vp]),
+    "b64x_host_alloc": (_vp, [_u64]),
+    "b64x_host_free": (None, [_vp]),
+    "b64x_lane_open": (_vp, []),
+    "b64x_lane_close": (None, [_vp]),
+    "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp, _vp]),
+    "b64x_lane_wait": (_int, [_vp]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),
     "b64x_build_info": (ctypes.c_char_p, []),

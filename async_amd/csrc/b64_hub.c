@@ -1,0 +1,430 @@
+/*
+ * b64_hub.c -- cross-stream batching of encoder blocks (see b64_hub.h).
+ *
+ * Life of an arena ("batch"):
+ *
+ *   FREE --reserve--> FILLING --full / end of loop turn--> READY
+ *        --lane free--> INFLIGHT --HIP host fn + eventfd--> DONE
+ *        --every job's ticket released--> FREE (kept for reuse)
+ *
+ * All of it runs on the loop's thread except batch_done(), which only
+ * publishes the flag and writes the eventfd.  The registry that maps an
+ * async_t to its hub is the only state shared between threads (loops on
+ * different threads each get their own hub) and is mutex-protected.
+ */
+#define _GNU_SOURCE
+#include "b64_hub.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
+enum {
+    HUB_LANES = 4,          /* batches in flight per loop */
+    HUB_MAX_FREE = 8,       /* idle arenas kept for reuse */
+    HUB_JOBS = 1 << 16,     /* jobs per arena */
+};
+
+typedef enum { B_FREE, B_FILLING, B_READY, B_INFLIGHT, B_DONE } batch_state;
+
+struct b64_batch {
+    b64_hub *hub;
+    b64_batch *next;             /* ready / free list */
+    uint8_t *h_in, *h_out;       /* pinned arenas */
+    uint64_t *h_in_off, *h_out_off; /* pinned, HUB_JOBS + 1 each */
+    b64_ticket **jobs;
+    size_t in_cap, out_cap;
+    size_t in_used, out_used;
+    uint32_t njobs;
+    unsigned refs;               /* tickets still holding a job */
+    b64x_alphabet abc;
+    batch_state state;
+    atomic_int done;
+    int err;
+};
+
+struct b64_hub {
+    async_t *async;
+    b64_hub *next_hub;           /* registry */
+    unsigned users;
+    int efd;
+    b64x_lane *lanes[HUB_LANES];
+    b64_batch *running[HUB_LANES];
+    b64_batch *filling;
+    b64_batch *ready, *ready_tail;
+    b64_batch *free_list;
+    unsigned nfree, inflight;
+    size_t batch_bytes;
+    bool flush_scheduled, in_wake, doomed;
+    action_1 *wakes;             /* scratch for hub_wake() */
+    size_t nwakes, wakes_cap;
+};
+
+static pthread_mutex_t registry_lock = PTHREAD_MUTEX_INITIALIZER;
+static b64_hub *registry;
+
+static size_t env_bytes(const char *name, size_t dflt, size_t lo)
+{
+    const char *v = getenv(name);
+    if (!v || !*v)
+        return dflt;
+    char *end = NULL;
+    unsigned long long x = strtoull(v, &end, 0);
+    return (!end || *end || x < lo) ? dflt : (size_t) x;
+}
+
+/* ---------------------------------------------------------------- batches */
+
+static void batch_free(b64_batch *b)
+{
+    b64x_host_free(b->h_in);
+    b64x_host_free(b->h_out);
+    b64x_host_free(b->h_in_off);
+    b64x_host_free(b->h_out_off);
+    free(b->jobs);
+    free(b);
+}
+
+static b64_batch *batch_new(b64_hub *h, size_t in_cap)
+{
+    b64_batch *b = calloc(1, sizeof *b);
+    if (!b)
+        return NULL;
+    b->hub = h;
+    b->in_cap = in_cap;
+    /* per job at most 4 characters beyond 4n/3 */
+    b->out_cap = (in_cap + 2) / 3 * 4 + 4 * (size_t) HUB_JOBS;
+    b->h_in = b64x_host_alloc(in_cap);
+    b->h_out = b64x_host_alloc(b->out_cap);
+    b->h_in_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
+    b->h_out_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
+    b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
+    if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->jobs) {
+        batch_free(b);
+        errno = ENOMEM;
+        return NULL;
+    }
+    return b;
+}
+
+static void batch_recycle(b64_hub *h, b64_batch *b)
+{
+    b->state = B_FREE;
+    b->in_used = b->out_used = 0;
+    b->njobs = 0;
+    b->err = 0;
+    atomic_store_explicit(&b->done, 0, memory_order_relaxed);
+    if (h->nfree < HUB_MAX_FREE) {
+        b->next = h->free_list;
+        h->free_list = b;
+        h->nfree++;
+    } else {
+        batch_free(b);
+    }
+}
+
+static b64_batch *batch_get(b64_hub *h, size_t need)
+{
+    for (b64_batch **p = &h->free_list; *p; p = &(*p)->next) {
+        if ((*p)->in_cap >= need) {
+            b64_batch *b = *p;
+            *p = b->next;
+            h->nfree--;
+            return b;
+        }
+    }
+    return batch_new(h, need > h->batch_bytes ? need : h->batch_bytes);
+}
+
+/* HIP runtime thread. */
+static void batch_done(void *arg)
+{
+    b64_batch *b = arg;
+    atomic_store_explicit(&b->done, 1, memory_order_release);
+    uint64_t one = 1;
+    ssize_t rc = write(b->hub->efd, &one, sizeof one);
+    (void) rc;
+}
+
+/* ------------------------------------------------------------ scheduling */
+
+static void seal(b64_hub *h)
+{
+    b64_batch *b = h->filling;
+    if (!b)
+        return;
+    h->filling = NULL;
+    b->state = B_READY;
+    b->next = NULL;
+    if (h->ready_tail)
+        h->ready_tail->next = b;
+    else
+        h->ready = b;
+    h->ready_tail = b;
+}
+
+static void launch_ready(b64_hub *h)
+{
+    for (int i = 0; i < HUB_LANES && h->ready; i++) {
+        if (h->running[i])
+            continue;
+        b64_batch *b = h->ready;
+        h->ready = b->next;
+        if (!h->ready)
+            h->ready_tail = NULL;
+        b->state = B_INFLIGHT;
+        h->running[i] = b;
+        h->inflight++;
+        int rc = 0;
+        if (!h->lanes[i] && !(h->lanes[i] = b64x_lane_open()))
+            rc = -(errno ? errno : ENODEV);
+        if (!rc)
+            rc = b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
+                                        b->h_out, b->h_out_off, &b->abc, batch_done, b);
+        if (rc) { /* report through the normal completion path */
+            b->err = rc;
+            batch_done(b);
+        }
+    }
+}
+
+static void hub_destroy(b64_hub *h);
+
+static void hub_flush(b64_hub *h)
+{
+    h->flush_scheduled = false;
+    if (h->doomed) {
+        hub_destroy(h);
+        return;
+    }
+    if (h->filling && h->filling->njobs)
+        seal(h);
+    launch_ready(h);
+}
+
+static void schedule_flush(b64_hub *h)
+{
+    if (h->flush_scheduled)
+        return;
+    h->flush_scheduled = true;
+    async_execute(h->async, (action_1) { h, (act_1) hub_flush });
+}
+
+static void push_wake(b64_hub *h, action_1 a)
+{
+    if (h->nwakes == h->wakes_cap) {
+        size_t cap = h->wakes_cap ? 2 * h->wakes_cap : 64;
+        action_1 *w = realloc(h->wakes, cap * sizeof *w);
+        if (!w)
+            abort();
+        h->wakes = w;
+        h->wakes_cap = cap;
+    }
+    h->wakes[h->nwakes++] = a;
+}
+
+/* A finished batch: publish every live job's output. */
+static void complete(b64_hub *h, b64_batch *b, bool collect)
+{
+    for (uint32_t j = 0; j < b->njobs; j++) {
+        b64_ticket *t = b->jobs[j];
+        if (!t)
+            continue;
+        t->out = b->h_out + b->h_out_off[j];
+        t->err = b->err;
+        atomic_store_explicit(&t->done, 1, memory_order_release);
+        if (collect)
+            push_wake(h, t->wake);
+    }
+    b->state = B_DONE;
+    if (b->refs == 0)
+        batch_recycle(h, b);
+}
+
+static void hub_wake(b64_hub *h)
+{
+    uint64_t v;
+    while (read(h->efd, &v, sizeof v) == (ssize_t) sizeof v)
+        ;
+    h->in_wake = true;
+    h->nwakes = 0;
+    for (int i = 0; i < HUB_LANES; i++) {
+        b64_batch *b = h->running[i];
+        if (b && atomic_load_explicit(&b->done, memory_order_acquire)) {
+            h->running[i] = NULL;
+            h->inflight--;
+            complete(h, b, true);
+        }
+    }
+    launch_ready(h);
+    /* Callbacks may close stages (and release tickets) or read again
+     * (and reserve): the wake list is the hub's own scratch, so copy out
+     * nothing but run them in order; no batch pointer is used below. */
+    size_t n = h->nwakes;
+    for (size_t i = 0; i < n; i++)
+        action_1_perf(h->wakes[i]);
+    h->in_wake = false;
+    if (h->doomed && !h->flush_scheduled)
+        hub_destroy(h);
+}
+
+/* ------------------------------------------------------------- lifecycle */
+
+b64_hub *b64_hub_acquire(async_t *async)
+{
+    pthread_mutex_lock(&registry_lock);
+    for (b64_hub *h = registry; h; h = h->next_hub) {
+        if (h->async == async && !h->doomed) {
+            h->users++;
+            pthread_mutex_unlock(&registry_lock);
+            return h;
+        }
+    }
+    b64_hub *h = calloc(1, sizeof *h);
+    if (!h) {
+        pthread_mutex_unlock(&registry_lock);
+        errno = ENOMEM;
+        return NULL;
+    }
+    h->async = async;
+    h->batch_bytes = env_bytes("ASYNC_B64_BATCH_BYTES", (size_t) 16 << 20, 4096);
+    h->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (h->efd < 0 ||
+        async_register(async, h->efd, (action_1) { h, (act_1) hub_wake }) < 0) {
+        int e = errno ? errno : EIO;
+        if (h->efd >= 0)
+            close(h->efd);
+        free(h);
+        pthread_mutex_unlock(&registry_lock);
+        errno = e;
+        return NULL;
+    }
+    h->users = 1;
+    h->next_hub = registry;
+    registry = h;
+    pthread_mutex_unlock(&registry_lock);
+    return h;
+}
+
+static void hub_destroy(b64_hub *h)
+{
+    pthread_mutex_lock(&registry_lock);
+    for (b64_hub **p = &registry; *p; p = &(*p)->next_hub) {
+        if (*p == h) {
+            *p = h->next_hub;
+            break;
+        }
+    }
+    pthread_mutex_unlock(&registry_lock);
+    for (int i = 0; i < HUB_LANES; i++) {
+        if (h->running[i]) { /* teardown: wait, do not wake anyone */
+            (void) b64x_lane_wait(h->lanes[i]);
+            b64_batch *b = h->running[i];
+            h->running[i] = NULL;
+            batch_free(b);
+        }
+        b64x_lane_close(h->lanes[i]);
+    }
+    if (h->filling)
+        batch_free(h->filling);
+    while (h->ready) {
+        b64_batch *b = h->ready;
+        h->ready = b->next;
+        batch_free(b);
+    }
+    while (h->free_list) {
+        b64_batch *b = h->free_list;
+        h->free_list = b->next;
+        batch_free(b);
+    }
+    (void) async_unregister(h->async, h->efd);
+    close(h->efd);
+    free(h->wakes);
+    free(h);
+}
+
+void b64_hub_release(b64_hub *h)
+{
+    if (!h || --h->users)
+        return;
+    pthread_mutex_lock(&registry_lock);
+    h->doomed = true; /* no new stage may pick it up */
+    pthread_mutex_unlock(&registry_lock);
+    if (!h->in_wake && !h->flush_scheduled)
+        hub_destroy(h);
+}
+
+/* -------------------------------------------------------------- the API */
+
+uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
+                         size_t min_room, size_t *granted)
+{
+    if (min_room > room)
+        min_room = room;
+    b64_batch *b = h->filling;
+    if (b && (memcmp(&b->abc, abc, sizeof *abc) || b->njobs == HUB_JOBS ||
+              b->in_cap - b->in_used < (min_room ? min_room : 1))) {
+        if (b->njobs) {
+            seal(h);
+            launch_ready(h);
+        }
+        b = h->filling; /* NULL after seal; kept if it was empty */
+        if (b && (b->in_cap < room || memcmp(&b->abc, abc, sizeof *abc))) {
+            h->filling = NULL;
+            batch_recycle(h, b);
+            b = NULL;
+        }
+    }
+    if (!b) {
+        b = batch_get(h, room);
+        if (!b)
+            return NULL;
+        b->state = B_FILLING;
+        b->abc = *abc;
+        h->filling = b;
+    }
+    size_t avail = b->in_cap - b->in_used;
+    *granted = room < avail ? room : avail;
+    return b->h_in + b->in_used;
+}
+
+void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
+                    action_1 wake)
+{
+    b64_batch *b = h->filling;
+    uint32_t j = b->njobs++;
+    b->h_in_off[j] = b->in_used;
+    b->in_used += n;
+    b->h_in_off[j + 1] = b->in_used;
+    b->h_out_off[j] = b->out_used;
+    b->out_used += out_len;
+    b->h_out_off[j + 1] = b->out_used;
+    b->jobs[j] = t;
+    b->refs++;
+    t->batch = b;
+    t->index = j;
+    t->err = 0;
+    t->out = NULL;
+    t->wake = wake;
+    atomic_store_explicit(&t->done, 0, memory_order_relaxed);
+    schedule_flush(h);
+}
+
+void b64_hub_cancel(b64_hub *h)
+{
+    (void) h; /* nothing was recorded */
+}
+
+void b64_ticket_release(b64_ticket *t)
+{
+    b64_batch *b = t->batch;
+    if (!b)
+        return;
+    t->batch = NULL;
+    b->jobs[t->index] = NULL;
+    if (--b->refs == 0 && b->state == B_DONE)
+        batch_recycle(b->hub, b);
+}

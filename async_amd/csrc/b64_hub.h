@@ -1,0 +1,62 @@
+/*
+ * b64_hub.h -- internal: cross-stream batching of encoder blocks for one
+ * event loop.
+ *
+ * Every base64 encoder stage on an async_t shares one hub.  A stage
+ * reserves room in the hub's open pinned arena, reads its upstream
+ * straight into it, and commits the block as a job; the hub launches the
+ * arena as one ragged batch (b64x_lane_encode_async: H2D, one kernel, D2H)
+ * when the arena fills or at the end of the current loop turn, on up to
+ * B64_HUB_LANES concurrent HIP streams.  Completion comes back through one
+ * eventfd registered with async_register(); the hub marks each job's
+ * ticket done and calls the stage's wake action.
+ *
+ * Many small messages (config 5: Zipf 64 B - 1 MiB) thus cost one launch
+ * and two copies per arena instead of per message.
+ */
+#ifndef ASYNC_AMD_B64_HUB_H
+#define ASYNC_AMD_B64_HUB_H
+
+#include <stdatomic.h>
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "action_1.h"
+#include "async.h"
+#include "b64x.h"
+
+typedef struct b64_hub b64_hub;
+typedef struct b64_batch b64_batch;
+
+/* One committed block, owned by the stage. */
+typedef struct {
+    b64_batch *batch;      /* NULL when idle */
+    uint32_t index;        /* job index in the batch */
+    atomic_int done;       /* output ready (or err set) */
+    int err;               /* negative errno if the batch failed */
+    const uint8_t *out;    /* the block's characters, valid once done */
+    action_1 wake;         /* performed on the loop when done */
+} b64_ticket;
+
+/* The hub for `async` (created on first use); NULL + errno on failure. */
+b64_hub *b64_hub_acquire(async_t *async);
+/* A stage is gone; the last release tears the hub down (waiting for its
+ * batches still in flight). */
+void b64_hub_release(b64_hub *h);
+
+/* Room for one block of at most `room` bytes, at least `min_room`, encoded
+ * with `abc`; returns where to write it, or NULL + errno.  *granted gets
+ * the room actually given.  Must be followed by commit or cancel before
+ * control returns to the loop. */
+uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
+                         size_t min_room, size_t *granted);
+/* Turn the reservation into a job of n bytes -> out_len characters. */
+void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
+                    action_1 wake);
+void b64_hub_cancel(b64_hub *h);
+/* The stage is done with the ticket (consumed, or closing before the
+ * batch finished: its output is then discarded). */
+void b64_ticket_release(b64_ticket *t);
+
+#endif /* ASYNC_AMD_B64_HUB_H */

@@ -34,18 +34,21 @@
  *    empty flush) is decoded without HOLD_TAIL, giving the reference's
  *    floor(6V/8) bytes overall.
  *
- * The byte stream each stage produces is the reference's, byte for byte.
- * Per-call counts differ: a stage returns what it has finished, and
- * returns -1/EAGAIN while the GPU is busy (a consumer written for the
- * reference already handles EAGAIN from any stream).  Upstream errors are
- * passed through with all state kept when nothing is in flight; count ==
- * 0 returns 0 (ref :103-104, :54-55).  The reference's assert at
- * src/base64encoder.c:140 (counts not divisible by 4) has no counterpart.
- * With no usable GPU the first read fails with ENODEV: there is no CPU
- * path.
+ * The byte stream each stage produces is the reference's, byte for byte,
+ * and the encoder's per-read counts are too whenever upstream keeps up
+ * (see stage_read()); while blocks are on the GPU a read returns -1/EAGAIN
+ * (a consumer written for the reference already handles EAGAIN from any
+ * stream).  Upstream errors are passed through with all state kept when
+ * nothing is in flight; count == 0 returns 0 (ref :103-104, :54-55).  The
+ * reference's assert at src/base64encoder.c:140 (counts not divisible by
+ * 4) has no counterpart.  With no usable GPU the first read fails with
+ * ENODEV: there is no CPU path.
  *
  * Tuning (environment, read when a stage is created):
- *   ASYNC_B64_STAGE_CAPACITY  staging bytes per slot (default 1 MiB)
+ *   ASYNC_B64_STAGE_CAPACITY  staging bytes per slot (default 1 MiB; the
+ *                             encoder grows it to hold its first read's
+ *                             count, up to ASYNC_B64_STAGE_MAX_CAPACITY,
+ *                             default 64 MiB)
  *   ASYNC_B64_MIN_PULL        gather at least this much from upstream
  *                             before launching, unless it runs dry
  *                             (default 64 KiB)
@@ -60,6 +63,7 @@
 #include <unistd.h>
 
 #include "async.h"
+#include "b64_hub.h"
 #include "b64x.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
@@ -70,9 +74,14 @@ typedef struct stage stage;
 
 typedef struct {
     stage *owner;
-    b64x_session *sess;
-    atomic_int done;  /* set by the HIP host function */
-    size_t out_pos, out_len;
+    b64x_session *sess; /* decoder: this slot's session */
+    b64_ticket ticket;  /* encoder: this slot's job in a hub batch */
+    atomic_int done;    /* decoder: set by the HIP host function */
+    bool resolved;    /* out_len/body_end valid (decoder: after done) */
+    size_t out_pos;
+    size_t body_end;  /* encoder: end of the full sextets; the finalize
+                         characters after it are served on their own */
+    size_t out_len;
 } slot;
 
 typedef enum { DIR_ENCODE, DIR_DECODE } direction;
@@ -83,15 +92,18 @@ struct stage {
     action_1 cb;        /* the consumer's callback, or NULL_ACTION_1 */
     direction dir;
     b64x_alphabet abc;
-    size_t cap, min_pull;
-    int efd;            /* GPU completion -> loop */
-    bool started;       /* sessions + eventfd exist */
+    size_t cap, min_pull, max_cap;
+    b64_hub *hub;       /* encoder: the loop's batching hub */
+    int efd;            /* decoder: GPU completion -> loop */
+    bool started;       /* hub / sessions + eventfd exist */
     int err;            /* sticky failure errno, 0 while healthy */
     slot slots[NSLOTS];
     unsigned head;      /* oldest busy slot */
     unsigned nbusy;     /* launched, output not fully served */
     bool final_queued;  /* the last block (or nothing) has been launched */
     bool launched_any;
+    bool short_seen;    /* an upstream read came up short (not EAGAIN)
+                           since the staged output last ran out */
     uint8_t carry[2];   /* encoder: bytes of the incomplete group */
     size_t ncarry;
 };
@@ -119,6 +131,7 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->abc = abc;
     st->cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
     st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
+    st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
     st->efd = -1;
     for (int i = 0; i < NSLOTS; i++)
         st->slots[i].owner = st;
@@ -150,10 +163,33 @@ static void slot_done(void *arg)
     (void) rc; /* EAGAIN only when the counter is saturated: still readable */
 }
 
-static int stage_start(stage *st)
+/* Hub completion of one of this stage's blocks (on the loop). */
+static void stage_notify(stage *st)
+{
+    action_1_perf(st->cb);
+}
+
+static int stage_start(stage *st, size_t count)
 {
     if (st->started)
         return 0;
+    if (st->dir == DIR_ENCODE) {
+        /* A fresh block must be able to hold a full read (see
+         * stage_read()); blocks go to the loop's hub. */
+        size_t need = (count + 3) / 4 * 3 + 3;
+        if (need > st->max_cap)
+            need = st->max_cap;
+        if (need > st->cap)
+            st->cap = need;
+        int rc = b64x_device_check(); /* fail loudly: no CPU path */
+        if (rc)
+            return rc;
+        st->hub = b64_hub_acquire(st->async);
+        if (!st->hub)
+            return -(errno ? errno : ENODEV);
+        st->started = true;
+        return 0;
+    }
     st->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     if (st->efd < 0)
         return -errno;
@@ -175,6 +211,12 @@ static int stage_start(stage *st)
 
 static void stage_stop(stage *st)
 {
+    if (st->hub) {
+        for (int i = 0; i < NSLOTS; i++)
+            b64_ticket_release(&st->slots[i].ticket);
+        b64_hub_release(st->hub);
+        st->hub = NULL;
+    }
     for (int i = 0; i < NSLOTS; i++) {
         if (st->slots[i].sess) {
             (void) b64x_session_wait(st->slots[i].sess);
@@ -201,6 +243,8 @@ static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
     *err = 0;
     while (got < want) {
         ssize_t n = bytestream_1_read(st->up, dst + got, room - got);
+        if (n > 0 && (size_t) n < room - got)
+            st->short_seen = true;
         if (n < 0) {
             *err = errno ? errno : EIO;
             break;
@@ -224,8 +268,23 @@ static slot *next_launch_slot(stage *st)
 static void slot_arm(stage *st, slot *sl)
 {
     atomic_store_explicit(&sl->done, 0, memory_order_relaxed);
-    sl->out_pos = sl->out_len = 0;
+    sl->resolved = false;
+    sl->out_pos = sl->body_end = sl->out_len = 0;
     st->nbusy++;
+}
+
+/* Characters finalize() emits for a last block of n bytes: the partial
+ * sextet plus padding (ref base64encoder.c:61-99). */
+static size_t finalize_len(size_t n, bool pad)
+{
+    switch (n % 3) {
+        case 1:
+            return pad ? 3 : 1;
+        case 2:
+            return pad ? 2 : 1;
+        default:
+            return 0;
+    }
 }
 
 /* Launch as many blocks as slots and upstream allow.  Returns 0, or a
@@ -235,34 +294,45 @@ static int top_up_encoder(stage *st)
 {
     slot *sl;
     while ((sl = next_launch_slot(st))) {
-        uint8_t *in = b64x_session_host_in(sl->sess);
+        /* Room in the hub's open arena: up to a full slot, but a few KiB
+         * will do (the next block gets a fresh arena and a full slot, so
+         * two slots always cover a full read). */
+        size_t room;
+        uint8_t *in = b64_hub_reserve(st->hub, &st->abc, st->cap,
+                                      st->ncarry + 4096, &room);
+        if (!in)
+            return -(errno ? errno : ENOMEM);
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;
-        size_t got = gather(st, in + st->ncarry, st->cap - st->ncarry, &eof,
+        size_t got = gather(st, in + st->ncarry, room - st->ncarry, &eof,
                             &uerr);
         size_t total = st->ncarry + got;
         size_t n;
         if (eof) {
             st->final_queued = true;
             st->ncarry = 0;
-            if (total == 0)
+            if (total == 0) {
+                b64_hub_cancel(st->hub);
                 return 0;
+            }
             n = total; /* finalize(): partial group + padding */
         } else {
             n = total - total % 3;
             st->ncarry = total - n;
             memcpy(st->carry, in + n, st->ncarry);
-            if (n == 0)
+            if (n == 0) {
+                b64_hub_cancel(st->hub);
                 return uerr ? uerr : EAGAIN;
+            }
         }
         slot_arm(st, sl);
-        int rc = b64x_session_encode_async(sl->sess, n, &st->abc, slot_done,
-                                           sl);
-        if (rc)
-            return rc;
-        sl->out_len = (size_t) b64x_encoded_len(n, eof && st->abc.pad);
         /* Non-final blocks are whole groups: no padding either way. */
+        sl->out_len = (size_t) b64x_encoded_len(n, eof && st->abc.pad);
+        b64_hub_commit(st->hub, &sl->ticket, n, sl->out_len,
+                       (action_1) { st, (act_1) stage_notify });
+        sl->body_end = sl->out_len - (eof ? finalize_len(n, st->abc.pad) : 0);
+        sl->resolved = true;
         if (uerr)
             return uerr;
     }
@@ -303,6 +373,90 @@ static int top_up_decoder(stage *st)
     return 0;
 }
 
+static int top_up(stage *st)
+{
+    return st->dir == DIR_ENCODE ? top_up_encoder(st) : top_up_decoder(st);
+}
+
+/* A finished slot's lengths (the decoder's are device-determined). */
+static bool slot_ready(slot *sl)
+{
+    if (sl->owner->dir == DIR_ENCODE)
+        return atomic_load_explicit(&sl->ticket.done, memory_order_acquire);
+    if (!atomic_load_explicit(&sl->done, memory_order_acquire))
+        return false;
+    if (!sl->resolved) {
+        sl->out_len = (size_t) b64x_session_result(sl->sess)->out_len;
+        sl->body_end = sl->out_len;
+        sl->resolved = true;
+    }
+    return true;
+}
+
+static const uint8_t *slot_out(slot *sl)
+{
+    return sl->owner->dir == DIR_ENCODE ? sl->ticket.out
+                                        : b64x_session_host_out(sl->sess);
+}
+
+static void retire_head(stage *st)
+{
+    b64_ticket_release(&st->slots[st->head].ticket);
+    st->nbusy--;
+    st->head = (st->head + 1) % NSLOTS;
+}
+
+/* Finished body characters from the head on, in order; *blocked is set
+ * when a slot still in flight ends the run. */
+static size_t staged_body(stage *st, bool *blocked)
+{
+    size_t total = 0;
+    *blocked = false;
+    for (unsigned i = 0; i < st->nbusy; i++) {
+        slot *sl = &st->slots[(st->head + i) % NSLOTS];
+        if (!slot_ready(sl)) {
+            *blocked = true;
+            break;
+        }
+        total += sl->body_end - sl->out_pos;
+        if (sl->body_end < sl->out_len)
+            break; /* finalize characters: a read of their own */
+    }
+    return total;
+}
+
+static size_t serve_body(stage *st, uint8_t *dst, size_t n)
+{
+    size_t done = 0;
+    while (done < n && st->nbusy) {
+        slot *sl = &st->slots[st->head];
+        size_t take = sl->body_end - sl->out_pos;
+        if (take > n - done)
+            take = n - done;
+        memcpy(dst + done, slot_out(sl) + sl->out_pos, take);
+        sl->out_pos += take;
+        done += take;
+        if (sl->out_pos == sl->out_len)
+            retire_head(st);
+        else if (sl->out_pos == sl->body_end)
+            break;
+    }
+    return done;
+}
+
+/*
+ * Read semantics: the reference encoder returns
+ * exactly `count` characters whenever its upstream fills the request
+ * (base64encoder.c:124-141), a short count only when upstream came up
+ * short, and the finalize() characters in a read of their own
+ * (:127-128 -> :61-99).  The encoder stage does the same -- full count or
+ * EAGAIN while blocks are in flight, a short count only when upstream has
+ * run dry (EAGAIN/EOF) and nothing is left on the GPU -- so wrappers that
+ * frame on read counts (chunkencoder) frame identically.  The decoder
+ * returns whatever is finished, up to `count` (the reference's decoder
+ * counts depend on where junk falls inside each read; no framing wrapper
+ * consumes them).
+ */
 static ssize_t stage_read(stage *st, void *buf, size_t count)
 {
     if (!count)
@@ -311,48 +465,60 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
         errno = st->err;
         return -1;
     }
-    int rc = stage_start(st);
+    int rc = stage_start(st, count);
     if (rc)
+        return stage_fail(st, rc);
+    rc = top_up(st);
+    if (rc < 0)
         return stage_fail(st, rc);
     for (;;) {
         slot *h = &st->slots[st->head];
-        if (st->nbusy &&
-            atomic_load_explicit(&h->done, memory_order_acquire)) {
-            if (st->dir == DIR_DECODE && h->out_len == 0 && h->out_pos == 0)
-                h->out_len = (size_t) b64x_session_result(h->sess)->out_len;
-            size_t avail = h->out_len - h->out_pos;
-            size_t n = avail < count ? avail : count;
-            if (n) {
-                memcpy(buf, b64x_session_host_out(h->sess) + h->out_pos, n);
-                h->out_pos += n;
-            }
-            if (h->out_pos == h->out_len) {
-                st->nbusy--;
-                st->head = (st->head + 1) % NSLOTS;
-            }
-            if (n) {
-                /* Keep the GPU busy while the consumer works. */
-                rc = st->dir == DIR_ENCODE ? top_up_encoder(st)
-                                           : top_up_decoder(st);
-                if (rc < 0)
-                    return stage_fail(st, rc);
-                return (ssize_t) n;
-            }
-            continue; /* an empty block: look at the next one */
+        if (st->nbusy && slot_ready(h) && h->ticket.err)
+            return stage_fail(st, h->ticket.err);
+        if (st->nbusy && slot_ready(h) && h->out_pos == h->body_end &&
+            h->out_pos < h->out_len) {
+            /* finalize(): partial sextet and pads, `count` at a time */
+            size_t n = h->out_len - h->out_pos;
+            if (n > count)
+                n = count;
+            memcpy(buf, slot_out(h) + h->out_pos, n);
+            h->out_pos += n;
+            if (h->out_pos == h->out_len)
+                retire_head(st);
+            return (ssize_t) n;
         }
-        rc = st->dir == DIR_ENCODE ? top_up_encoder(st) : top_up_decoder(st);
-        if (rc < 0)
-            return stage_fail(st, rc);
-        if (st->nbusy) {
-            if (atomic_load_explicit(&st->slots[st->head].done,
-                                     memory_order_acquire))
-                continue;
+        bool blocked;
+        size_t staged = staged_body(st, &blocked);
+        /* A short count only where the reference would return one: at
+         * EOF, or after upstream itself came up short (a full-or-EAGAIN
+         * upstream such as nicestream never does); or when no slot is
+         * free to pull more (a read larger than both slots). */
+        bool serve = staged >= count || (staged && st->dir == DIR_DECODE) ||
+                     (staged && !blocked &&
+                      (st->final_queued || st->short_seen || !next_launch_slot(st)));
+        if (serve) {
+            size_t n = serve_body(st, buf, staged < count ? staged : count);
+            if (n == staged)
+                st->short_seen = false;
+            rc = top_up(st); /* keep the GPU busy while the consumer works */
+            if (rc < 0)
+                return stage_fail(st, rc);
+            return (ssize_t) n;
+        }
+        if (blocked) {
             errno = EAGAIN; /* the eventfd brings the consumer back */
             return -1;
         }
+        if (st->nbusy) { /* finished slots with nothing left to serve */
+            retire_head(st);
+            rc = top_up(st);
+            if (rc < 0)
+                return stage_fail(st, rc);
+            continue;
+        }
         if (st->final_queued)
             return 0;
-        errno = rc ? rc : EAGAIN;
+        errno = rc > 0 ? rc : EAGAIN;
         return -1;
     }
 }

@@ -1974,6 +1974,112 @@ int b64x_session_wait(b64x_session *s)
     return hip_err(hipStreamSynchronize(s->stream));
 }
 
+// ------------------------------------------------------------ batch lanes --
+
+void *b64x_host_alloc(uint64_t bytes)
+{
+    void *p = nullptr;
+    if (!device_info()) return nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void b64x_host_free(void *p)
+{
+    if (p) (void) hipHostFree(p);
+}
+
+struct b64x_lane {
+    int device;
+    hipStream_t stream;
+    uint8_t *d_in, *d_out;
+    uint64_t *d_offs;
+    uint64_t in_cap, out_cap, offs_cap;  // bytes / words allocated
+};
+
+b64x_lane *b64x_lane_open(void)
+{
+    if (!device_info()) {
+        errno = ENODEV;
+        return nullptr;
+    }
+    b64x_lane *l = (b64x_lane *) calloc(1, sizeof(*l));
+    if (!l) return nullptr;
+    (void) hipGetDevice(&l->device);
+    if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) {
+        free(l);
+        errno = EIO;
+        return nullptr;
+    }
+    return l;
+}
+
+void b64x_lane_close(b64x_lane *l)
+{
+    if (!l) return;
+    (void) hipSetDevice(l->device);
+    (void) hipStreamSynchronize(l->stream);
+    if (l->d_in) (void) hipFree(l->d_in);
+    if (l->d_out) (void) hipFree(l->d_out);
+    if (l->d_offs) (void) hipFree(l->d_offs);
+    (void) hipStreamDestroy(l->stream);
+    free(l);
+}
+
+// Grow a device buffer to at least `need` (rounded up: growth is rare).
+static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need)
+{
+    if (need <= *cap) return 0;
+    uint64_t want = need + need / 4 + (1u << 20);
+    int err;
+    if ((err = hip_err(hipStreamSynchronize(l->stream)))) return err;
+    if (*buf) (void) hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    if (hipMalloc(buf, want) != hipSuccess) return -ENOMEM;
+    *cap = want;
+    return 0;
+}
+
+int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
+                           const uint64_t *h_in_off, uint8_t *h_out,
+                           const uint64_t *h_out_off, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg)
+{
+    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off))) return -EINVAL;
+    int err;
+    if ((err = hip_err(hipSetDevice(l->device)))) return err;
+    if (njobs) {
+        const uint64_t in_bytes = h_in_off[njobs], out_bytes = h_out_off[njobs];
+        const uint64_t words = (uint64_t) njobs + 1;
+        if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_out, &l->out_cap, out_bytes + 64))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, 2 * words * 8))) return err;
+        if ((err = hip_err(hipMemcpyAsync(l->d_offs, h_in_off, words * 8, hipMemcpyHostToDevice,
+                                          l->stream))) ||
+            (err = hip_err(hipMemcpyAsync(l->d_offs + words, h_out_off, words * 8,
+                                          hipMemcpyHostToDevice, l->stream))))
+            return err;
+        if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
+                                                      hipMemcpyHostToDevice, l->stream))))
+            return err;
+        if ((err = b64x_encode_batch(l->d_in, l->d_offs, njobs, l->d_out, l->d_offs + words,
+                                     abc, l->stream)))
+            return err;
+        if (out_bytes && (err = hip_err(hipMemcpyAsync(h_out, l->d_out, out_bytes,
+                                                       hipMemcpyDeviceToHost, l->stream))))
+            return err;
+    }
+    if (done) return hip_err(hipLaunchHostFunc(l->stream, done, arg));
+    return 0;
+}
+
+int b64x_lane_wait(b64x_lane *l)
+{
+    if (!l) return -EINVAL;
+    return hip_err(hipStreamSynchronize(l->stream));
+}
+
 // Tuning and calibration hooks for scripts/bench_variants.py (exported,
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)

@@ -181,6 +181,35 @@ const b64x_dec_result *b64x_session_result(const b64x_session *s);
 /* Wait for everything queued on the session. */
 int b64x_session_wait(b64x_session *s);
 
+/* ---- batch lanes (cross-stream batching of host blocks) --------------- */
+
+/* Pinned host memory for batch arenas (hipHostMalloc); NULL on failure. */
+void *b64x_host_alloc(uint64_t bytes);
+void b64x_host_free(void *p);
+
+/* A lane: one HIP stream plus device buffers that grow on demand.  It
+ * runs one ragged batch at a time out of caller-owned pinned arenas; the
+ * bytestream_1 stages pack many streams' blocks into one batch so that a
+ * launch (and its two copies) is amortised over them (SURVEY.md §8(f)
+ * row f3, ref src/queuestream.c:150-191 being the per-message feed). */
+typedef struct b64x_lane b64x_lane;
+
+b64x_lane *b64x_lane_open(void);
+void b64x_lane_close(b64x_lane *l);
+/* Encode njobs buffers: buffer i is h_in[h_in_off[i] .. h_in_off[i+1])
+ * and its b64x_encoded_len(len, abc->pad) characters go to
+ * h_out + h_out_off[i] (both offset arrays hold njobs+1 monotone entries
+ * starting at 0; the last = bytes copied each way).  All four host
+ * buffers must be pinned (b64x_host_alloc) and stay untouched until
+ * `done(arg)` has run.  Asynchronous; the lane's device buffers are grown
+ * (synchronously) when a batch needs more. */
+int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
+                           const uint64_t *h_in_off, uint8_t *h_out,
+                           const uint64_t *h_out_off, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg);
+/* Wait for everything queued on the lane. */
+int b64x_lane_wait(b64x_lane *l);
+
 /* ---- utilities ----------------------------------------------------------- */
 
 /* Fill n bytes with the splitmix64 stream used by every synthetic

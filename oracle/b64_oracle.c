@@ -15,6 +15,10 @@
  *                      oracle/README.md for what pins it)
  *   dec_read()      <- src/base64decoder.c:52-80 (decoder_read)
  *   nice_read()     <- src/nicestream.c:34-51
+ *   queue_read()    <- src/queuestream.c:150-191 over blobstream elements
+ *                      (src/blobstream.c:30-41), queue terminated
+ *   chunk_read()    <- src/chunkencoder.c:31-77 (framing), :167-191
+ *                      (max_chunk_size clamp)
  *   the reftest     <- test/asynctest-base64encoder.c:11-151
  *
  * Differences from the reference are limited to plumbing: no event loop
@@ -459,4 +463,156 @@ ssize_t orc_reftest(size_t length, uint8_t *enc_out, size_t enc_cap,
     if (tee.overflow || enc.overflow_reads)
         return -1;
     return r;
+}
+
+/* ------------------------------------------------- config-5 egress stack -- */
+
+typedef struct {
+    ostream base;
+    const uint8_t *data;
+    const size_t *lens;
+    size_t npieces, piece, off, base_off;
+} queue_source;
+
+/* queuestream do_read with every element a blobstream and the queue
+ * terminated: fill `count` across elements, dropping each at its EOF. */
+static ssize_t queue_read(ostream *s, void *buf, size_t count)
+{
+    queue_source *q = (queue_source *) s;
+    uint8_t *dst = buf;
+    size_t got = 0;
+    while (got < count && q->piece < q->npieces) {
+        size_t left = q->lens[q->piece] - q->off;
+        if (!left) { /* blobstream EOF: close and unlink the element */
+            q->base_off += q->lens[q->piece];
+            q->piece++;
+            q->off = 0;
+            continue;
+        }
+        size_t n = left < count - got ? left : count - got;
+        memcpy(dst + got, q->data + q->base_off + q->off, n);
+        q->off += n;
+        got += n;
+    }
+    return (ssize_t) got; /* 0 = terminated and empty */
+}
+
+enum { ORC_CHUNK_HEAD = 11, ORC_CHUNK_MAX = 16 * 1024 * 1024 };
+
+typedef struct {
+    ostream base;
+    ostream *up;
+    size_t max_chunk;
+    int termination;
+    uint8_t *buf;
+    size_t next, eoc, chunk_count;
+    bool eof_pending;
+} chunk_stream;
+
+static ssize_t chunk_read(ostream *s, void *buf, size_t count)
+{
+    chunk_stream *c = (chunk_stream *) s;
+    if (!count)
+        return 0;
+    if (c->next >= c->eoc) {
+        if (c->eof_pending)
+            return 0;
+        ssize_t n = c->up->read(c->up, c->buf + ORC_CHUNK_HEAD, c->max_chunk);
+        if (n < 0)
+            return n;
+        if (n == 0) {
+            c->eof_pending = true;
+            c->eoc = ORC_CHUNK_HEAD;
+            if (c->termination == 0) {
+                c->buf[c->eoc++] = '\r';
+                c->buf[c->eoc++] = '\n';
+            } else if (c->termination == 2) {
+                c->eoc -= 2;
+            }
+        } else {
+            c->eoc = ORC_CHUNK_HEAD + (size_t) n;
+        }
+        c->next = ORC_CHUNK_HEAD - 2;
+        size_t v = (size_t) n;
+        do {
+            c->buf[--c->next] = (uint8_t) "0123456789abcdef"[v % 16];
+            v /= 16;
+        } while (v);
+        if (c->chunk_count++ > 0) {
+            c->buf[--c->next] = '\n';
+            c->buf[--c->next] = '\r';
+        }
+    }
+    size_t n = c->eoc - c->next;
+    if (n > count)
+        n = count;
+    memcpy(buf, c->buf + c->next, n);
+    c->next += n;
+    return (ssize_t) n;
+}
+
+ssize_t orc_chunked_encode(const uint8_t *in, const size_t *piece_len,
+                           size_t npieces, size_t max_chunk, int termination,
+                           size_t read_size, char pos62, char pos63, int pad,
+                           char padchar, uint8_t *out, size_t out_cap)
+{
+    queue_source q = { { queue_read }, in, piece_len, npieces, 0, 0, 0 };
+    enc_stream enc;
+    enc_init(&enc, &q.base, pos62, pos63, pad != 0, padchar);
+    chunk_stream c;
+    memset(&c, 0, sizeof c);
+    c.base.read = chunk_read;
+    c.up = &enc.base;
+    c.max_chunk = max_chunk < 2 ? 2 : max_chunk > ORC_CHUNK_MAX ? ORC_CHUNK_MAX : max_chunk;
+    c.termination = termination;
+    /* +2: the encoder's overrun (assert :140) is caught, not corrupting */
+    c.buf = malloc(ORC_CHUNK_HEAD + c.max_chunk + 2);
+    if (!c.buf)
+        return -1;
+    c.buf[ORC_CHUNK_HEAD - 2] = '\r';
+    c.buf[ORC_CHUNK_HEAD - 1] = '\n';
+    ssize_t r = drain(&c.base, read_size, out, out_cap);
+    free(c.buf);
+    return enc.overflow_reads ? -1 : r;
+}
+
+typedef struct {
+    ostream base;
+    ostream *up;
+    ssize_t *log;
+    size_t cap, n;
+} count_tap;
+
+static ssize_t count_tap_read(ostream *s, void *buf, size_t count)
+{
+    count_tap *t = (count_tap *) s;
+    ssize_t n = t->up->read(t->up, buf, count);
+    if (n > 0) {
+        if (t->n < t->cap)
+            t->log[t->n] = n;
+        t->n++;
+    }
+    return n;
+}
+
+ssize_t orc_encode_counts(const uint8_t *in, size_t n, size_t src_chunk,
+                          size_t burst, size_t read_size, char pos62,
+                          char pos63, int pad, char padchar, ssize_t *counts,
+                          size_t max_counts)
+{
+    mem_source src;
+    nice_stream nice;
+    enc_stream enc;
+    ostream *up = source_chain(&src, &nice, in, n, src_chunk, burst);
+    enc_init(&enc, up, pos62, pos63, pad != 0, padchar);
+    count_tap t = { { count_tap_read }, &enc.base, counts, max_counts, 0 };
+    size_t cap = (n + 2) / 3 * 4 + 8;
+    uint8_t *out = malloc(cap);
+    if (!out)
+        return -1;
+    ssize_t r = drain(&t.base, read_size, out, cap);
+    free(out);
+    if (r < 0 || enc.overflow_reads)
+        return -1;
+    return (ssize_t) t.n;
 }

@@ -60,6 +60,24 @@ ssize_t orc_decode_stream(const uint8_t *in, size_t n, size_t src_chunk,
 ssize_t orc_reftest(size_t length, uint8_t *enc_out, size_t enc_cap,
                     size_t *enc_len, uint8_t *dec_out, size_t dec_cap);
 
+/* The config-5 egress stack: a terminated queuestream
+ * of `npieces` blobs (piece_len[i] bytes each, concatenated at `in`) ->
+ * encoder -> chunkencoder(max_chunk, termination 0/1/2 = SIMPLE /
+ * STOP_AT_TRAILER / STOP_AT_FINAL_EXTENSIONS), drained `read_size` at a
+ * time.  Returns the framed length, or -1 (assert domain / no memory). */
+ssize_t orc_chunked_encode(const uint8_t *in, const size_t *piece_len,
+                           size_t npieces, size_t max_chunk, int termination,
+                           size_t read_size, char pos62, char pos63, int pad,
+                           char padchar, uint8_t *out, size_t out_cap);
+
+/* Like orc_encode_stream(), logging the encoder's positive read returns
+ * (the first max_counts of them) -- what a counting wrapper such as the
+ * chunkencoder sees.  Returns the number of positive reads, -1 on error. */
+ssize_t orc_encode_counts(const uint8_t *in, size_t n, size_t src_chunk,
+                          size_t burst, size_t read_size, char pos62,
+                          char pos63, int pad, char padchar, ssize_t *counts,
+                          size_t max_counts);
+
 #ifdef __cplusplus
 }
 #endif

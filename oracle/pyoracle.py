@@ -42,6 +42,12 @@ def lib() -> ctypes.CDLL:
         L.orc_decode_stream.restype = _ssz
         L.orc_reftest.argtypes = [_sz, _vp, _sz, ctypes.POINTER(_sz), _vp, _sz]
         L.orc_reftest.restype = _ssz
+        L.orc_chunked_encode.argtypes = [_vp, _vp, _sz, _sz, ctypes.c_int, _sz, _ch, _ch,
+                                         ctypes.c_int, _ch, _vp, _sz]
+        L.orc_chunked_encode.restype = _ssz
+        L.orc_encode_counts.argtypes = [_vp, _sz, _sz, _sz, _sz, _ch, _ch, ctypes.c_int, _ch,
+                                        _vp, _sz]
+        L.orc_encode_counts.restype = _ssz
         _lib = L
     return _lib
 
@@ -127,3 +133,34 @@ def reftest(length: int = 1000001):
     if n < 0:
         raise RuntimeError("oracle reftest failed")
     return enc[: elen.value].tobytes(), dec[:n].tobytes()
+
+
+def chunked_encode(data, piece_lens=None, max_chunk=1 << 20, termination=0, read_size=None,
+                   pos62=-1, pos63=-1, pad=True, padchar=-1) -> bytes:
+    """The config-5 egress stack: terminated queuestream of pieces ->
+    encoder -> chunkencoder(max_chunk), drained read_size at a time."""
+    a = _arr(data)
+    lens = np.asarray(piece_lens if piece_lens is not None else [a.size], dtype=np.uintp)
+    rs = read_size or max(max_chunk, 16)
+    chars = (a.size + 2) // 3 * 4
+    cap = chars + (chars // max(max_chunk, 2) + 2) * 16 + 16
+    out = np.empty(cap, dtype=np.uint8)
+    n = lib().orc_chunked_encode(_p(a), lens.ctypes.data, lens.size, max_chunk, termination,
+                                 rs, _c(pos62), _c(pos63), int(bool(pad)), _c(padchar),
+                                 out.ctypes.data, cap)
+    if n < 0:
+        raise AssertDomain("chunked stack failed (assert domain?)")
+    return out[:n].tobytes()
+
+
+def encode_counts(data, read_size, src_chunk=0, burst=0, pos62=-1, pos63=-1, pad=True,
+                  padchar=-1) -> list[int]:
+    """The reference encoder's positive read returns for this read pattern."""
+    a = _arr(data)
+    cap = a.size // 2 + 64
+    counts = np.empty(cap, dtype=np.intp)
+    n = lib().orc_encode_counts(_p(a), a.size, src_chunk, burst, read_size, _c(pos62),
+                                _c(pos63), int(bool(pad)), _c(padchar), counts.ctypes.data, cap)
+    if n < 0:
+        raise AssertDomain("encode_counts failed (assert domain?)")
+    return counts[:min(n, cap)].tolist()

@@ -16,7 +16,9 @@
 #include "base64decoder.h"
 #include "base64encoder.h"
 #include "blobstream.h"
+#include "chunkencoder.h"
 #include "nicestream.h"
+#include "queuestream.h"
 
 /* ---- counting source: test/asynctest-base64encoder.c:11-78 ------------ */
 
@@ -119,7 +121,18 @@ typedef struct {
     int err;      /* errno of a failed read, 0 otherwise */
     int done;
     size_t eagains, reads;
+    ssize_t *counts; /* optional log of positive read returns */
+    size_t max_counts, ncounts;
+    size_t *live;    /* optional: consumers still running; quit at 0 */
 } consumer;
+
+static void consumer_finish(consumer *c)
+{
+    c->done = 1;
+    bytestream_1_close(c->material);
+    if (!c->live || --*c->live == 0)
+        async_quit_loop(c->async);
+}
 
 static void consume(consumer *c)
 {
@@ -137,28 +150,25 @@ static void consume(consumer *c)
             return; /* the registered callback brings us back */
         }
         c->err = errno;
-        c->done = 1;
-        bytestream_1_close(c->material);
-        async_quit_loop(c->async);
+        consumer_finish(c);
         return;
     }
     if (n == 0) {
         free(buf);
-        c->done = 1;
-        bytestream_1_close(c->material);
-        async_quit_loop(c->async);
+        consumer_finish(c);
         return;
     }
     if (c->len + (size_t) n > c->cap) {
         free(buf);
         c->err = ENOSPC;
-        c->done = 1;
-        bytestream_1_close(c->material);
-        async_quit_loop(c->async);
+        consumer_finish(c);
         return;
     }
     memcpy(c->out + c->len, buf, (size_t) n);
     c->len += (size_t) n;
+    if (c->counts && c->ncounts < c->max_counts)
+        c->counts[c->ncounts] = n;
+    c->ncounts++;
     free(buf);
     async_execute(c->async, (action_1) { c, (act_1) consume });
 }
@@ -263,4 +273,154 @@ ssize_t h_copy_stream(const uint8_t *in, size_t n, size_t burst,
         return -1;
     return run(async, blob_chain(async, in, n, burst), read_size, out, cap,
                err_out, eagains);
+}
+
+/* The GPU encoder stage's positive read returns, for comparison with the
+ * reference's (oracle orc_encode_counts).  Returns how many, or -1. */
+ssize_t h_encode_counts(const uint8_t *in, size_t n, size_t src_chunk,
+                        size_t burst, size_t read_size, char pos62, char pos63,
+                        int pad, char padchar, ssize_t *counts,
+                        size_t max_counts, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    (void) src_chunk;
+    base64encoder_t *enc = base64_encode(async, blob_chain(async, in, n, burst),
+                                         pos62, pos63, pad != 0, padchar);
+    size_t cap = (n + 2) / 3 * 4 + 16;
+    uint8_t *out = malloc(cap);
+    consumer c;
+    memset(&c, 0, sizeof c);
+    c.async = async;
+    c.material = base64encoder_as_bytestream_1(enc);
+    c.read_size = read_size;
+    c.out = out;
+    c.cap = cap;
+    c.counts = counts;
+    c.max_counts = max_counts;
+    action_1 cb = { &c, (act_1) consume };
+    bytestream_1_register_callback(c.material, cb);
+    async_execute(async, cb);
+    int rc = async_loop(async);
+    destroy_async(async);
+    free(out);
+    if (err_out)
+        *err_out = rc < 0 ? errno : c.err;
+    return rc < 0 || c.err ? -1 : (ssize_t) c.ncounts;
+}
+
+/* chunkencoder over blob -> nice(burst), no GPU (the reference's
+ * test/asynctest-chunkencoder.c reads 100 at a time, MAX_CHUNK 30). */
+ssize_t h_chunk_stream(const uint8_t *in, size_t n, size_t burst,
+                       size_t max_chunk, int termination, size_t read_size,
+                       uint8_t *out, size_t cap, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    chunkencoder_t *ch = chunk_encode_2(async, blob_chain(async, in, n, burst),
+                                        max_chunk,
+                                        (chunkencoder_termination_t) termination);
+    return run(async, chunkencoder_as_bytestream_1(ch), read_size, out, cap,
+               err_out, NULL);
+}
+
+/* queuestream of `npieces` blobs (enqueued, or pushed in reverse order when
+ * `push`), each behind nice(burst); terminated only after the first read
+ * has answered EAGAIN, so the notify path is exercised.  No GPU. */
+typedef struct {
+    queuestream_t *q;
+    int fired;
+} late_terminate;
+
+static void do_terminate(late_terminate *t)
+{
+    if (!t->fired) {
+        t->fired = 1;
+        queuestream_terminate(t->q);
+    }
+}
+
+ssize_t h_queue_stream(const uint8_t *in, const size_t *lens, size_t npieces,
+                       int push, size_t burst, size_t read_size, uint8_t *out,
+                       size_t cap, int *err_out, size_t *eagains)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    queuestream_t *q = make_queuestream(async);
+    size_t off = 0;
+    const uint8_t **starts = malloc((npieces ? npieces : 1) * sizeof *starts);
+    for (size_t i = 0; i < npieces; i++) {
+        starts[i] = in + off;
+        off += lens[i];
+    }
+    for (size_t k = 0; k < npieces; k++) {
+        size_t i = push ? npieces - 1 - k : k;
+        bytestream_1 s = blob_chain(async, starts[i], lens[i], burst);
+        if (push)
+            queuestream_push(q, s);
+        else
+            queuestream_enqueue(q, s);
+    }
+    free(starts);
+    late_terminate *t = calloc(1, sizeof *t);
+    t->q = q;
+    async_timer_start(async, async_now(async) + 2000000, /* 2 ms */
+                      (action_1) { t, (act_1) do_terminate });
+    ssize_t r = run(async, queuestream_as_bytestream_1(q), read_size, out, cap,
+                    err_out, eagains);
+    free(t);
+    return r;
+}
+
+/* `nmsg` independent egress stacks
+ * queuestream(message) -> base64_encode (GPU) -> chunk_encode(max_chunk),
+ * all on one loop, each drained `read_size` at a time into
+ * out + out_off[i] (capacity out_off[i+1] - out_off[i]); out_len[i]
+ * receives each framed length.  Returns 0, or -1 with *err_out. */
+int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                    size_t max_chunk, size_t read_size, char pos62, char pos63,
+                    int pad, char padchar, uint8_t *out, const uint64_t *out_off,
+                    uint64_t *out_len, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    consumer *cs = calloc(nmsg ? nmsg : 1, sizeof *cs);
+    size_t live = nmsg;
+    for (size_t i = 0; i < nmsg; i++) {
+        queuestream_t *q = make_queuestream(async);
+        queuestream_enqueue_bytes(q, in + in_off[i], in_off[i + 1] - in_off[i]);
+        queuestream_terminate(q);
+        base64encoder_t *e = base64_encode(async, queuestream_as_bytestream_1(q),
+                                           pos62, pos63, pad != 0, padchar);
+        chunkencoder_t *ch = chunk_encode(async, base64encoder_as_bytestream_1(e),
+                                          max_chunk);
+        consumer *c = &cs[i];
+        c->async = async;
+        c->material = chunkencoder_as_bytestream_1(ch);
+        c->read_size = read_size;
+        c->out = out + out_off[i];
+        c->cap = out_off[i + 1] - out_off[i];
+        c->live = &live;
+        action_1 cb = { c, (act_1) consume };
+        bytestream_1_register_callback(c->material, cb);
+        async_execute(async, cb);
+    }
+    int rc = nmsg ? async_loop(async) : 0;
+    int err = rc < 0 ? errno : 0;
+    for (size_t i = 0; i < nmsg; i++) {
+        out_len[i] = cs[i].len;
+        if (!err && cs[i].err)
+            err = cs[i].err;
+        if (!cs[i].done && !err)
+            err = EPIPE;
+    }
+    destroy_async(async);
+    free(cs);
+    if (err_out)
+        *err_out = err;
+    return err ? -1 : 0;
 }

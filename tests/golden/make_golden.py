@@ -184,7 +184,147 @@ def digests():
     }
 
 
+# ---- config 5: Zipf lengths, encoder read counts, chunk framing --------
+
+def zipf_lengths(n_msgs=16384, seed=0x2F, rmax=16384, s=1.1):
+    """L = 64*r, P(r) ~ r^-s over r in [1, rmax],
+    by inverse CDF of the harmonic weights; u = top 53 bits of splitmix64
+    word i (seed 0x2F) / 2^53."""
+    w = [r ** -s for r in range(1, rmax + 1)]
+    tot = sum(w)
+    cdf, acc = [], 0.0
+    for x in w:
+        acc += x
+        cdf.append(acc / tot)
+    words = splitmix64(seed, 8 * n_msgs)
+    out = []
+    import bisect
+    for i in range(n_msgs):
+        u = (int.from_bytes(words[8 * i:8 * i + 8], "little") >> 11) / float(1 << 53)
+        r = min(bisect.bisect_right(cdf, u), rmax - 1) + 1
+        out.append(64 * r)
+    return out
+
+
+def enc_read_counts(n, count, pad=True):
+    """Positive read returns of the reference encoder (base64encoder.c
+    :101-142) drained with reads of `count` from an upstream that always
+    fills the request (a terminated queuestream / blobstream): the bit
+    bookkeeping only, restated independently of oracle/."""
+    b, left, out, state = 0, n, [], "data"
+    pads = 0
+    while True:
+        if state == "pads":
+            k = min(count, pads)
+            out.append(k)
+            pads -= k
+            if pads == 0:
+                return out
+            continue
+        need = (count * 6 + 7 - b) // 8
+        got = min(need, left)
+        if got == 0:  # finalize() :61-99
+            if b == 0:
+                return out
+            tail = (3 if b == 2 else 2) if pad else 1
+            k = min(count, tail)
+            out.append(k)
+            if k == tail:
+                return out
+            pads, state = tail - k, "pads"
+            continue
+        left -= got
+        bits = b + 8 * got
+        chars = bits // 6
+        b = bits % 6
+        assert chars <= count, "reference assert (:140) domain"
+        out.append(chars)
+
+
+def chunk_frame(chars: bytes, counts, termination=0) -> bytes:
+    """chunkencoder.c:31-77 framing of an upstream whose reads returned
+    `counts` (then EOF)."""
+    out, pos = bytearray(), 0
+    for i, n in enumerate(counts):
+        if i:
+            out += b"\r\n"
+        out += b"%x\r\n" % n + chars[pos:pos + n]
+        pos += n
+    assert pos == len(chars)
+    if counts:
+        out += b"\r\n"
+    out += b"0" + {0: b"\r\n\r\n", 1: b"\r\n", 2: b""}[termination]
+    return bytes(out)
+
+
+# The body of test/asynctest-chunkencoder.c:10-26 (fixture text; UTF-8 as
+# in the C source), framed with MAX_CHUNK 30 (:164) from a stringstream.
+CHUNK_TEXT = (
+    "SMS Prinzregent Luitpold was the fifth and "
+    "final vessel of the Kaiser class of battleships of the Imperial"
+    " German Navy. Prinzregent Luitpold's keel was laid in October 1910"
+    " at the Germaniawerft dockyard in Kiel. She was launched on 17"
+    " February 1912 and was commissioned into the navy on 19 August 1913."
+    " Prinzregent Luitpold was assigned to the III Battle Squadron of the"
+    " High Seas Fleet for the majority of her career; in December 1916,"
+    " she was transferred to the IV Battle Squadron. Along with her four"
+    " sister ships, Kaiser, Friedrich der Grosse, Kaiserin, and K\u00f6nig"
+    " Albert, Prinzregent Luitpold participated in all of the major fleet"
+    " operations of World War I, including the Battle of Jutland on 31"
+    " May \u2013 1 June 1916. The ship was also involved in Operation Albion,"
+    " an amphibious assault on the Russian-held islands in the Gulf of"
+    " Riga, in late 1917.").encode("utf-8")
+
+
+def chunk_fixtures():
+    text = CHUNK_TEXT
+    counts = [min(30, len(text) - i) for i in range(0, len(text), 30)]
+    fx = {"ref_test": {"text_hex": text.hex(), "max_chunk": 30, "read_size": 100,
+                       "framed_hex": chunk_frame(text, counts).hex()},
+          "terminations": [{"termination": t, "framed_hex": chunk_frame(b"abc", [3], t).hex()}
+                           for t in (0, 1, 2)] +
+                          [{"termination": t, "empty": True,
+                            "framed_hex": chunk_frame(b"", [], t).hex()} for t in (0, 1, 2)]}
+    lens = zipf_lengths()
+    fx["zipf"] = {"n_msgs": len(lens), "seed": 0x2F, "first64": lens[:64],
+                  "total": sum(lens), "max": max(lens), "min": min(lens),
+                  "sha256": hashlib.sha256(",".join(map(str, lens)).encode()).hexdigest()}
+    # Encoder read counts for a few (n, count) pairs, and framed stacks of
+    # the first Zipf messages (payload = splitmix64(0x5EED) over the
+    # concatenation), max_chunk 4096 and 1 MiB.
+    fx["enc_counts"] = []
+    for n, c, pad in ((0, 200, True), (1, 200, True), (2, 4, True), (5, 4, False),
+                      (1000001, 200, True), (3000, 1024, True), (3001, 1024, False),
+                      (7, 6, True), (11, 2, True), (8, 1, True)):
+        try:
+            rle = []
+            for k in enc_read_counts(n, c, pad):
+                if rle and rle[-1][0] == k:
+                    rle[-1][1] += 1
+                else:
+                    rle.append([k, 1])
+            fx["enc_counts"].append({"n": n, "count": c, "pad": pad, "counts_rle": rle})
+        except AssertionError:
+            pass
+    first = lens[:24]
+    payload = splitmix64(0x5EED, sum(first))
+    stacks, off = [], 0
+    for L in first:
+        msg = payload[off:off + L]
+        off += L
+        chars = base64.b64encode(msg)
+        for mc in (4096, 1 << 20):
+            framed = chunk_frame(chars, enc_read_counts(L, mc), 0)
+            stacks.append({"len": L, "max_chunk": mc, "framed_len": len(framed),
+                           "framed_sha256": hashlib.sha256(framed).hexdigest()})
+    fx["stacks"] = {"payload": "splitmix64(0x5EED) over the first 24 Zipf messages",
+                    "items": stacks}
+    return fx
+
+
 def main():
+    with open(os.path.join(HERE, "chunk.json"), "w") as f:
+        json.dump(chunk_fixtures(), f, indent=1)
     rng = random.Random(0xB64)
     with open(os.path.join(HERE, "kat_encode.json"), "w") as f:
         json.dump(kat_encode(rng), f, separators=(",", ":"))

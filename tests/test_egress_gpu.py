@@ -1,0 +1,98 @@
+"""Config 5 on the GPU:
+queuestream -> GPU base64 encoder stage -> chunkencoder, many stacks on one
+loop sharing the batching hub, checked against the oracle's restatement of
+the same stack -- including the chunk framing, which follows the encoder's
+per-read counts."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as orc
+from tests import util
+
+pytestmark = pytest.mark.gpu
+
+FX = util.golden("chunk.json")
+
+
+@pytest.mark.parametrize("case", FX["enc_counts"], ids=lambda c: f"n{c['n']}_c{c['count']}")
+@pytest.mark.parametrize("burst", [0, 113])
+def test_stage_read_counts_match_reference(case, burst):
+    """The GPU stage returns the reference encoder's read counts
+    (full count, short only at the end, finalize() on its own)."""
+    data = util.splitmix64(0x5EED, case["n"]).tobytes()
+    want = [v for v, k in case["counts_rle"] for _ in range(k)]
+    got, err = util.encode_counts(data, case["count"], burst, pad=case["pad"])
+    assert err == 0
+    assert got == want
+
+
+@pytest.mark.parametrize("cap", [64, 4096])
+@pytest.mark.parametrize("seed", range(4))
+def test_stage_read_counts_small_slots(monkeypatch, cap, seed):
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    monkeypatch.setenv("ASYNC_B64_MIN_PULL", "1")
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(0, 50000))
+    count = int(rng.choice([4, 8, 200, 1024, 10240]))
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    for burst in (0, 97):
+        got, err = util.encode_counts(data, count, burst)
+        assert err == 0
+        assert got == orc.encode_counts(data, count, burst=burst)
+
+
+@pytest.mark.parametrize("max_chunk", [4096, 1 << 20])
+def test_egress_stacks_vs_oracle(max_chunk):
+    lens = util.zipf_lengths()[:300]
+    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    framed, err = util.egress_stacks(payload, lens, max_chunk, 10240)
+    assert err == 0
+    off = 0
+    for i, L in enumerate(lens.tolist()):
+        msg = payload[off:off + L].tobytes()
+        off += L
+        assert framed[i] == orc.chunked_encode(msg, max_chunk=max_chunk), (i, L)
+
+
+def test_egress_stacks_fixture():
+    """The first 24 Zipf messages against the committed framed digests."""
+    items = FX["stacks"]["items"]
+    lens = [it["len"] for it in items[::2]]
+    payload = util.splitmix64(0x5EED, sum(lens))
+    for k, mc in enumerate((4096, 1 << 20)):
+        framed, err = util.egress_stacks(payload, lens, mc, 10240)
+        assert err == 0
+        for i, f in enumerate(framed):
+            it = items[2 * i + k]
+            assert it["max_chunk"] == mc
+            assert len(f) == it["framed_len"]
+            assert hashlib.sha256(f).hexdigest() == it["framed_sha256"]
+
+
+def test_egress_stacks_alphabet_and_small_reads():
+    lens = [0, 1, 2, 3, 64, 65, 4095, 4096, 4097, 70000]
+    payload = util.splitmix64(9, sum(lens))
+    framed, err = util.egress_stacks(payload, lens, 1000, 7, ".", "_", False, "-")
+    assert err == 0
+    off = 0
+    for i, L in enumerate(lens):
+        msg = payload[off:off + L].tobytes()
+        off += L
+        assert framed[i] == orc.chunked_encode(msg, max_chunk=1000, pos62=".", pos63="_",
+                                               pad=False, padchar="-"), L
+
+
+@pytest.mark.slow
+def test_config5_full():
+    """All 16,384 Zipf messages (1.10 GB), max_chunk 1 MiB, tcp-sized reads."""
+    lens = util.zipf_lengths()
+    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240)
+    assert err == 0
+    off = 0
+    for i, L in enumerate(lens.tolist()):
+        msg = payload[off:off + L].tobytes()
+        off += L
+        assert framed[i] == orc.chunked_encode(msg, max_chunk=1 << 20), i

@@ -56,6 +56,16 @@ def harness() -> ctypes.CDLL:
         L.h_decode_stream.restype = ssz
         L.h_copy_stream.argtypes = [vp, sz, sz, sz, vp, sz, ip, ctypes.POINTER(sz)]
         L.h_copy_stream.restype = ssz
+        L.h_encode_counts.argtypes = [vp, sz, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
+        L.h_encode_counts.restype = ssz
+        L.h_chunk_stream.argtypes = [vp, sz, sz, sz, ctypes.c_int, sz, vp, sz, ip]
+        L.h_chunk_stream.restype = ssz
+        L.h_queue_stream.argtypes = [vp, vp, sz, ctypes.c_int, sz, sz, vp, sz, ip,
+                                     ctypes.POINTER(sz)]
+        L.h_queue_stream.restype = ssz
+        L.h_egress_stacks.argtypes = [vp, vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, vp,
+                                      vp, ip]
+        L.h_egress_stacks.restype = ctypes.c_int
         _harness = L
     return _harness
 
@@ -107,3 +117,80 @@ def stage_reftest(length=1000001):
                             dec.ctypes.data, dec.size, ctypes.byref(err), ctypes.byref(eag))
     return (None if n < 0 else (enc[: elen.value].tobytes(), dec[:n].tobytes())), \
         err.value, eag.value
+
+
+def zipf_lengths(n_msgs=16384, seed=0x2F, rmax=16384, s=1.1) -> np.ndarray:
+    """SURVEY.md §8(d) config 5 message lengths (same definition as
+    tests/golden/make_golden.py:zipf_lengths, vectorised)."""
+    r = np.arange(1, rmax + 1, dtype=np.float64)
+    w = r ** -s
+    cdf = np.cumsum(w) / w.sum()
+    words = splitmix64(seed, 8 * n_msgs).view("<u8")
+    u = (words >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    idx = np.minimum(np.searchsorted(cdf, u, side="right"), rmax - 1)
+    return (64 * (idx + 1)).astype(np.int64)
+
+
+def encode_counts(data: bytes, read_size: int, burst=0, pos62=-1, pos63=-1, pad=True,
+                  padchar=-1):
+    """The GPU encoder stage's positive read returns; (list|None, errno)."""
+    a, p = _buf(data)
+    cap = len(data) // 2 + 64
+    counts = np.empty(cap, dtype=np.intp)
+    err = ctypes.c_int(0)
+    n = harness().h_encode_counts(p, len(data), 0, burst, read_size, cch(pos62), cch(pos63),
+                                  int(bool(pad)), cch(padchar), counts.ctypes.data, cap,
+                                  ctypes.byref(err))
+    return (None if n < 0 else counts[:min(n, cap)].tolist()), err.value
+
+
+def chunk_stream(data: bytes, max_chunk: int, termination=0, read_size=100, burst=0):
+    a, p = _buf(data)
+    cap = len(data) + (len(data) // max(max_chunk, 2) + 2) * 16 + 16
+    out = np.empty(cap, np.uint8)
+    err = ctypes.c_int(0)
+    n = harness().h_chunk_stream(p, len(data), burst, max_chunk, termination, read_size,
+                                 out.ctypes.data, cap, ctypes.byref(err))
+    return (None if n < 0 else out[:n].tobytes()), err.value
+
+
+def queue_stream(pieces, push=False, burst=0, read_size=100):
+    data = b"".join(pieces)
+    a, p = _buf(data)
+    lens = np.asarray([len(x) for x in pieces] or [0], dtype=np.uintp)
+    out = np.empty(len(data) + 16, np.uint8)
+    err = ctypes.c_int(0)
+    eag = ctypes.c_size_t(0)
+    n = harness().h_queue_stream(p, lens.ctypes.data, len(pieces), int(push), burst,
+                                 read_size, out.ctypes.data, out.size, ctypes.byref(err),
+                                 ctypes.byref(eag))
+    return (None if n < 0 else out[:n].tobytes()), err.value, eag.value
+
+
+def framed_cap(n: int, max_chunk: int) -> int:
+    chars = (n + 2) // 3 * 4
+    return chars + (chars // max(max_chunk, 2) + 3) * 16 + 16
+
+
+def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos62=-1,
+                  pos63=-1, pad=True, padchar=-1):
+    """Run len(lens) GPU egress stacks on one loop; returns
+    (list of framed bytes | None, errno)."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    in_off = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(lens, out=in_off[1:])
+    caps = np.array([framed_cap(int(n), max_chunk) for n in lens], np.uint64)
+    out_off = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(caps, out=out_off[1:])
+    out = np.empty(int(out_off[-1]) or 1, np.uint8)
+    out_len = np.zeros(max(lens.size, 1), np.uint64)
+    err = ctypes.c_int(0)
+    src = np.ascontiguousarray(payload, dtype=np.uint8)
+    rc = harness().h_egress_stacks(src.ctypes.data, in_off.ctypes.data, lens.size, max_chunk,
+                                   read_size, cch(pos62), cch(pos63), int(bool(pad)),
+                                   cch(padchar), out.ctypes.data, out_off.ctypes.data,
+                                   out_len.ctypes.data, ctypes.byref(err))
+    if rc != 0:
+        return None, err.value
+    return [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
+            for i in range(lens.size)], 0
