@@ -308,7 +308,13 @@ static int top_up_encoder(stage *st)
         size_t got = gather(st, in + st->ncarry, room - st->ncarry, &eof,
                             &uerr);
         size_t total = st->ncarry + got;
-        size_t n;
+        /* The block encodes all `total` bytes.  Its full sextets,
+         * floor(8*total/6) characters, are served now -- the reference
+         * emits them in the read that brought the bytes in
+         * (base64encoder.c:132-139).  The 0-2 bytes of a trailing partial
+         * group are carried: the next block re-encodes them and skips the
+         * characters (one per carried byte) already served from this one. */
+        size_t skip = st->ncarry;
         if (eof) {
             st->final_queued = true;
             st->ncarry = 0;
@@ -316,22 +322,24 @@ static int top_up_encoder(stage *st)
                 b64_hub_cancel(st->hub);
                 return 0;
             }
-            n = total; /* finalize(): partial group + padding */
         } else {
-            n = total - total % 3;
-            st->ncarry = total - n;
-            memcpy(st->carry, in + n, st->ncarry);
-            if (n == 0) {
+            if (got == 0) {
                 b64_hub_cancel(st->hub);
                 return uerr ? uerr : EAGAIN;
             }
+            st->ncarry = total % 3;
+            memcpy(st->carry, in + total - st->ncarry, st->ncarry);
         }
         slot_arm(st, sl);
-        /* Non-final blocks are whole groups: no padding either way. */
-        sl->out_len = (size_t) b64x_encoded_len(n, eof && st->abc.pad);
-        b64_hub_commit(st->hub, &sl->ticket, n, sl->out_len,
+        sl->out_len = (size_t) b64x_encoded_len(total, st->abc.pad);
+        b64_hub_commit(st->hub, &sl->ticket, total, sl->out_len,
                        (action_1) { st, (act_1) stage_notify });
-        sl->body_end = sl->out_len - (eof ? finalize_len(n, st->abc.pad) : 0);
+        sl->out_pos = skip;
+        sl->body_end = total * 8 / 6;
+        if (eof) /* finalize(): the partial sextet and the pads */
+            sl->body_end = sl->out_len - finalize_len(total, st->abc.pad);
+        else
+            sl->out_len = sl->body_end; /* the rest is re-encoded later */
         sl->resolved = true;
         if (uerr)
             return uerr;

@@ -146,38 +146,87 @@ def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
     return dt, opos
 
 
+def run_egress(n_msgs: int):
+    """Config 5: n_msgs Zipf messages, each its own queuestream -> GPU
+    encoder stage -> chunkencoder(1 MiB) stack, all on one loop, drained
+    10,240 bytes per read (tcp_connection.c:22); host memory in, framed host
+    memory out.  The oracle's restatement of the same stack (1 thread) is
+    timed on a bounded sample beside it."""
+    from oracle import pyoracle as orc
+    from tests import util
+    lens = util.zipf_lengths()[:n_msgs]
+    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
+    t0 = time.perf_counter()
+    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240)
+    dt = time.perf_counter() - t0
+    nbytes = int(lens.sum())
+    # bit check on a sample of messages (all of them is the slow GPU test)
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    idx = list(range(0, n_msgs, max(1, n_msgs // 64)))
+    ok = err == 0 and all(
+        framed[i] == orc.chunked_encode(payload[offs[i]:offs[i + 1]].tobytes(),
+                                        max_chunk=1 << 20) for i in idx)
+    # CPU baseline: the oracle stack on the first messages, ~10 s budget
+    t1, done, k = time.perf_counter(), 0, 0
+    while k < n_msgs and time.perf_counter() - t1 < 10.0:
+        orc.chunked_encode(payload[offs[k]:offs[k + 1]].tobytes(), max_chunk=1 << 20,
+                           read_size=10240)
+        done += int(lens[k])
+        k += 1
+    cpu_dt = time.perf_counter() - t1
+    print(json.dumps({"measure": "egress_config5", "messages": n_msgs, "bytes": nbytes,
+                      "framed_bytes": int(sum(len(f) for f in framed)) if framed else 0,
+                      "seconds": dt, "GiB_s": nbytes / dt / 2**30,
+                      "msgs_per_s": n_msgs / dt, "exact_sampled": bool(ok),
+                      "cpu_oracle": {"messages": k, "bytes": done, "seconds": cpu_dt,
+                                     "GiB_s": done / cpu_dt / 2**30, "cores": 1}}),
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--total", type=int, default=1024, help="MiB of input bytes")
     ap.add_argument("--block", type=int, default=32, help="MiB per session block")
     ap.add_argument("--k", type=int, default=4, help="sessions in flight")
     ap.add_argument("--stage-total", type=int, default=256, help="MiB through the stages")
+    ap.add_argument("--only", default="", help="comma list: sessions,resident,stages,egress")
+    ap.add_argument("--egress-msgs", type=int, default=16384, help="config-5 messages")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
+    want = (lambda k: not only or k in only)
 
     import torch
     from async_amd import b64
 
+    if want("egress"):
+        run_egress(args.egress_msgs)
+    if only == {"egress"}:
+        return
     total = args.total << 20
     block = args.block << 20
     src = splitmix(total)
     # Device-resident reference result for the bit check.
     ref_chars = b64.encode(torch.from_numpy(src).cuda()).cpu().numpy()
-    chars = np.empty(len(ref_chars), np.uint8)
-    dt, m = run_sessions(src, block, args.k, "encode", chars)
-    ok = m == len(ref_chars) and np.array_equal(chars, ref_chars)
-    print(json.dumps({"measure": "sessions_encode", "bytes": total, "block": block,
-                      "k": args.k, "seconds": dt, "GiB_s": total / dt / 2**30,
-                      "exact": bool(ok)}), flush=True)
-    back = np.empty(total + 16, np.uint8)
-    dt, m = run_sessions(ref_chars, block, args.k, "decode", back)
-    ok = m == total and np.array_equal(back[:m], src)
-    print(json.dumps({"measure": "sessions_decode", "chars": len(ref_chars), "bytes": m,
-                      "block": block, "k": args.k, "seconds": dt,
-                      "GiB_s": m / dt / 2**30, "exact": bool(ok)}), flush=True)
+    if want("sessions"):
+        chars = np.empty(len(ref_chars), np.uint8)
+        dt, m = run_sessions(src, block, args.k, "encode", chars)
+        ok = m == len(ref_chars) and np.array_equal(chars, ref_chars)
+        print(json.dumps({"measure": "sessions_encode", "bytes": total, "block": block,
+                          "k": args.k, "seconds": dt, "GiB_s": total / dt / 2**30,
+                          "exact": bool(ok)}), flush=True)
+        back = np.empty(total + 16, np.uint8)
+        dt, m = run_sessions(ref_chars, block, args.k, "decode", back)
+        ok = m == total and np.array_equal(back[:m], src)
+        print(json.dumps({"measure": "sessions_decode", "chars": len(ref_chars), "bytes": m,
+                          "block": block, "k": args.k, "seconds": dt,
+                          "GiB_s": m / dt / 2**30, "exact": bool(ok)}), flush=True)
+        del chars, back
 
-    print(json.dumps({"measure": "pcie_calibration", "bytes": 256 << 20,
-                      **pcie_calibration(256 << 20)}), flush=True)
-    for kk in (2, 4, 8):
+    if want("resident"):
+        print(json.dumps({"measure": "pcie_calibration", "bytes": 256 << 20,
+                          **pcie_calibration(256 << 20)}), flush=True)
+    for kk in ((2, 4, 8) if want("resident") else ()):
         dt = run_resident(src, block, kk, "encode", total)
         print(json.dumps({"measure": "resident_encode", "bytes": total, "block": block,
                           "k": kk, "seconds": dt, "GiB_s": total / dt / 2**30,
@@ -188,6 +237,8 @@ def main():
                           "pcie_GB_s": (total + len(ref_chars)) / dt / 1e9}), flush=True)
 
     # The bytestream_1 stages on the product loop (tests/csrc harness).
+    if not want("stages"):
+        return
     from tests import util
     st_total = args.stage_total << 20
     data = src[:st_total]
