@@ -17,14 +17,18 @@
 
 #include <errno.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/eventfd.h>
+#include <time.h>
 #include <unistd.h>
 
 enum {
     HUB_LANES = 4,          /* batches in flight per loop */
-    HUB_MAX_FREE = 8,       /* idle arenas kept for reuse */
+    HUB_MAX_LIVE = HUB_LANES + 4, /* arenas a hub holds before idle
+                                     stages are made to wait */
+    POOL_MAX = 16,          /* idle arenas kept process-wide for reuse */
     HUB_JOBS = 1 << 16,     /* jobs per arena */
 };
 
@@ -55,16 +59,39 @@ struct b64_hub {
     b64_batch *running[HUB_LANES];
     b64_batch *filling;
     b64_batch *ready, *ready_tail;
-    b64_batch *free_list;
-    unsigned nfree, inflight;
+    unsigned inflight;
+    unsigned live;               /* arenas taken from the pool */
     size_t batch_bytes;
-    bool flush_scheduled, in_wake, doomed;
+    bool flush_scheduled, kick_scheduled, in_wake, doomed;
     action_1 *wakes;             /* scratch for hub_wake() */
     size_t nwakes, wakes_cap;
+    action_1 *waiters;           /* idle stages waiting for an arena */
+    size_t nwaiters, waiters_cap;
+    action_1 *kicking;           /* the list hub_kick() is working through */
+    size_t nkicking;
+    struct {                     /* ASYNC_B64_HUB_TRACE=1: printed at teardown */
+        bool on;
+        unsigned long batches, jobs, allocs, wake_calls, max_ready;
+        unsigned long long in_bytes, out_bytes;
+        double wake_s, launch_s, t_first, t_last;
+    } tr;
 };
+
+static double mono_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
 
 static pthread_mutex_t registry_lock = PTHREAD_MUTEX_INITIALIZER;
 static b64_hub *registry;
+
+/* Idle arenas, shared by all hubs of the process (pinned allocation costs
+ * milliseconds; a hub's life may be one message). */
+static pthread_mutex_t pool_lock = PTHREAD_MUTEX_INITIALIZER;
+static b64_batch *pool;
+static unsigned npool;
 
 static size_t env_bytes(const char *name, size_t dflt, size_t lo)
 {
@@ -110,33 +137,59 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     return b;
 }
 
-static void batch_recycle(b64_hub *h, b64_batch *b)
+static void schedule_kick(b64_hub *h);
+
+/* Back to the process pool (or freed); wakes stages waiting for room. */
+static void batch_put(b64_batch *b)
 {
     b->state = B_FREE;
     b->in_used = b->out_used = 0;
     b->njobs = 0;
     b->err = 0;
+    b->hub = NULL;
     atomic_store_explicit(&b->done, 0, memory_order_relaxed);
-    if (h->nfree < HUB_MAX_FREE) {
-        b->next = h->free_list;
-        h->free_list = b;
-        h->nfree++;
-    } else {
-        batch_free(b);
+    pthread_mutex_lock(&pool_lock);
+    if (npool < POOL_MAX) {
+        b->next = pool;
+        pool = b;
+        npool++;
+        b = NULL;
     }
+    pthread_mutex_unlock(&pool_lock);
+    if (b)
+        batch_free(b);
+}
+
+static void batch_recycle(b64_hub *h, b64_batch *b)
+{
+    batch_put(b);
+    h->live--;
+    if (h->nwaiters)
+        schedule_kick(h);
 }
 
 static b64_batch *batch_get(b64_hub *h, size_t need)
 {
-    for (b64_batch **p = &h->free_list; *p; p = &(*p)->next) {
+    b64_batch *b = NULL;
+    pthread_mutex_lock(&pool_lock);
+    for (b64_batch **p = &pool; *p; p = &(*p)->next) {
         if ((*p)->in_cap >= need) {
-            b64_batch *b = *p;
+            b = *p;
             *p = b->next;
-            h->nfree--;
-            return b;
+            npool--;
+            break;
         }
     }
-    return batch_new(h, need > h->batch_bytes ? need : h->batch_bytes);
+    pthread_mutex_unlock(&pool_lock);
+    if (!b) {
+        h->tr.allocs++;
+        b = batch_new(h, need > h->batch_bytes ? need : h->batch_bytes);
+        if (!b)
+            return NULL;
+    }
+    b->hub = h;
+    h->live++;
+    return b;
 }
 
 /* HIP runtime thread. */
@@ -164,10 +217,18 @@ static void seal(b64_hub *h)
     else
         h->ready = b;
     h->ready_tail = b;
+    if (h->tr.on) {
+        unsigned long depth = 0;
+        for (b64_batch *r = h->ready; r; r = r->next)
+            depth++;
+        if (depth > h->tr.max_ready)
+            h->tr.max_ready = depth;
+    }
 }
 
 static void launch_ready(b64_hub *h)
 {
+    double t0 = h->tr.on ? mono_s() : 0;
     for (int i = 0; i < HUB_LANES && h->ready; i++) {
         if (h->running[i])
             continue;
@@ -188,16 +249,33 @@ static void launch_ready(b64_hub *h)
             b->err = rc;
             batch_done(b);
         }
+        if (h->tr.on) {
+            h->tr.batches++;
+            h->tr.jobs += b->njobs;
+            h->tr.in_bytes += b->in_used;
+            h->tr.out_bytes += b->out_used;
+            if (!h->tr.t_first)
+                h->tr.t_first = t0;
+        }
     }
+    if (h->tr.on)
+        h->tr.launch_s += mono_s() - t0;
 }
 
 static void hub_destroy(b64_hub *h);
+
+/* A doomed hub goes once nothing scheduled on the loop refers to it. */
+static bool hub_idle(const b64_hub *h)
+{
+    return !h->in_wake && !h->flush_scheduled && !h->kick_scheduled;
+}
 
 static void hub_flush(b64_hub *h)
 {
     h->flush_scheduled = false;
     if (h->doomed) {
-        hub_destroy(h);
+        if (hub_idle(h))
+            hub_destroy(h);
         return;
     }
     if (h->filling && h->filling->njobs)
@@ -211,6 +289,60 @@ static void schedule_flush(b64_hub *h)
         return;
     h->flush_scheduled = true;
     async_execute(h->async, (action_1) { h, (act_1) hub_flush });
+}
+
+/* Room freed up: let every waiting stage retry (deferred, so no stage is
+ * re-entered from inside another stage's read()). */
+static void hub_kick(b64_hub *h)
+{
+    h->kick_scheduled = false;
+    if (h->doomed) {
+        if (hub_idle(h))
+            hub_destroy(h);
+        return;
+    }
+    /* Oldest first, and only until one of them still finds no room (it
+     * re-queues itself): waking thousands of stages for one free arena
+     * would cost a retry each. */
+    size_t n = h->nwaiters;
+    action_1 *w = h->waiters;
+    h->waiters = NULL;
+    h->nwaiters = h->waiters_cap = 0;
+    h->kicking = w;
+    h->nkicking = n;
+    size_t i = 0;
+    while (i < n && !h->doomed) {
+        action_1 a = w[i++];
+        if (!a.act)
+            continue; /* forgotten: its stage closed meanwhile */
+        action_1_perf(a);
+        if (h->nwaiters)
+            break;
+    }
+    h->kicking = NULL;
+    h->nkicking = 0;
+    for (; i < n; i++) { /* the rest keep their place */
+        if (!w[i].act)
+            continue;
+        if (h->nwaiters == h->waiters_cap) {
+            size_t cap = h->waiters_cap ? 2 * h->waiters_cap : 64;
+            action_1 *nw = realloc(h->waiters, cap * sizeof *nw);
+            if (!nw)
+                abort();
+            h->waiters = nw;
+            h->waiters_cap = cap;
+        }
+        h->waiters[h->nwaiters++] = w[i];
+    }
+    free(w);
+}
+
+static void schedule_kick(b64_hub *h)
+{
+    if (h->kick_scheduled || h->doomed)
+        return;
+    h->kick_scheduled = true;
+    async_execute(h->async, (action_1) { h, (act_1) hub_kick });
 }
 
 static void push_wake(b64_hub *h, action_1 a)
@@ -249,6 +381,7 @@ static void hub_wake(b64_hub *h)
     uint64_t v;
     while (read(h->efd, &v, sizeof v) == (ssize_t) sizeof v)
         ;
+    double t0 = h->tr.on ? mono_s() : 0;
     h->in_wake = true;
     h->nwakes = 0;
     for (int i = 0; i < HUB_LANES; i++) {
@@ -267,7 +400,12 @@ static void hub_wake(b64_hub *h)
     for (size_t i = 0; i < n; i++)
         action_1_perf(h->wakes[i]);
     h->in_wake = false;
-    if (h->doomed && !h->flush_scheduled)
+    if (h->tr.on) {
+        h->tr.wake_calls++;
+        h->tr.t_last = mono_s();
+        h->tr.wake_s += h->tr.t_last - t0;
+    }
+    if (h->doomed && hub_idle(h))
         hub_destroy(h);
 }
 
@@ -291,6 +429,7 @@ b64_hub *b64_hub_acquire(async_t *async)
     }
     h->async = async;
     h->batch_bytes = env_bytes("ASYNC_B64_BATCH_BYTES", (size_t) 16 << 20, 4096);
+    h->tr.on = env_bytes("ASYNC_B64_HUB_TRACE", 0, 0) != 0;
     h->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     if (h->efd < 0 ||
         async_register(async, h->efd, (action_1) { h, (act_1) hub_wake }) < 0) {
@@ -311,6 +450,13 @@ b64_hub *b64_hub_acquire(async_t *async)
 
 static void hub_destroy(b64_hub *h)
 {
+    if (h->tr.on)
+        fprintf(stderr,
+                "b64_hub: batches %lu jobs %lu in %llu out %llu allocs %lu "
+                "max_ready %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f\n",
+                h->tr.batches, h->tr.jobs, h->tr.in_bytes, h->tr.out_bytes,
+                h->tr.allocs, h->tr.max_ready, h->tr.wake_calls, h->tr.wake_s,
+                h->tr.launch_s, h->tr.t_last - h->tr.t_first);
     pthread_mutex_lock(&registry_lock);
     for (b64_hub **p = &registry; *p; p = &(*p)->next_hub) {
         if (*p == h) {
@@ -322,27 +468,22 @@ static void hub_destroy(b64_hub *h)
     for (int i = 0; i < HUB_LANES; i++) {
         if (h->running[i]) { /* teardown: wait, do not wake anyone */
             (void) b64x_lane_wait(h->lanes[i]);
-            b64_batch *b = h->running[i];
+            batch_put(h->running[i]);
             h->running[i] = NULL;
-            batch_free(b);
         }
         b64x_lane_close(h->lanes[i]);
     }
     if (h->filling)
-        batch_free(h->filling);
+        batch_put(h->filling);
     while (h->ready) {
         b64_batch *b = h->ready;
         h->ready = b->next;
-        batch_free(b);
-    }
-    while (h->free_list) {
-        b64_batch *b = h->free_list;
-        h->free_list = b->next;
-        batch_free(b);
+        batch_put(b);
     }
     (void) async_unregister(h->async, h->efd);
     close(h->efd);
     free(h->wakes);
+    free(h->waiters);
     free(h);
 }
 
@@ -353,14 +494,26 @@ void b64_hub_release(b64_hub *h)
     pthread_mutex_lock(&registry_lock);
     h->doomed = true; /* no new stage may pick it up */
     pthread_mutex_unlock(&registry_lock);
-    if (!h->in_wake && !h->flush_scheduled)
+    if (hub_idle(h))
         hub_destroy(h);
+}
+
+void b64_hub_forget(b64_hub *h, void *obj)
+{
+    for (size_t i = 0; i < h->nkicking; i++)
+        if (h->kicking[i].obj == obj)
+            h->kicking[i].act = NULL;
+    size_t k = 0;
+    for (size_t i = 0; i < h->nwaiters; i++)
+        if (h->waiters[i].obj != obj)
+            h->waiters[k++] = h->waiters[i];
+    h->nwaiters = k;
 }
 
 /* -------------------------------------------------------------- the API */
 
 uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
-                         size_t min_room, size_t *granted)
+                         size_t min_room, size_t *granted, action_1 waiter)
 {
     if (min_room > room)
         min_room = room;
@@ -374,11 +527,25 @@ uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
         b = h->filling; /* NULL after seal; kept if it was empty */
         if (b && (b->in_cap < room || memcmp(&b->abc, abc, sizeof *abc))) {
             h->filling = NULL;
-            batch_recycle(h, b);
+            batch_put(b);
+            h->live--;
             b = NULL;
         }
     }
     if (!b) {
+        if (waiter.act && h->live >= HUB_MAX_LIVE) {
+            if (h->nwaiters == h->waiters_cap) {
+                size_t cap = h->waiters_cap ? 2 * h->waiters_cap : 64;
+                action_1 *w = realloc(h->waiters, cap * sizeof *w);
+                if (!w)
+                    abort();
+                h->waiters = w;
+                h->waiters_cap = cap;
+            }
+            h->waiters[h->nwaiters++] = waiter;
+            errno = EAGAIN;
+            return NULL;
+        }
         b = batch_get(h, room);
         if (!b)
             return NULL;

@@ -48,9 +48,16 @@ void b64_hub_release(b64_hub *h);
 /* Room for one block of at most `room` bytes, at least `min_room`, encoded
  * with `abc`; returns where to write it, or NULL + errno.  *granted gets
  * the room actually given.  Must be followed by commit or cancel before
- * control returns to the loop. */
+ * control returns to the loop.  Backpressure: when the hub already holds
+ * its share of arenas and a new one is needed, a caller passing a
+ * `waiter` (a stage with nothing staged or in flight) gets NULL/EAGAIN and
+ * the waiter is performed once an arena is recycled; NULL_ACTION_1-like
+ * {.act = NULL} callers (stages holding data, which must make progress)
+ * are always served. */
 uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
-                         size_t min_room, size_t *granted);
+                         size_t min_room, size_t *granted, action_1 waiter);
+/* Drop any waiter whose object is `obj` (its stage is closing). */
+void b64_hub_forget(b64_hub *h, void *obj);
 /* Turn the reservation into a job of n bytes -> out_len characters. */
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
                     action_1 wake);

@@ -68,7 +68,7 @@
 #include "base64decoder.h"
 #include "base64encoder.h"
 
-enum { NSLOTS = 2 };
+enum { NSLOTS = 4 }; /* blocks in flight or staged per stage (read-ahead) */
 
 typedef struct stage stage;
 
@@ -212,6 +212,7 @@ static int stage_start(stage *st, size_t count)
 static void stage_stop(stage *st)
 {
     if (st->hub) {
+        b64_hub_forget(st->hub, st);
         for (int i = 0; i < NSLOTS; i++)
             b64_ticket_release(&st->slots[i].ticket);
         b64_hub_release(st->hub);
@@ -232,8 +233,10 @@ static void stage_stop(stage *st)
     st->started = false;
 }
 
-/* Pull from upstream into dst until `want` bytes, EOF, EAGAIN or an
- * error.  Returns bytes gathered; *eof / *err report why it stopped. */
+/* Pull from upstream into dst until at least min_pull bytes have come
+ * in, or EOF, EAGAIN or an error; after a short read it asks once more,
+ * so the EOF of a finite upstream lands in the same block.  Returns bytes
+ * gathered; *eof / *err report why it stopped. */
 static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
                      int *err)
 {
@@ -241,10 +244,9 @@ static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
     size_t want = st->min_pull < room ? st->min_pull : room;
     *eof = false;
     *err = 0;
-    while (got < want) {
-        ssize_t n = bytestream_1_read(st->up, dst + got, room - got);
-        if (n > 0 && (size_t) n < room - got)
-            st->short_seen = true;
+    while (got < room) {
+        size_t ask = room - got;
+        ssize_t n = bytestream_1_read(st->up, dst + got, ask);
         if (n < 0) {
             *err = errno ? errno : EIO;
             break;
@@ -254,6 +256,10 @@ static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
             break;
         }
         got += (size_t) n;
+        if ((size_t) n < ask)
+            st->short_seen = true;
+        else if (got >= want)
+            break;
     }
     return got;
 }
@@ -298,10 +304,22 @@ static int top_up_encoder(stage *st)
          * will do (the next block gets a fresh arena and a full slot, so
          * two slots always cover a full read). */
         size_t room;
+        /* Backpressure: a stage may be made to wait for an arena unless
+         * it holds finished output that cannot be served without more
+         * input (it must make progress, or arenas could stay pinned by
+         * partially read jobs forever). */
+        bool must_progress = st->nbusy > 0;
+        for (unsigned i = 0; i < st->nbusy && must_progress; i++)
+            if (!atomic_load_explicit(&st->slots[(st->head + i) % NSLOTS].ticket.done,
+                                      memory_order_acquire))
+                must_progress = false; /* a completion will wake us */
+        action_1 waiter = { NULL, NULL };
+        if (!must_progress)
+            waiter = (action_1) { st, (act_1) stage_notify };
         uint8_t *in = b64_hub_reserve(st->hub, &st->abc, st->cap,
-                                      st->ncarry + 4096, &room);
+                                      st->ncarry + 4096, &room, waiter);
         if (!in)
-            return -(errno ? errno : ENOMEM);
+            return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;

@@ -146,42 +146,66 @@ def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
     return dt, opos
 
 
-def run_egress(n_msgs: int):
+def _oracle_stack_rate(payload, lens, threads):
+    """The oracle's restatement of the same stack (queuestream -> encoder ->
+    chunkencoder(1 MiB), 10,240-byte reads) over all messages, `threads`
+    Python threads (ctypes drops the GIL inside the C oracle)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import pyoracle as orc
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    n = len(lens)
+    bounds = np.linspace(0, offs[-1], threads + 1)
+    cuts = np.searchsorted(offs, bounds)
+
+    def work(t):
+        for i in range(cuts[t], cuts[t + 1]):
+            orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
+                               read_size=10240)
+    t0 = time.perf_counter()
+    if threads == 1:
+        work(0)
+    else:
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(work, range(threads)))
+    dt = time.perf_counter() - t0
+    assert cuts[-1] == n
+    return dt
+
+
+def run_egress(n_msgs: int, thread_counts=(1, 4, 8, 16)):
     """Config 5: n_msgs Zipf messages, each its own queuestream -> GPU
-    encoder stage -> chunkencoder(1 MiB) stack, all on one loop, drained
-    10,240 bytes per read (tcp_connection.c:22); host memory in, framed host
-    memory out.  The oracle's restatement of the same stack (1 thread) is
-    timed on a bounded sample beside it."""
+    encoder stage -> chunkencoder(1 MiB) stack, drained 10,240 bytes per
+    read (tcp_connection.c:22); host memory in, framed host memory out.
+    T event loops (threads, one hub each) share the messages by bytes.
+    The oracle stack is timed with the same thread counts beside it."""
     from oracle import pyoracle as orc
     from tests import util
     lens = util.zipf_lengths()[:n_msgs]
     payload = util.splitmix64(0x5EED, int(lens.sum()))
-    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
-    t0 = time.perf_counter()
-    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240)
-    dt = time.perf_counter() - t0
     nbytes = int(lens.sum())
-    # bit check on a sample of messages (all of them is the slow GPU test)
     offs = np.concatenate([[0], np.cumsum(lens)])
-    idx = list(range(0, n_msgs, max(1, n_msgs // 64)))
-    ok = err == 0 and all(
-        framed[i] == orc.chunked_encode(payload[offs[i]:offs[i + 1]].tobytes(),
-                                        max_chunk=1 << 20) for i in idx)
-    # CPU baseline: the oracle stack on the first messages, ~10 s budget
-    t1, done, k = time.perf_counter(), 0, 0
-    while k < n_msgs and time.perf_counter() - t1 < 10.0:
-        orc.chunked_encode(payload[offs[k]:offs[k + 1]].tobytes(), max_chunk=1 << 20,
-                           read_size=10240)
-        done += int(lens[k])
-        k += 1
-    cpu_dt = time.perf_counter() - t1
-    print(json.dumps({"measure": "egress_config5", "messages": n_msgs, "bytes": nbytes,
-                      "framed_bytes": int(sum(len(f) for f in framed)) if framed else 0,
-                      "seconds": dt, "GiB_s": nbytes / dt / 2**30,
-                      "msgs_per_s": n_msgs / dt, "exact_sampled": bool(ok),
-                      "cpu_oracle": {"messages": k, "bytes": done, "seconds": cpu_dt,
-                                     "GiB_s": done / cpu_dt / 2**30, "cores": 1}}),
-          flush=True)
+    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
+    for T in thread_counts:
+        times = np.zeros(2)
+        res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times, raw=True,
+                                      threads=T)
+        dt = float(times.sum())
+        out, out_off, out_len = res
+        idx = list(range(0, n_msgs, max(1, n_msgs // 64)))
+        ok = err == 0 and all(
+            out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes() ==
+            orc.chunked_encode(payload[offs[i]:offs[i + 1]].tobytes(), max_chunk=1 << 20)
+            for i in idx)
+        framed_total = int(out_len.sum())
+        del out, res
+        cpu_dt = _oracle_stack_rate(payload, lens, T)
+        print(json.dumps({"measure": "egress_config5", "threads": T, "messages": n_msgs,
+                          "bytes": nbytes, "framed_bytes": framed_total, "seconds": dt,
+                          "setup_s": float(times[0]), "loop_s": float(times[1]),
+                          "GiB_s": nbytes / dt / 2**30, "msgs_per_s": n_msgs / dt,
+                          "exact_sampled": bool(ok),
+                          "cpu_oracle": {"threads": T, "seconds": cpu_dt,
+                                         "GiB_s": nbytes / cpu_dt / 2**30}}), flush=True)
 
 
 def main():

@@ -8,9 +8,11 @@
  * waits for the registered callback after EAGAIN and quits at EOF.
  * Python calls these through ctypes (tests/test_stages_gpu.py).
  */
+#define _GNU_SOURCE
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "async.h"
 #include "base64decoder.h"
@@ -380,11 +382,19 @@ ssize_t h_queue_stream(const uint8_t *in, const size_t *lens, size_t npieces,
  * all on one loop, each drained `read_size` at a time into
  * out + out_off[i] (capacity out_off[i+1] - out_off[i]); out_len[i]
  * receives each framed length.  Returns 0, or -1 with *err_out. */
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
 int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
                     size_t max_chunk, size_t read_size, char pos62, char pos63,
                     int pad, char padchar, uint8_t *out, const uint64_t *out_off,
-                    uint64_t *out_len, int *err_out)
+                    uint64_t *out_len, int *err_out, double *times)
 {
+    double t0 = now_s();
     async_t *async = make_async();
     if (!async)
         return -1;
@@ -409,8 +419,14 @@ int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
         bytestream_1_register_callback(c->material, cb);
         async_execute(async, cb);
     }
+    double t1 = now_s();
     int rc = nmsg ? async_loop(async) : 0;
     int err = rc < 0 ? errno : 0;
+    double t2 = now_s();
+    if (times) {
+        times[0] = t1 - t0; /* stack creation (queuestream copies) */
+        times[1] = t2 - t1; /* the loop: pulls, GPU batches, framing, reads */
+    }
     for (size_t i = 0; i < nmsg; i++) {
         out_len[i] = cs[i].len;
         if (!err && cs[i].err)
@@ -420,6 +436,89 @@ int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
     }
     destroy_async(async);
     free(cs);
+    if (err_out)
+        *err_out = err;
+    return err ? -1 : 0;
+}
+
+/* Config 5 over `nthreads` event loops (one per thread, each with its own
+ * hub): messages are split into contiguous ranges of about equal bytes.
+ * times[0] = slowest thread's setup, times[1] = wall time of the loops. */
+typedef struct {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    size_t first, count, max_chunk, read_size;
+    char pos62, pos63, padchar;
+    int pad;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint64_t *out_len;
+    int err;
+    double times[2];
+} egress_share;
+
+static void *egress_thread(void *arg)
+{
+    egress_share *e = arg;
+    size_t f = e->first;
+    /* out pointers are absolute; shift offsets to this share */
+    e->err = 0;
+    if (h_egress_stacks(e->in, e->in_off + f, e->count, e->max_chunk, e->read_size,
+                        e->pos62, e->pos63, e->pad, e->padchar, e->out,
+                        e->out_off + f, e->out_len + f, &e->err, e->times) < 0 &&
+        !e->err)
+        e->err = EIO;
+    return NULL;
+}
+
+#include <pthread.h>
+
+int h_egress_stacks_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                       size_t max_chunk, size_t read_size, char pos62, char pos63,
+                       int pad, char padchar, uint8_t *out, const uint64_t *out_off,
+                       uint64_t *out_len, int *err_out, double *times,
+                       size_t nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > nmsg)
+        nthreads = nmsg ? nmsg : 1;
+    egress_share *sh = calloc(nthreads, sizeof *sh);
+    pthread_t *th = calloc(nthreads, sizeof *th);
+    uint64_t total = in_off[nmsg];
+    size_t first = 0;
+    for (size_t t = 0; t < nthreads; t++) {
+        uint64_t goal = total / nthreads * (t + 1);
+        size_t last = first;
+        if (t + 1 == nthreads)
+            last = nmsg;
+        else
+            while (last < nmsg && in_off[last] < goal)
+                last++;
+        sh[t] = (egress_share) { in, in_off, first, last - first, max_chunk, read_size,
+                                 pos62, pos63, padchar, pad, out, out_off, out_len, 0,
+                                 { 0, 0 } };
+        first = last;
+    }
+    double t0 = now_s();
+    for (size_t t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, egress_thread, &sh[t]);
+    int err = 0;
+    double setup = 0;
+    for (size_t t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (!err && sh[t].err)
+            err = sh[t].err;
+        if (sh[t].times[0] > setup)
+            setup = sh[t].times[0];
+    }
+    double t1 = now_s();
+    if (times) {
+        times[0] = setup;
+        times[1] = t1 - t0 - setup;
+    }
+    free(sh);
+    free(th);
     if (err_out)
         *err_out = err;
     return err ? -1 : 0;

@@ -96,3 +96,18 @@ def test_config5_full():
         msg = payload[off:off + L].tobytes()
         off += L
         assert framed[i] == orc.chunked_encode(msg, max_chunk=1 << 20), i
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_egress_stacks_threads(threads):
+    """Several event loops (one per thread, each with its own hub) on one
+    GPU, sharing the messages."""
+    lens = util.zipf_lengths()[:400]
+    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240, threads=threads)
+    assert err == 0
+    off = 0
+    for i, L in enumerate(lens.tolist()):
+        msg = payload[off:off + L].tobytes()
+        off += L
+        assert framed[i] == orc.chunked_encode(msg, max_chunk=1 << 20), (i, L)

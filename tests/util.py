@@ -64,8 +64,10 @@ def harness() -> ctypes.CDLL:
                                      ctypes.POINTER(sz)]
         L.h_queue_stream.restype = ssz
         L.h_egress_stacks.argtypes = [vp, vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, vp,
-                                      vp, ip]
+                                      vp, ip, vp]
         L.h_egress_stacks.restype = ctypes.c_int
+        L.h_egress_stacks_mt.argtypes = L.h_egress_stacks.argtypes + [sz]
+        L.h_egress_stacks_mt.restype = ctypes.c_int
         _harness = L
     return _harness
 
@@ -173,9 +175,11 @@ def framed_cap(n: int, max_chunk: int) -> int:
 
 
 def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos62=-1,
-                  pos63=-1, pad=True, padchar=-1):
+                  pos63=-1, pad=True, padchar=-1, times=None, raw=False, threads=1):
     """Run len(lens) GPU egress stacks on one loop; returns
-    (list of framed bytes | None, errno)."""
+    (list of framed bytes | None, errno).  `times` (a float64[2] array)
+    receives the C-side setup and loop seconds; raw=True returns
+    (out, out_off, out_len) instead of a list."""
     lens = np.asarray(lens, dtype=np.uint64)
     in_off = np.zeros(lens.size + 1, np.uint64)
     np.cumsum(lens, out=in_off[1:])
@@ -183,14 +187,21 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
     out_off = np.zeros(lens.size + 1, np.uint64)
     np.cumsum(caps, out=out_off[1:])
     out = np.empty(int(out_off[-1]) or 1, np.uint8)
+    out.fill(0)  # fault the pages in outside the measured call
     out_len = np.zeros(max(lens.size, 1), np.uint64)
     err = ctypes.c_int(0)
     src = np.ascontiguousarray(payload, dtype=np.uint8)
-    rc = harness().h_egress_stacks(src.ctypes.data, in_off.ctypes.data, lens.size, max_chunk,
-                                   read_size, cch(pos62), cch(pos63), int(bool(pad)),
-                                   cch(padchar), out.ctypes.data, out_off.ctypes.data,
-                                   out_len.ctypes.data, ctypes.byref(err))
+    tp = times.ctypes.data if times is not None else None
+    args = (src.ctypes.data, in_off.ctypes.data, lens.size, max_chunk, read_size, cch(pos62),
+            cch(pos63), int(bool(pad)), cch(padchar), out.ctypes.data, out_off.ctypes.data,
+            out_len.ctypes.data, ctypes.byref(err), tp)
+    if threads > 1:
+        rc = harness().h_egress_stacks_mt(*args, threads)
+    else:
+        rc = harness().h_egress_stacks(*args)
     if rc != 0:
         return None, err.value
+    if raw:
+        return (out, out_off, out_len), 0
     return [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
             for i in range(lens.size)], 0
