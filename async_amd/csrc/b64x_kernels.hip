@@ -370,8 +370,9 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 }
 
 // Runtime tuning knobs (scripts/bench_variants.py; not part of the public
-// ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant.
-int g_tune[4] = {0, 0, 0, 0};
+// ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
+// chunks, 3 = plain-store pricing, 4 = 1: ungrouped strided batch kernels.
+int g_tune[5] = {0, 0, 0, 0, 0};
 
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(kThreads) void k_copy_probe(
 // quads per buffer; one tile of U slots per lane per block (non-persistent
 // grid), non-temporal loads and stores on whole, dword-aligned quads, the
 // buffer tails (and misaligned buffers) bytewise.
-template <int U>
+template <int U, bool NTL>
 __global__ __launch_bounds__(kThreads) void k_encode_strided(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
     uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
@@ -519,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_strided(
             dsts[u] = out + (uint64_t) b * out_stride + (uint64_t) q * 16;
             avails[u] = len - (uint64_t) q * 12;
             fast[u] = avails[u] >= 12 && ((((uintptr_t) srcs[u]) | ((uintptr_t) dsts[u])) & 3) == 0;
-            if (fast[u]) v[u] = ld12<true>(srcs[u]);
+            if (fast[u]) v[u] = ld12<NTL>(srcs[u]);
         }
     }
 #pragma unroll
@@ -533,6 +534,144 @@ __global__ __launch_bounds__(kThreads) void k_encode_strided(
             else
                 enc_bytes(tab, srcs[u], r, dsts[u], avails[u] <= 12, a);
         }
+    }
+}
+
+// Uniform-stride batch encode, grouped: block g owns buffers
+// [g*bpb, (g+1)*bpb) -- a run whose input and output spans start on 128-B
+// lines (bpb is chosen so), so no line is shared between blocks, which the
+// GPU spreads over XCDs with separate L2s (a shared line is fetched once
+// per XCD: the 22 % over-fetch of k_encode_strided on config 4).  Lanes
+// walk the block's bpb*qpb (buffer, quad) slots in order; the buffer index
+// is a multiply-high by magic = ceil(2^32/qpb), exact while slots < 2^16.
+template <int U, bool NTL>
+__global__ __launch_bounds__(kThreads) void k_encode_group(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
+    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
+    uint32_t qpb, uint32_t bpb, uint32_t magic, EncAlpha a)
+{
+    __shared__ uint8_t tab[64];
+    build_enc_table(tab, a);
+    __syncthreads();
+    const uint32_t b0 = blockIdx.x * bpb;
+    const uint32_t nb = min(bpb, nbuf - b0);
+    const uint32_t slots = nb * qpb;
+    const uint8_t *gin = in + (uint64_t) b0 * in_stride;
+    uint8_t *gout = out + (uint64_t) b0 * out_stride;
+    for (uint32_t s0 = 0; s0 < slots; s0 += U * kThreads) {
+        u32x3a4 v[U];
+        const uint8_t *srcs[U];
+        uint8_t *dsts[U];
+        uint32_t avails[U];
+        bool fast[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t t = s0 + u * kThreads + threadIdx.x;
+            fast[u] = false;
+            avails[u] = 0;
+            srcs[u] = gin;
+            dsts[u] = gout;
+            if (t < slots) {
+                const uint32_t b = __umulhi(t, magic), q = t - b * qpb;
+                srcs[u] = gin + (uint64_t) b * in_stride + q * 12u;
+                dsts[u] = gout + (uint64_t) b * out_stride + q * 16u;
+                const uint64_t av = len - (uint64_t) q * 12;
+                avails[u] = av > 12 ? 13u : (uint32_t) av;
+                fast[u] = av >= 12 && ((((uintptr_t) srcs[u]) | ((uintptr_t) dsts[u])) & 3) == 0;
+                if (fast[u]) v[u] = ld12<NTL>(srcs[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (fast[u]) {
+                store16<true>(dsts[u], enc_quad(tab, v[u].x, v[u].y, v[u].z));
+            } else if (avails[u]) {
+                const uint32_t r = avails[u] < 12 ? avails[u] : 12;
+                if (avails[u] < 12 && (((uintptr_t) srcs[u]) & 3) == 0)
+                    enc_tail(tab, srcs[u], r, dsts[u], a);
+                else
+                    enc_bytes(tab, srcs[u], r, dsts[u], avails[u] <= 12, a);
+            }
+        }
+    }
+}
+
+// Encode the lane whose 16 characters cross buffer b's padded last group
+// (len % 3 = r != 0): groups before it are ordinary, the partial group has
+// r bytes and its padding, groups after it belong to buffer b+1 and start
+// 3-r bytes earlier in the (contiguous) input.  x, y, z: the 12 input bytes
+// from the lane's first group on; p: the lane's character offset in b.
+DEV uint4 enc_seam(const uint8_t *tab, uint32_t x, uint32_t y, uint32_t z, uint32_t p,
+                   uint32_t E, uint32_t r, const EncAlpha &a)
+{
+    uint32_t o[4];
+#pragma unroll
+    for (uint32_t g = 0; g < 4; g++) {
+        const uint32_t c = p + 4 * g;
+        const bool partial = c + 4 == E, after = c + 4 > E;
+        const uint32_t off = 3 * g - (after ? 3 - r : 0);
+        const uint32_t wi = off >> 2, sh = (off & 3) * 8;
+        const uint32_t lo = wi == 0 ? x : wi == 1 ? y : z;
+        const uint32_t hi = wi == 0 ? y : wi == 1 ? z : 0u;
+        const uint32_t d = (uint32_t) ((((uint64_t) hi << 32) | lo) >> sh);
+        uint32_t b0 = d & 0xFFu, b1 = (d >> 8) & 0xFFu, b2 = (d >> 16) & 0xFFu;
+        if (partial) {
+            b2 = 0;
+            if (r == 1) b1 = 0;
+        }
+        uint32_t ch = enc_group(tab, (b0 << 16) | (b1 << 8) | b2);
+        if (partial)
+            ch = r == 1 ? (ch & 0xFFFFu) | (a.padc * 0x01010000u)
+                        : (ch & 0xFFFFFFu) | (a.padc << 24);
+        o[g] = ch;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Batch encode for the tight layout (in_stride = len, out_stride = E: the
+// batch is one contiguous character stream), indexed by output slot: lane
+// t writes characters [16t, 16t+16) with one aligned dwordx4 store and
+// reads the 12 bytes they come from with one dwordx4 load at the dword
+// below (realigned with v_alignbyte).  Only the lane that holds a
+// buffer's padded last group (one in E/16) takes enc_seam(); loads and
+// stores stay unmasked in full tiles (GUARD only in the remainder launch).
+// Buffer b = umulhi64(16t, ceil(2^64/E)); the last buffer is left to the
+// caller (its lanes could read past the input).
+template <int U, bool GUARD>
+__global__ __launch_bounds__(kThreads) void k_encode_tight(
+    const uint8_t *__restrict__ in, uint64_t len, uint32_t E, uint32_t r, uint64_t m64,
+    uint8_t *__restrict__ out, uint64_t slot0, uint64_t nslots, EncAlpha a)
+{
+    __shared__ uint8_t tab[64];
+    build_enc_table(tab, a);
+    __syncthreads();
+    uint32_t x[U], y[U], z[U], pp[U];
+    bool seam[U];
+    const uint64_t base = slot0 + (uint64_t) blockIdx.x * U * kThreads + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t t = base + (uint64_t) u * kThreads;
+        const uint64_t o = 16 * t;
+        const uint64_t b = __umul64hi(o, m64);
+        const uint32_t p = (uint32_t) (o - b * E);
+        const uint64_t pos = b * len + 3 * (uint64_t) (p >> 2);
+        pp[u] = p;
+        seam[u] = r != 0 && p + 16 >= E;
+        x[u] = y[u] = z[u] = 0;
+        if (!GUARD || t < nslots) {
+            const u32x4a4 w = __builtin_nontemporal_load((const u32x4a4 *) (in + (pos & ~3ull)));
+            const uint32_t s = (uint32_t) (pos & 3);
+            x[u] = __builtin_amdgcn_alignbyte(w.y, w.x, s);
+            y[u] = __builtin_amdgcn_alignbyte(w.z, w.y, s);
+            z[u] = __builtin_amdgcn_alignbyte(w.w, w.z, s);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t t = base + (uint64_t) u * kThreads;
+        uint4 c = enc_quad(tab, x[u], y[u], z[u]);
+        if (seam[u]) c = enc_seam(tab, x[u], y[u], z[u], pp[u], E, r, a);
+        if (!GUARD || t < nslots) store16<true>(out + 16 * t, c);
     }
 }
 
@@ -642,6 +781,29 @@ DEV void map_chunk(const uint8_t *tab_, uint4 w, uint32_t nin, LaneChunk &lc)
     // Re-read the table (volatile): sharing the hot path's lookups would keep
     // all 16 per-character values of every in-flight chunk alive.
     const volatile uint8_t *tab = tab_;
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = 4 * g + j;
+            uint32_t t = tab[(dw[g] >> (8 * j)) & 0xFFu];
+            bool ok = t < 64u && (uint32_t) k < nin;
+            v |= (ok ? t : 0u) << (18 - 6 * j);
+            m |= (ok ? 1u : 0u) << k;
+        }
+        lc.G[g] = v;
+    }
+    lc.vmask = m;
+}
+
+// map_chunk without the volatile re-read, for kernels whose table pointer
+// the compiler can see is LDS (a volatile access defeats address-space
+// inference and becomes a FLAT load, counted against VMEM).
+DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
+{
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
     uint32_t m = 0;
 #pragma unroll
@@ -1238,7 +1400,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
 // and publishes the buffer's length.  Any other slot marks the buffer.
 // Both go through atomicMax on outlen[] (zeroed by the launcher), so a mark
 // always wins; the fix-up then decodes marked buffers exactly.
-template <int U, bool PLAIN>
+template <int U, bool PLAIN, bool NTL>
 __global__ __launch_bounds__(kThreads) void k_decode_slots(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
     uint8_t *__restrict__ out, uint64_t out_stride,
@@ -1262,7 +1424,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
             const uint8_t *src = in + (uint64_t) b * in_stride + (uint64_t) q * 16;
             const uint64_t avail = len - (uint64_t) q * 16;
             nin[u] = avail >= 16 ? 16u : (uint32_t) avail;
-            if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<true>(src);
+            if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<NTL>(src);
             else w[u] = load_chars(src, nin[u]);
         }
     }
@@ -1300,6 +1462,144 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
         } else {
             if (PLAIN) outlen[b] = kNeedsExact;
             else atomicMax(&outlen[b], (unsigned long long) kNeedsExact);
+        }
+    }
+}
+
+// Uniform-stride batch decode for rows with room (out_stride >= 12*S):
+// every lane loads 16
+// characters and stores 12 bytes unconditionally, so no memory operation
+// is exec-masked.  The last slot of a row over-reads into the next row's
+// characters and over-writes past out_len inside its own row (those bytes
+// are unspecified, include/b64x.h); its length follows the prefix rule.
+// A lane that is not clean marks the row for k_decode_batch_fix, which
+// rewrites it exactly.  The caller excludes the last row (its last slot
+// could read past the input) and runs it through k_decode_slots.
+template <int U, bool GUARD>
+__global__ __launch_bounds__(kThreads) void k_decode_rows(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
+    uint8_t *__restrict__ out, uint64_t out_stride,
+    unsigned long long *__restrict__ outlen, uint32_t S, uint64_t m64, uint64_t slot0,
+    uint64_t nslots, DecAlpha a)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint64_t base = slot0 + (uint64_t) blockIdx.x * U * kThreads + threadIdx.x;
+    uint4 w[U];
+    uint64_t bb[U];
+    uint32_t qq[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t t = base + (uint64_t) u * kThreads;
+        const uint64_t b = __umul64hi(t, m64);
+        bb[u] = b;
+        qq[u] = (uint32_t) (t - b * S);
+        w[u] = make_uint4(0, 0, 0, 0);
+        if (!GUARD || t < nslots)
+            w[u] = ld16<true>(in + b * in_stride + 16ull * qq[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t t = base + (uint64_t) u * kThreads;
+        const uint32_t q = qq[u];
+        const bool last = q == S - 1;
+        const uint32_t nin = last ? (uint32_t) (len - 16ull * q) : 16u;
+        uint32_t G[4], bad;
+        map_fast(tab, w[u], nin, G, bad);
+        uint32_t k = 16;
+        bool ok = bad == 0;
+        if (last && !ok) {
+            LaneChunk lc;
+            map_chunk_lds(tab, w[u], nin, lc);
+            const uint32_t m = lc.vmask;
+            ok = (m & (m + 1)) == 0;  // alphabet characters form a prefix
+            k = __popc(m);
+#pragma unroll
+            for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+        }
+        uint32_t o0, o1, o2;
+        groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+        if (!GUARD || t < nslots) {
+            __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
+                                        (u32x3a4 *) (out + bb[u] * out_stride + 12ull * q));
+            if (!ok)
+                atomicMax(&outlen[bb[u]], (unsigned long long) kNeedsExact);
+            else if (last)
+                atomicMax(&outlen[bb[u]], (unsigned long long) ((16ull * q + k) * 6 / 8));
+        }
+    }
+}
+
+// Grouped twin of k_decode_slots (see k_encode_group): block g owns
+// buffers [g*bpb, (g+1)*bpb), lanes walk its bpb*S 16-character slots.
+template <int U, bool NTL>
+__global__ __launch_bounds__(kThreads) void k_decode_group(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
+    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
+    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t bpb, uint32_t magic,
+    DecAlpha a)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint32_t b0 = blockIdx.x * bpb;
+    const uint32_t nb = min(bpb, nbuf - b0);
+    const uint32_t slots = nb * S;
+    const uint8_t *gin = in + (uint64_t) b0 * in_stride;
+    uint8_t *gout = out + (uint64_t) b0 * out_stride;
+    for (uint32_t s0 = 0; s0 < slots; s0 += U * kThreads) {
+        uint4 w[U];
+        uint32_t nin[U], bq[U][2];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t t = s0 + u * kThreads + threadIdx.x;
+            nin[u] = 0;
+            bq[u][0] = bq[u][1] = 0;
+            w[u] = make_uint4(0, 0, 0, 0);
+            if (t < slots) {
+                const uint32_t b = __umulhi(t, magic), q = t - b * S;
+                bq[u][0] = b;
+                bq[u][1] = q;
+                const uint8_t *src = gin + (uint64_t) b * in_stride + q * 16u;
+                const uint64_t avail = len - (uint64_t) q * 16;
+                nin[u] = avail >= 16 ? 16u : (uint32_t) avail;
+                if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<NTL>(src);
+                else w[u] = load_chars(src, nin[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!nin[u]) continue;
+            const uint32_t b = bq[u][0], q = bq[u][1];
+            uint8_t *dst = gout + (uint64_t) b * out_stride + q * 12u;
+            uint32_t G[4], bad;
+            map_fast(tab, w[u], nin[u], G, bad);
+            uint32_t nbytes = 12, k = 16;
+            bool ok = bad == 0;
+            if (!ok && q == S - 1) {
+                LaneChunk lc;
+                map_chunk(tab, w[u], nin[u], lc);
+                const uint32_t m = lc.vmask;
+                ok = (m & (m + 1)) == 0;  // alphabet characters form a prefix
+                k = __popc(m);
+                nbytes = 3 * (k >> 2) + ((6 * (k & 3)) >> 3);
+#pragma unroll
+                for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+            }
+            if (ok) {
+                uint32_t o0, o1, o2;
+                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+                if (nbytes == 12 && (((uintptr_t) dst) & 3) == 0) {
+                    __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+                } else if (nbytes) {
+                    store_bytes12(dst, o0, o1, o2, nbytes);
+                }
+                if (q == S - 1)
+                    atomicMax(&outlen[b0 + b], (unsigned long long) ((16ull * q + k) * 6 / 8));
+            } else {
+                atomicMax(&outlen[b0 + b], (unsigned long long) kNeedsExact);
+            }
         }
     }
 }
@@ -1587,6 +1887,34 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
     return launch_status();
 }
 
+// Buffers per block for the grouped batch kernels: enough slots per block
+// (~4 per lane) and, where a power of two up to 64 allows, input and output
+// spans that start on 128-B lines.  0 = the grouped kernels do not apply
+// (slots per block must stay below 2^16 for the multiply-high division).
+// g_tune[4] bits: 1 = grouped batch kernels, 2 = temporal (cached) loads.
+static bool batch_ntl() { return !(g_tune[4] & 2); }
+
+static uint32_t plan_group(uint64_t slots_per_buf, uint64_t in_stride, uint64_t out_stride)
+{
+    if (!(g_tune[4] & 1) || slots_per_buf == 0 || slots_per_buf >= (1u << 15)) return 0;
+    uint32_t bpb = 1;
+    while ((uint64_t) bpb * slots_per_buf < 4 * kThreads && 2 * bpb * slots_per_buf < 65536)
+        bpb *= 2;
+    uint32_t best = bpb;
+    for (uint32_t p = bpb; p <= 64 && (uint64_t) p * slots_per_buf < 65536; p *= 2) {
+        if ((p * in_stride) % 128 == 0 && (p * out_stride) % 128 == 0) {
+            best = p;
+            break;
+        }
+    }
+    return best;
+}
+
+static uint32_t magic_of(uint32_t d)  // ceil(2^32 / d), d >= 2
+{
+    return (uint32_t) ((0xFFFFFFFFull + d) / d);
+}
+
 int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                         uint32_t nbuf, void *d_out, uint64_t out_stride,
                         const b64x_alphabet *abc, void *stream)
@@ -1602,8 +1930,54 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
     constexpr int U = 2;
+    const EncAlpha ea = enc_alpha(abc);
+    const uint64_t E = b64x_encoded_len(len, ea.pad);
+    const uint32_t r = (uint32_t) (len % 3);
+    // Tight layout: one contiguous character stream (k_encode_tight).
+    if (g_tune[4] == 0 && in_stride == len && out_stride == E && nbuf >= 3 && len >= 16 &&
+        (ea.pad || r == 0) && E < (1ull << 32) && (((uintptr_t) d_in) & 3) == 0 &&
+        (((uintptr_t) d_out) & 15) == 0) {
+        const uint64_t m64 = ~0ull / E + 1;  // ceil(2^64 / E)
+        const uint64_t nslots = (nbuf - 1) * E / 16;  // lanes wholly before the last buffer
+        const uint64_t tile = (uint64_t) U * kThreads;
+        const uint64_t full = nslots / tile;
+        hipStream_t st = (hipStream_t) stream;
+        int err;
+        if (full) {
+            hipLaunchKernelGGL((k_encode_tight<U, false>), dim3((uint32_t) full), dim3(kThreads),
+                               0, st, (const uint8_t *) d_in, len, (uint32_t) E, r, m64,
+                               (uint8_t *) d_out, (uint64_t) 0, nslots, ea);
+            if ((err = launch_status())) return err;
+        }
+        if (nslots > full * tile) {
+            hipLaunchKernelGGL((k_encode_tight<U, true>), dim3(1), dim3(kThreads), 0, st,
+                               (const uint8_t *) d_in, len, (uint32_t) E, r, m64,
+                               (uint8_t *) d_out, full * tile, nslots, ea);
+            if ((err = launch_status())) return err;
+        }
+        // The last two buffers whole (the second-to-last may end inside the
+        // last slot above; rewriting it is idempotent).
+        const uint8_t *tin = (const uint8_t *) d_in + (nbuf - 2) * len;
+        uint8_t *tout = (uint8_t *) d_out + (nbuf - 2) * E;
+        auto k = k_encode_strided<U, true>;
+        hipLaunchKernelGGL(k, dim3((uint32_t) ((2 * qpb + U * kThreads - 1) / (U * kThreads))),
+                           dim3(kThreads), 0, st, tin, in_stride, len, 2u, tout, out_stride,
+                           (uint32_t) qpb, (uint32_t) (2 * qpb), ea);
+        return launch_status();
+    }
+    const uint32_t bpb = qpb >= 2 ? plan_group(qpb, in_stride, out_stride) : 0;
+    const bool ntl = batch_ntl();
+    if (bpb) {
+        auto k = ntl ? k_encode_group<U, true> : k_encode_group<U, false>;
+        hipLaunchKernelGGL(k, dim3((uint32_t) ((nbuf + bpb - 1) / bpb)),
+                           dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
+                           in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
+                           bpb, magic_of((uint32_t) qpb), enc_alpha(abc));
+        return launch_status();
+    }
     const uint64_t per_block = (uint64_t) kThreads * U;
-    hipLaunchKernelGGL(k_encode_strided<U>, dim3((uint32_t) ((slots + per_block - 1) / per_block)),
+    auto k = ntl ? k_encode_strided<U, true> : k_encode_strided<U, false>;
+    hipLaunchKernelGGL(k, dim3((uint32_t) ((slots + per_block - 1) / per_block)),
                        dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
                        in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
                        (uint32_t) slots, enc_alpha(abc));
@@ -1722,17 +2096,60 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     const DecAlpha a = dec_alpha(abc);
     int err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s));
     if (err) return err;
-    if (slots) {
+    const uint32_t bpb = S >= 2 && g_tune[3] != 1 ? plan_group(S, in_stride, out_stride) : 0;
+    const bool ntl = batch_ntl();
+    // Rows with room: the uniform kernel over all rows but the last.
+    if (g_tune[4] == 0 && nbuf >= 2 && S >= 2 && out_stride >= 12 * S && (in_stride & 3) == 0 &&
+        (out_stride & 3) == 0 && (((uintptr_t) d_in) & 3) == 0 &&
+        (((uintptr_t) d_out) & 3) == 0) {
+        constexpr int U = 2;
+        const uint64_t m64 = ~0ull / S + 1;  // ceil(2^64 / S)
+        const uint64_t nrows = (uint64_t) S * (nbuf - 1);
+        const uint64_t tile = (uint64_t) U * kThreads, full = nrows / tile;
+        if (full) {
+            hipLaunchKernelGGL((k_decode_rows<U, false>), dim3((uint32_t) full), dim3(kThreads), 0,
+                               s, (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, m64,
+                               (uint64_t) 0, nrows, a);
+            if ((err = launch_status())) return err;
+        }
+        if (nrows > full * tile) {
+            hipLaunchKernelGGL((k_decode_rows<U, true>), dim3(1), dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, m64,
+                               full * tile, nrows, a);
+            if ((err = launch_status())) return err;
+        }
+        const uint64_t lb = nbuf - 1;
+        hipLaunchKernelGGL((k_decode_slots<U, false, true>), dim3((S + U * kThreads - 1) / (U * kThreads)),
+                           dim3(kThreads), 0, s, (const uint8_t *) d_in + lb * in_stride,
+                           in_stride, len, (uint8_t *) d_out + lb * out_stride, out_stride,
+                           (unsigned long long *) d_outlen + lb, (uint32_t) S, (uint32_t) S, a);
+        if ((err = launch_status())) return err;
+    } else if (slots && bpb) {
+        constexpr int U = 2;
+        auto k = ntl ? k_decode_group<U, true> : k_decode_group<U, false>;
+        hipLaunchKernelGGL(k, dim3((nbuf + bpb - 1) / bpb), dim3(kThreads), 0, s,
+                           (const uint8_t *) d_in, in_stride, len, nbuf, (uint8_t *) d_out,
+                           out_stride, (unsigned long long *) d_outlen, (uint32_t) S, bpb,
+                           magic_of((uint32_t) S), a);
+        if ((err = launch_status())) return err;
+    } else if (slots) {
         constexpr int U = 2;
         const uint64_t per_block = (uint64_t) kThreads * U;
         const dim3 g((uint32_t) ((slots + per_block - 1) / per_block));
         if (g_tune[3] == 1)  // benchmark-only: racy plain stores (prices the atomics)
-            hipLaunchKernelGGL((k_decode_slots<U, true>), g, dim3(kThreads), 0, s,
+            hipLaunchKernelGGL((k_decode_slots<U, true, true>), g, dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
+                               (uint32_t) slots, a);
+        else if (ntl)
+            hipLaunchKernelGGL((k_decode_slots<U, false, true>), g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
                                out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
                                (uint32_t) slots, a);
         else
-            hipLaunchKernelGGL((k_decode_slots<U, false>), g, dim3(kThreads), 0, s,
+            hipLaunchKernelGGL((k_decode_slots<U, false, false>), g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
                                out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
                                (uint32_t) slots, a);
@@ -2084,7 +2501,7 @@ int b64x_lane_wait(b64x_lane *l)
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)
 {
-    if (idx < 0 || idx >= 4) return -EINVAL;
+    if (idx < 0 || idx >= 5) return -EINVAL;
     int old = g_tune[idx];
     g_tune[idx] = value;
     return old;

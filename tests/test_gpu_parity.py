@@ -215,17 +215,76 @@ def _strided_check(nbuf, length, sample_idx, g4=None):
         assert ehost[i * qstride_out:(i + 1) * qstride_out].tobytes() == want, i
     if g4:
         assert hashlib.sha256(ehost[:qstride_out].tobytes()).hexdigest().startswith(g4)
-    cap = b64.decoded_cap(qstride_out)
-    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
-    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
-    b64.decode_strided(enc, qstride_out, qstride_out, nbuf, dec, cap, outlen)
-    assert int(outlen.min()) == length and int(outlen.max()) == length
-    assert torch.equal(dec.view(nbuf, cap)[:, :length], x.view(nbuf, length))
+    # exact-capacity rows (per-slot kernel) and 16-byte rows (the uniform
+    # row kernel needs out_stride >= 12 * ceil(E/16))
+    for cap in (b64.decoded_cap(qstride_out), (b64.decoded_cap(qstride_out) + 15) // 16 * 16):
+        dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+        outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+        b64.decode_strided(enc, qstride_out, qstride_out, nbuf, dec, cap, outlen)
+        assert int(outlen.min()) == length and int(outlen.max()) == length
+        assert torch.equal(dec.view(nbuf, cap)[:, :length], x.view(nbuf, length))
 
 
 def test_strided_small_shapes():
     for nbuf, length in ((1, 1), (3, 2), (7, 3), (64, 12), (100, 1023), (33, 5000)):
         _strided_check(nbuf, length, range(nbuf))
+
+
+@pytest.mark.parametrize("length", [16, 17, 18, 19, 20, 21, 22, 23, 28, 100, 101, 102, 1000,
+                                    1001, 1024, 4096, 4097])
+@pytest.mark.parametrize("nbuf", [3, 4, 257])
+def test_strided_tight_layout(length, nbuf):
+    """in_stride = len, out_stride = E: the output-indexed tight kernel
+    (every len mod 3 and E mod 16 seam shape) plus its tail launch."""
+    _strided_check(nbuf, length, range(nbuf))
+
+
+@pytest.mark.parametrize("abc", [("-", "_", True, "#"), (".", "_", False, -1)])
+def test_strided_tight_alphabets(abc):
+    rng = np.random.default_rng(5)
+    for length in (1024, 1026, 31):
+        nbuf = 50
+        E = b64.encoded_len(length, abc[2])
+        host = rng.integers(0, 256, nbuf * length, dtype=np.uint8)
+        enc = torch.zeros(nbuf * E, dtype=torch.uint8, device=DEV)
+        b64.encode_strided(dev(host), length, length, nbuf, enc, E, abc=abc)
+        eh = enc.cpu().numpy()
+        for i in range(nbuf):
+            assert eh[i * E:(i + 1) * E].tobytes() == orc.encode(
+                host[i * length:(i + 1) * length], *abc), (length, i)
+
+
+@pytest.mark.parametrize("cap_extra", [0, 5, 16])
+@pytest.mark.parametrize("length,gap_in,gap_out", [(777, 5, 3), (1024, 0, 0), (4096, 16, 8),
+                                                   (13, 1, 0), (100, 0, 7)])
+def test_strided_odd_strides_and_junk(length, gap_in, gap_out, cap_extra):
+    """Grouped batch kernels with strides that break line alignment, plus
+    buffers with junk (exact fix-up path), each buffer vs the oracle."""
+    rng = np.random.default_rng(length + gap_in)
+    nbuf = 301
+    E = b64.encoded_len(length)
+    ins, outs = length + gap_in, E + gap_out
+    host = rng.integers(0, 256, nbuf * ins, dtype=np.uint8)
+    x = dev(host)
+    enc = torch.zeros(nbuf * outs, dtype=torch.uint8, device=DEV)
+    b64.encode_strided(x, ins, length, nbuf, enc, outs)
+    eh = enc.cpu().numpy()
+    for i in range(nbuf):
+        want = orc.encode(host[i * ins:i * ins + length])
+        assert eh[i * outs:i * outs + E].tobytes() == want, i
+    # junk in every 7th buffer: a CR, a '=', a run of spaces
+    for i in range(0, nbuf, 7):
+        j = i * outs + int(rng.integers(0, E))
+        eh[j] = (13, 61, 32)[i % 3]
+    cap = b64.decoded_cap(E) + cap_extra
+    dec = torch.zeros(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(dev(eh), outs, E, nbuf, dec, cap, outlen)
+    dh, ol = dec.cpu().numpy(), outlen.cpu().numpy()
+    for i in range(nbuf):
+        want = orc.decode(eh[i * outs:i * outs + E])
+        assert int(ol[i]) == len(want), i
+        assert dh[i * cap:i * cap + len(want)].tobytes() == want, i
 
 
 @pytest.mark.slow
