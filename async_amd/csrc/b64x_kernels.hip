@@ -977,7 +977,7 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
                 }
             }
             LaneChunk lc;
-            map_chunk(tab, w[u], nin[u], lc);
+            map_chunk_lds(tab, w[u], nin[u], lc);
             if (st.carry == 0 && is_last && cpos + kChunk >= re) {
                 int got = fast_prefix(lc, hold, out + 3 * st.groups);
                 if (got >= 0) {
@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
             }
         }
         LaneChunk lc;
-        map_chunk(tab, w, nin, lc);
+        map_chunk_lds(tab, w, nin, lc);
         cnt += __popc(lc.vmask);
         if (dirty == kNoDirty) {
             const bool final = last && pos + kChunk >= re;
@@ -1153,9 +1153,17 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
     if (lane == 0) {
         DecodeWs v = ws_view(ws, nranges);
         v.counts[r] = cnt;
-        if (dirty != kNoDirty)
-            atomicMax((unsigned long long *) v.fd,
-                      (unsigned long long) ~(((uint64_t) r << 32) | dirty));
+        if (dirty != kNoDirty) {
+            // Only an improvement is published: on input that is dirty
+            // everywhere (CRLF every 76 characters) every range would
+            // otherwise hit this one word with an atomic, serialised at
+            // its L2 channel.  The device-scope load sees what earlier
+            // ranges published.
+            const unsigned long long key = ~(((uint64_t) r << 32) | dirty);
+            const unsigned long long cur = __hip_atomic_load(
+                (unsigned long long *) v.fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (key > cur) atomicMax((unsigned long long *) v.fd, key);
+        }
     }
 }
 

@@ -173,6 +173,10 @@ def bench_batch(args, world, rank, b64):
                                                         x.view(nbuf, L)))
     if not ok:
         raise SystemExit(f"rank {rank}: batch round trip mismatch")
+    # warm the exchange path too (first reduction / collective launches load
+    # their code objects and set up communicators)
+    for _ in range(2):
+        _, tot_list = shard.exchange_totals(int(outlen.sum()), device=coll_device())
     K = args.batch_steps
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     sync_all(world)
