@@ -371,8 +371,10 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 
 // Runtime tuning knobs (scripts/bench_variants.py; not part of the public
 // ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
-// chunks, 3 = plain-store pricing, 4 = 1: ungrouped strided batch kernels.
-int g_tune[5] = {0, 0, 0, 0, 0};
+// chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
+// bit 1 cached loads, any bit: not the tight/row kernels), 5 = 1: the
+// chunk-by-chunk pass 2.
+int g_tune[6] = {0, 0, 0, 0, 0, 0};
 
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
@@ -1277,6 +1279,178 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2(
     }
 }
 
+// ---- pass 2, one-shot per range (ranges of at most kP2Range characters) --
+//
+// k_decode_pass2 works chunk by chunk with a carry through LDS, a 6-step
+// __shfl_up scan, three wave fences per chunk and a dependent lookahead
+// load at the end of every range, on 4 waves per SIMD: latency-bound on
+// input that is dirty everywhere (CRLF-76).  This version issues all of a
+// range's loads at once (its base, both chunks, 64 lookahead bytes),
+// prefix-sums with ballot bit planes, compacts the whole range's sextets
+// into the wave's LDS buffer, converts them to bytes in LDS and stores the
+// bytes with dword stores realigned to the output (v_alignbyte), one
+// fence per stage.
+constexpr uint32_t kP2Range = 2048;
+constexpr uint32_t kP2Sx = kP2Range + 64;        // + lookahead, 16-aligned
+constexpr uint32_t kP2Bb = kP2Range / 4 * 3 + 64;
+
+struct __attribute__((aligned(16))) P2Smem {
+    uint8_t tab[256];
+    uint8_t sx[kWavesPerBlock][kP2Sx];
+    uint32_t bb[kWavesPerBlock][kP2Bb / 4];
+};
+
+// Exclusive prefix over the wave of x < 32, and the total: one ballot per
+// bit plane, no LDS traffic.
+DEV uint32_t wave_scan_small(uint32_t x, uint32_t &total)
+{
+    uint32_t ex = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const uint64_t b = __ballot((x >> i) & 1u);
+        ex += __builtin_amdgcn_mbcnt_hi((uint32_t) (b >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t) b, 0u)) << i;
+        tot += (uint32_t) __popcll(b) << i;
+    }
+    total = tot;
+    return ex;
+}
+
+// Store bytes bb[0..nb) (in LDS) to global `dst` (any alignment): dword
+// k of the aligned span covers dst bytes 4k-s .. 4k-s+3 (s = dst & 3).
+DEV void store_realigned(const uint32_t *bb, uint32_t nb, uint8_t *dst)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t s = (uint32_t) ((uintptr_t) dst & 3);
+    uint8_t *a0 = dst - s;
+    const uint32_t K = (s + nb + 3) >> 2;
+    for (uint32_t k0 = 3 * lane; k0 < K; k0 += 3 * 64) {
+        uint32_t d[3];
+        bool full = true;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const uint32_t k = k0 + i;
+            const uint32_t cur = k * 4 < nb + s ? bb[k < (nb + 3) / 4 ? k : 0] : 0u;
+            const uint32_t prv = k ? bb[k - 1] : 0u;
+            d[i] = s == 0 ? cur : __builtin_amdgcn_alignbyte(cur, prv, 4 - s);
+            const int j0 = (int) (4 * k) - (int) s;
+            full = full && j0 >= 0 && (uint32_t) j0 + 4 <= nb;
+        }
+        if (full) {
+            *(u32x3a4 *) (a0 + 4 * k0) = u32x3a4{d[0], d[1], d[2]};
+            continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int j0 = (int) (4 * (k0 + i)) - (int) s;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int j = j0 + b;
+                if (j >= 0 && (uint32_t) j < nb) dst[j] = (uint8_t) (d[i] >> (8 * b));
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_pass2b(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
+{
+    DecodeWs w = ws_view(ws, nranges);
+    const uint64_t packed = *w.fd_cur;
+    if (packed == 0) return;
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t off0 = (uint32_t) ~packed;
+    __shared__ P2Smem sm;
+    build_dec_table(sm.tab, a);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *sx = sm.sx[wv];
+    uint32_t *bb = sm.bb[wv];
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges, first = r == r0;
+        const uint64_t start = first ? rb + off0 : rb;
+        // every load of the range up front
+        const uint64_t B = w.bases[r];
+        uint4 c[2];
+        uint32_t nin[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+        }
+        const bool la_ok = !last && re + lane < n;
+        uint32_t la = la_ok ? in[re + lane] : 0u;
+        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
+        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            LaneChunk lc;
+            map_chunk_lds(sm.tab, c[h], nin[h], lc);
+            uint32_t tot;
+            const uint32_t ex = wave_scan_small(__popc(lc.vmask), tot);
+            int pos = T + (int) ex;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if ((lc.vmask >> k) & 1u) {
+                    if (pos >= 0) sx[pos] = (uint8_t) sextet(lc, k);
+                    pos++;
+                }
+            }
+            T += (int) tot;
+        }
+        bool at_end = last;
+        if (!last && T > 0 && (T & 3)) {
+            // complete the range's last group from the characters after it
+            bool ok = la_ok;
+            for (uint64_t q = re;;) {
+                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+                const bool v = t < 64u;
+                const uint64_t m = __ballot(v);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                const int need = 4 - (T & 3);
+                if (v && (int) rank < need) sx[T + rank] = (uint8_t) t;
+                const int got = __popcll(m);
+                if (got >= need) {
+                    T += need;
+                    break;
+                }
+                T += got;
+                q += 64;
+                if (q >= n) {
+                    at_end = true;  // the stream's final, incomplete group
+                    break;
+                }
+                ok = q + lane < n;
+                la = ok ? in[q + lane] : 0u;
+            }
+        }
+        wave_lds_order();
+        if (T > 0) {
+            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
+            for (uint32_t L = lane; 4 * L < ng; L += 64) {
+                const uint4 sv = *(const uint4 *) (sx + 16 * L);
+                uint32_t o0, o1, o2;
+                groups_to_bytes(group_of_bytes(sv.x), group_of_bytes(sv.y),
+                                group_of_bytes(sv.z), group_of_bytes(sv.w), o0, o1, o2);
+                bb[3 * L] = o0;
+                bb[3 * L + 1] = o1;
+                bb[3 * L + 2] = o2;
+            }
+            wave_lds_order();
+            store_realigned(bb, 3 * ng, ob);
+            if (rem && at_end && !hold) emit_partial(sx + 4 * ng, ob + 3 * ng, (int) rem);
+        }
+        wave_lds_order();  // the next range reuses sx and bb
+    }
+}
+
 // Batches: buffer b is in[ioff(b) .. +len(b)) -> out + ooff(b).
 struct BatchLayout {
     const uint64_t *in_off;   // nbuf+1 offsets, or null for a uniform stride
@@ -2055,6 +2229,13 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
                        nchars, p.R, p.nranges, a, ws, d_res, hold);
     if ((err = launch_status())) return err;
+    if (p.R <= kP2Range && g_tune[5] == 0) {
+        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 8);
+        hipLaunchKernelGGL(k_decode_pass2b, dim3(b2), dim3(kThreads), 0, s,
+                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+                           a, ws, hold);
+        return launch_status();
+    }
     const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 4);
     hipLaunchKernelGGL(k_decode_pass2, dim3(b2), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
@@ -2509,7 +2690,7 @@ int b64x_lane_wait(b64x_lane *l)
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)
 {
-    if (idx < 0 || idx >= 5) return -EINVAL;
+    if (idx < 0 || idx >= 6) return -EINVAL;
     int old = g_tune[idx];
     g_tune[idx] = value;
     return old;
