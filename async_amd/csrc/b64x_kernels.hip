@@ -373,8 +373,9 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
 // chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
 // bit 1 cached loads, any bit: not the tight/row kernels), 5 = 1: the
-// chunk-by-chunk pass 2.
-int g_tune[6] = {0, 0, 0, 0, 0, 0};
+// chunk-by-chunk pass 2, 6 = 1: the first-form tight/row batch kernels,
+// 7 = lanes' slots per batch-kernel tile (2 or 4).
+int g_tune[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
@@ -677,6 +678,109 @@ __global__ __launch_bounds__(kThreads) void k_encode_tight(
     }
 }
 
+// The seam lane of k_encode_tight2: x, y, z are the 12 input bytes from
+// the lane's first group on, q the normal encoding of them, p the lane's
+// character offset in its buffer (p + 16 >= E, r = len % 3 != 0).  Groups
+// before the partial group gs are q's; the partial group keeps q's first
+// r characters, gets the character of the zero-extended last byte and the
+// padding (finalize(), src/base64encoder.c:61-99); groups after it start
+// the next buffer, whose bytes sit 3 - r earlier than a full group would
+// put them -- i.e. the 9 bytes from offset r, encoded one group later.
+DEV uint4 enc_seam2(const uint8_t *tab, uint32_t x, uint32_t y, uint32_t z, uint4 q,
+                    uint32_t p, uint32_t E, uint32_t r, const EncAlpha &a)
+{
+    const uint32_t gs = ((E - p) >> 2) - 1;  // 0..3
+    // groups of the next buffer: bytes r .. r+8 of x:y:z
+    const uint32_t x2 = __builtin_amdgcn_alignbyte(y, x, r);
+    const uint32_t y2 = __builtin_amdgcn_alignbyte(z, y, r);
+    const uint32_t z2 = __builtin_amdgcn_alignbyte(0u, z, r);
+    const uint32_t n0 = enc_group(tab, __builtin_amdgcn_perm(0u, x2, 0x0c000102u));
+    const uint32_t n1 = enc_group(tab, __builtin_amdgcn_perm(y2, x2, 0x0c030405u));
+    const uint32_t n2 = enc_group(tab, __builtin_amdgcn_perm(z2, y2, 0x0c020304u));
+    // the partial group: last real byte is byte 3*gs + r - 1 of x:y:z
+    const uint32_t bi = 3 * gs + r - 1;
+    const uint32_t wd = bi < 4 ? x : bi < 8 ? y : z;
+    const uint32_t lb = (wd >> (8 * (bi & 3))) & 0xFFu;
+    const uint32_t qg = gs == 0 ? q.x : gs == 1 ? q.y : gs == 2 ? q.z : q.w;
+    const uint32_t pads = a.padc * 0x01010101u;
+    const uint32_t pg = r == 1
+        ? (qg & 0xFFu) | ((uint32_t) tab[(lb & 3u) << 4] << 8) | (pads & 0xFFFF0000u)
+        : (qg & 0xFFFFu) | ((uint32_t) tab[(lb & 15u) << 2] << 16) | (pads & 0xFF000000u);
+    uint4 o;
+    o.x = gs == 0 ? pg : q.x;
+    o.y = gs == 1 ? pg : gs == 0 ? n0 : q.y;
+    o.z = gs == 2 ? pg : gs < 2 ? n1 : q.z;
+    o.w = gs == 3 ? pg : n2;
+    return o;
+}
+
+// Tight-layout batch encode, second form: the block's first output slot
+// gives its buffer b0 and offset p0 once (scalar), each lane's slot is a
+// 32-bit offset from there, split with a 32-bit multiply-high (magic =
+// ceil(2^32/E), exact below 2^32/E -- the launcher checks).  Seam lanes
+// (one per buffer) take enc_seam2.  Blocks that touch the last two buffers
+// or the end of the output ("tail" blocks, block-uniform) guard their
+// loads and stores, so one launch covers the whole batch.
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_encode_tight2(
+    const uint8_t *__restrict__ in, uint64_t len, uint32_t E, uint32_t r, uint32_t magic,
+    uint64_t m64, uint8_t *__restrict__ out, uint64_t nslots, uint64_t total_in,
+    uint64_t total_out, uint64_t tail_slot, EncAlpha a)
+{
+    __shared__ uint8_t tab[64];
+    build_enc_table(tab, a);
+    __syncthreads();
+    const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
+    const uint64_t b0 = __umul64hi(16 * s0, m64);
+    const uint32_t p0 = (uint32_t) (16 * s0 - b0 * E);
+    const uint8_t *ib = in + b0 * len;
+    uint32_t pp[U];
+    uint64_t pos[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t rel = p0 + 16u * (u * kThreads + threadIdx.x);
+        const uint32_t bl = __umulhi(rel, magic);
+        pp[u] = rel - bl * E;
+        pos[u] = (uint64_t) bl * len + 3 * (pp[u] >> 2);
+    }
+    if (s0 + U * kThreads > tail_slot) {
+        // tail block: guarded loads (the last buffer's windows may run past
+        // the input) and stores (the output may end inside a slot)
+        for (int u = 0; u < U; u++) {
+            const uint64_t t = s0 + u * kThreads + threadIdx.x;
+            if (t >= nslots) continue;
+            const uint8_t *src = ib + (pos[u] & ~3ull);
+            const uint64_t gofs = (uint64_t) (src - in);
+            const uint32_t nin = total_in - gofs >= 16 ? 16u : (uint32_t) (total_in - gofs);
+            const uint4 w = load_chars(src, nin);
+            const uint32_t s = (uint32_t) (pos[u] & 3);
+            const uint32_t x = __builtin_amdgcn_alignbyte(w.y, w.x, s);
+            const uint32_t y = __builtin_amdgcn_alignbyte(w.z, w.y, s);
+            const uint32_t z = __builtin_amdgcn_alignbyte(w.w, w.z, s);
+            uint4 c = enc_quad(tab, x, y, z);
+            if (r != 0 && pp[u] + 16 >= E) c = enc_seam2(tab, x, y, z, c, pp[u], E, r, a);
+            const uint32_t dw[4] = {c.x, c.y, c.z, c.w};
+            const uint64_t left = total_out - 16 * t;
+            store_bytes16(out + 16 * t, dw, left >= 16 ? 16u : (uint32_t) left);
+        }
+        return;
+    }
+    u32x4a4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        w[u] = __builtin_nontemporal_load((const u32x4a4 *) (ib + (pos[u] & ~3ull)));
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t s = (uint32_t) (pos[u] & 3);
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[u].y, w[u].x, s);
+        const uint32_t y = __builtin_amdgcn_alignbyte(w[u].z, w[u].y, s);
+        const uint32_t z = __builtin_amdgcn_alignbyte(w[u].w, w[u].z, s);
+        uint4 c = enc_quad(tab, x, y, z);
+        if (r != 0 && pp[u] + 16 >= E) c = enc_seam2(tab, x, y, z, c, pp[u], E, r, a);
+        store16<true>(out + 16 * (s0 + u * kThreads + threadIdx.x), c);
+    }
+}
+
 // Ragged batch: one block per buffer.
 __global__ __launch_bounds__(kThreads) void k_encode_ragged(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
@@ -763,6 +867,22 @@ DEV void map_fast(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t G[4], uint
         acc |= t0 | t1 | t2 | t3;
     }
     bad = acc & ~63u;
+}
+
+// map_fast keeping the OR of each dword's four table values (A[g] < 64:
+// dword g is all alphabet), for callers that judge dwords separately.
+DEV void map_fast_acc(const uint8_t *tab, uint4 w, uint32_t G[4], uint32_t A[4])
+{
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        uint32_t t0 = tab[dw[g] & 0xFFu];
+        uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
+        uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
+        uint32_t t3 = tab[dw[g] >> 24];
+        G[g] = (t0 << 18) | (t1 << 12) | (t2 << 6) | t3;
+        A[g] = t0 | t1 | t2 | t3;
+    }
 }
 
 // Slow-path view of a lane's 16 characters: groups with every absent or
@@ -1713,6 +1833,164 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(
     }
 }
 
+// The last slot of a row (its nlast = 1..16 characters in range) under
+// the prefix rule of a padded or unaligned end: on return G holds the
+// groups with out-of-prefix characters zeroed, k the prefix length, and
+// the result says whether the shape applies.  Common shape first: every
+// dword before d (the dword holding the last in-range character, uniform)
+// all alphabet (A[g] < 64) and d's in-range characters an alphabet prefix
+// -- 4 lookups; anything else takes the general per-character rule.
+DEV bool row_last_slot(const uint8_t *tab, uint4 w, const uint32_t A[4], uint32_t G[4],
+                       uint32_t nlast, uint32_t &k)
+{
+    const uint32_t d = (nlast - 1) >> 2;
+    bool pre = true;
+#pragma unroll
+    for (uint32_t g = 0; g < 3; g++)
+        if (g < d) pre = pre && A[g] < 64u;
+    const uint32_t wd = d == 0 ? w.x : d == 1 ? w.y : d == 2 ? w.z : w.w;
+    uint32_t v = 0, Gd = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t t = tab[(wd >> (8 * j)) & 0xFFu];
+        const bool okj = 4 * d + j < nlast && t < 64u;
+        v |= (okj ? 1u : 0u) << j;
+        Gd |= (okj ? t : 0u) << (18 - 6 * j);
+    }
+    if (pre && (v & (v + 1)) == 0) {
+        k = 4 * d + __popc(v);
+#pragma unroll
+        for (uint32_t g = 0; g < 4; g++)
+            if (g == d) G[g] = Gd;
+        return true;
+    }
+    LaneChunk lc;
+    map_chunk_lds(tab, w, nlast, lc);
+    const uint32_t m = lc.vmask;
+    k = __popc(m);
+#pragma unroll
+    for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+    return (m & (m + 1)) == 0;  // alphabet characters form a prefix
+}
+
+// Uniform-stride batch decode, second form (rows with room, out_stride >=
+// 12*S, every row): the block's first slot gives its row b0 and slot q0
+// once, each lane's slot is a 32-bit offset from there split with a 32-bit
+// multiply-high (magic = ceil(2^32/S), exact in range -- the launcher
+// checks).  Blocks clear of the last row store every slot unconditionally
+// (the last slot of a row over-writes past out_len inside its own row);
+// blocks that touch the last row ("tail", block-uniform) read page-safely
+// and store only decoded bytes, so one launch covers the batch.  Lengths
+// and marks go through atomicMax on the zeroed outlen[] as in
+// k_decode_slots.  LAST = 1: the rows' last slots take row_last_slot's
+// cheap check inline for every lane (no branch), 0: in a branch.
+template <int U, int PRICE, int LAST>
+__global__ __launch_bounds__(kThreads) void k_decode_rows2(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
+    uint8_t *__restrict__ out, uint64_t out_stride,
+    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t magic, uint64_t m64,
+    uint64_t nslots, uint64_t tail_slot, DecAlpha a)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
+    const uint64_t b0 = __umul64hi(s0, m64);
+    const uint32_t q0 = (uint32_t) (s0 - b0 * S);
+    const uint8_t *ib = in + b0 * in_stride;
+    uint8_t *ob = out + b0 * out_stride;
+    unsigned long long *olb = outlen + b0;
+    const uint32_t nlast = len - 16 * (S - 1);  // characters in a row's last slot
+    const uint32_t d = (nlast - 1) >> 2;        // dword of the last in-range one
+    uint32_t bl[U], qq[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t rel = q0 + u * kThreads + threadIdx.x;
+        bl[u] = __umulhi(rel, magic);
+        qq[u] = rel - bl[u] * S;
+    }
+    if (s0 + U * kThreads > tail_slot) {
+        // tail block: page-safe loads, decoded bytes only
+        for (int u = 0; u < U; u++) {
+            const uint64_t t = s0 + u * kThreads + threadIdx.x;
+            const uint32_t q = qq[u];
+            if (t >= nslots) continue;
+            const bool last = q == S - 1;
+            const uint4 wv = load_chars(ib + (uint64_t) bl[u] * in_stride + 16 * q,
+                                        last ? nlast : 16u);
+            uint32_t G[4], A[4], k = 16;
+            map_fast_acc(tab, wv, G, A);
+            bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
+            if (last) ok = row_last_slot(tab, wv, A, G, nlast, k);
+            unsigned long long *ol = olb + bl[u];
+            if (!ok) {
+                atomicMax(ol, (unsigned long long) kNeedsExact);
+                continue;
+            }
+            uint32_t o0, o1, o2;
+            groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+            store_bytes12(ob + (uint64_t) bl[u] * out_stride + 12 * q, o0, o1, o2,
+                          3 * (k >> 2) + ((6 * (k & 3)) >> 3));
+            if (last) atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
+        }
+        return;
+    }
+    uint4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) w[u] = ld16<true>(ib + (uint64_t) bl[u] * in_stride + 16 * qq[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t q = qq[u];
+        const bool last = q == S - 1;
+        uint32_t G[4], A[4];
+        map_fast_acc(tab, w[u], G, A);
+        uint32_t k = 16;
+        bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
+        if (PRICE & 2) {
+            ok = true;
+        } else if (LAST) {
+            // the common last-slot shape for every lane, selected by `last`
+            bool pre = true;
+#pragma unroll
+            for (uint32_t g = 0; g < 3; g++)
+                if (g < d) pre = pre && A[g] < 64u;
+            const uint32_t wd = d == 0 ? w[u].x : d == 1 ? w[u].y : d == 2 ? w[u].z : w[u].w;
+            uint32_t v = 0, Gd = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t t = tab[(wd >> (8 * j)) & 0xFFu];
+                const bool okj = 4 * d + j < nlast && t < 64u;
+                v |= (okj ? 1u : 0u) << j;
+                Gd |= (okj ? t : 0u) << (18 - 6 * j);
+            }
+            const bool fast_last = pre && (v & (v + 1)) == 0;
+            if (last) {
+                ok = fast_last;
+                k = 4 * d + __popc(v);
+            }
+#pragma unroll
+            for (uint32_t g = 0; g < 4; g++)
+                if (g == d && last) G[g] = Gd;
+            if (last && !fast_last) ok = row_last_slot(tab, w[u], A, G, nlast, k);
+        } else if (last) {
+            ok = row_last_slot(tab, w[u], A, G, nlast, k);
+        }
+        uint32_t o0, o1, o2;
+        groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+        __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
+                                    (u32x3a4 *) (ob + (uint64_t) bl[u] * out_stride + 12 * q));
+        unsigned long long *ol = olb + bl[u];
+        if (PRICE & 1) {  // benchmark-only pricing of the atomics (racy)
+            if (!ok) *ol = kNeedsExact;
+            else if (last) *ol = (16ull * q + k) * 6 / 8;
+        } else if (!ok) {
+            atomicMax(ol, (unsigned long long) kNeedsExact);
+        } else if (last) {
+            atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
+        }
+    }
+}
+
 // Grouped twin of k_decode_slots (see k_encode_group): block g owns
 // buffers [g*bpb, (g+1)*bpb), lanes walk its bpb*S 16-character slots.
 template <int U, bool NTL>
@@ -2115,6 +2393,33 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     const EncAlpha ea = enc_alpha(abc);
     const uint64_t E = b64x_encoded_len(len, ea.pad);
     const uint32_t r = (uint32_t) (len % 3);
+    // Tight layout, one launch (k_encode_tight2).
+    const bool tight = in_stride == len && out_stride == E && len >= 16 && (ea.pad || r == 0) &&
+                       (((uintptr_t) d_in) & 3) == 0 && (((uintptr_t) d_out) & 15) == 0;
+    if (g_tune[4] == 0 && g_tune[6] == 0 && tight && E < (1u << 20)) {
+        const uint32_t Uw = g_tune[7] == 4 ? 4 : 2;
+        const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + E) / E);
+        const uint64_t e = (uint64_t) magic * E - (1ull << 32);
+        if ((E + 16ull * Uw * kThreads) * e < (1ull << 32)) {
+            const uint64_t total_out = (uint64_t) nbuf * E;
+            const uint64_t nslots = (total_out + 15) / 16;
+            const uint64_t tail_slot = (nbuf - 1) * E / 16 ? (nbuf - 1) * E / 16 - 1 : 0;
+            const uint64_t m64 = ~0ull / E + 1;
+            const uint64_t per = (uint64_t) Uw * kThreads;
+            const dim3 g((uint32_t) ((nslots + per - 1) / per));
+            if (Uw == 4)
+                hipLaunchKernelGGL(k_encode_tight2<4>, g, dim3(kThreads), 0, (hipStream_t) stream,
+                                   (const uint8_t *) d_in, len, (uint32_t) E, r, magic, m64,
+                                   (uint8_t *) d_out, nslots, (uint64_t) nbuf * len, total_out,
+                                   tail_slot, ea);
+            else
+                hipLaunchKernelGGL(k_encode_tight2<2>, g, dim3(kThreads), 0, (hipStream_t) stream,
+                                   (const uint8_t *) d_in, len, (uint32_t) E, r, magic, m64,
+                                   (uint8_t *) d_out, nslots, (uint64_t) nbuf * len, total_out,
+                                   tail_slot, ea);
+            return launch_status();
+        }
+    }
     // Tight layout: one contiguous character stream (k_encode_tight).
     if (g_tune[4] == 0 && in_stride == len && out_stride == E && nbuf >= 3 && len >= 16 &&
         (ea.pad || r == 0) && E < (1ull << 32) && (((uintptr_t) d_in) & 3) == 0 &&
@@ -2287,10 +2592,35 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (err) return err;
     const uint32_t bpb = S >= 2 && g_tune[3] != 1 ? plan_group(S, in_stride, out_stride) : 0;
     const bool ntl = batch_ntl();
+    const bool rows = nbuf >= 2 && S >= 2 && out_stride >= 12 * S && (in_stride & 3) == 0 &&
+                      (out_stride & 3) == 0 && (((uintptr_t) d_in) & 3) == 0 &&
+                      (((uintptr_t) d_out) & 3) == 0;
+    bool done = false;
+    if (g_tune[4] == 0 && g_tune[6] == 0 && rows && S < (1u << 20)) {
+        const uint32_t Uw = g_tune[7] == 2 ? 2 : 4;
+        const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
+        const uint64_t e = (uint64_t) magic * S - (1ull << 32);
+        const uint64_t relmax = S + (uint64_t) Uw * kThreads;
+        if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40)) {
+            const uint64_t m64 = ~0ull / S + 1;
+            const uint64_t per = (uint64_t) Uw * kThreads;
+            const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
+            const dim3 g((uint32_t) ((slots + per - 1) / per));
+            auto k = Uw == 4 ? k_decode_rows2<4, 0, 0> : k_decode_rows2<2, 0, 0>;
+            if (g_tune[3] == 11) k = Uw == 4 ? k_decode_rows2<4, 0, 1> : k_decode_rows2<2, 0, 1>;
+            if (Uw == 4 && g_tune[3] == 8) k = k_decode_rows2<4, 1, 0>;  // pricing only (racy)
+            if (Uw == 4 && g_tune[3] == 9) k = k_decode_rows2<4, 2, 0>;  // pricing (wrong lengths)
+            hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s, (const uint8_t *) d_in, in_stride,
+                               (uint32_t) len, (uint8_t *) d_out, out_stride,
+                               (unsigned long long *) d_outlen, (uint32_t) S, magic, m64, slots,
+                               tail_slot, a);
+            if ((err = launch_status())) return err;
+            done = true;
+        }
+    }
     // Rows with room: the uniform kernel over all rows but the last.
-    if (g_tune[4] == 0 && nbuf >= 2 && S >= 2 && out_stride >= 12 * S && (in_stride & 3) == 0 &&
-        (out_stride & 3) == 0 && (((uintptr_t) d_in) & 3) == 0 &&
-        (((uintptr_t) d_out) & 3) == 0) {
+    if (done) {
+    } else if (g_tune[4] == 0 && rows) {
         constexpr int U = 2;
         const uint64_t m64 = ~0ull / S + 1;  // ceil(2^64 / S)
         const uint64_t nrows = (uint64_t) S * (nbuf - 1);
@@ -2690,7 +3020,7 @@ int b64x_lane_wait(b64x_lane *l)
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)
 {
-    if (idx < 0 || idx >= 6) return -EINVAL;
+    if (idx < 0 || idx >= 8) return -EINVAL;
     int old = g_tune[idx];
     g_tune[idx] = value;
     return old;

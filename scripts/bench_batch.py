@@ -20,9 +20,14 @@ KNOBS = [tuple(int(x) for x in kv.split(":")) for kv in
          os.environ.get("KNOBS", "3:0,3:1").split(",")]
 s = torch.cuda.current_stream()
 res = {}
-for name, nbuf, L in (("cfg4", 1 << 20, 1024), ("cfg3", 1 << 16, 4096)):
+CAPS = [int(c) for c in os.environ.get("CAPS", "0").split(",")]
+CFGS = os.environ.get("CFGS", "cfg4,cfg3").split(",")
+for name, nbuf, L, capr in [(n, nb, L, c) for n, nb, L in (("cfg4", 1 << 20, 1024),
+                                                              ("cfg3", 1 << 16, 4096))
+                            if n in CFGS for c in CAPS]:
     Es = b64.encoded_len(L)
-    cap = (b64.decoded_cap(Es) + 15) // 16 * 16
+    # decode row stride: capacity rounded up to `capr` bytes (0: 12 per slot)
+    cap = (b64.decoded_cap(Es) + capr - 1) // capr * capr if capr else 12 * ((Es + 15) // 16)
     x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
     b64.fill_splitmix64(x, 0x5EED)
     enc = torch.empty(nbuf * Es, dtype=torch.uint8, device="cuda")
@@ -47,7 +52,7 @@ for name, nbuf, L in (("cfg4", 1 << 20, 1024), ("cfg3", 1 << 16, 4096)):
         ok = bool((outlen == L).all()) and torch.equal(dec.view(nbuf, cap)[:, :L], x.view(nbuf, L))
         lib.b64x__tune(idx, old)
         per = nbuf * (L + Es)
-        res[f"{name} knob{idx}={val}"] = {
+        res[f"{name} cap{capr} knob{idx}={val}"] = {
             "ok": ok, "enc_ms": statistics.median(ts["enc"]), "dec_ms": statistics.median(ts["dec"]),
             "enc_GBps": per / statistics.median(ts["enc"]) / 1e6,
             "dec_GBps": per / statistics.median(ts["dec"]) / 1e6}

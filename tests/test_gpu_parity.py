@@ -287,6 +287,44 @@ def test_strided_odd_strides_and_junk(length, gap_in, gap_out, cap_extra):
         assert dh[i * cap:i * cap + len(want)].tobytes() == want, i
 
 
+@pytest.mark.parametrize("E", [20, 24, 28, 31, 32, 33, 40, 1368, 1372])
+def test_strided_rows_last_slot_shapes(E):
+    """Dense rows (out_stride = 12 per 16-character slot, the row kernel):
+    every row's last slot gets a different shape -- clean, padded, '='
+    inside the prefix, junk after the padding, junk at each position, a
+    lone alphabet character after junk -- each row vs the oracle."""
+    rng = np.random.default_rng(E)
+    nbuf = 1500
+    S = (E + 15) // 16
+    alpha = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/",
+                          dtype=np.uint8)
+    rows = rng.choice(alpha, (nbuf, E))
+    lo = 16 * (S - 1)
+    for i in range(nbuf):
+        kind = i % 6
+        if kind == 1:  # standard padding
+            rows[i, E - 1 - (i // 6) % 2:] = ord("=")
+        elif kind == 2:  # one junk byte anywhere in the last slot
+            rows[i, lo + int(rng.integers(0, E - lo))] = (10, 13, 61, 32, 0xE9)[i % 5]
+        elif kind == 3:  # a junk run to the end of the row
+            rows[i, lo + int(rng.integers(0, E - lo)):] = ord("=")
+        elif kind == 4:  # junk then one alphabet character at the very end
+            if E - lo >= 2:
+                rows[i, E - 2] = ord("\n")
+        elif kind == 5:  # junk in an interior slot as well
+            rows[i, int(rng.integers(0, E))] = ord(" ")
+    flat = rows.reshape(-1)
+    cap = 12 * S
+    dec = torch.zeros(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(dev(flat), E, E, nbuf, dec, cap, outlen)
+    dh, ol = dec.cpu().numpy(), outlen.cpu().numpy()
+    for i in range(nbuf):
+        want = orc.decode(rows[i].tobytes())
+        assert int(ol[i]) == len(want), (i, i % 6)
+        assert dh[i * cap:i * cap + len(want)].tobytes() == want, (i, i % 6)
+
+
 @pytest.mark.slow
 def test_strided_cfg3_full():
     """65,536 x 4 KiB (BASELINE config 3)."""
