@@ -374,8 +374,9 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
 // bit 1 cached loads, any bit: not the tight/row kernels), 5 = 1: the
 // chunk-by-chunk pass 2, 6 = 1: the first-form tight/row batch kernels,
-// 7 = lanes' slots per batch-kernel tile (2 or 4).
-int g_tune[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+// 7 = lanes' slots per batch-kernel tile (2 or 4), 8 = 1: the one-block
+// decode scan.
+int g_tune[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
@@ -1149,14 +1150,20 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
 //           hit one; 0 = none.  The scan moves it to fd_cur and zeroes it.
 //   counts  alphabet characters per range (pass 1, every range)
 //   bases   exclusive prefix of counts (scan, dirty calls only)
+//   status  per scan tile: flag (bits 63..62: 1 aggregate, 2 inclusive
+//           prefix; 0 = not yet) | value, for the scan's decoupled
+//           look-back; zero between calls (the scan's last tile clears it)
 struct DecodeWs {
     uint64_t *fd;
     uint64_t *fd_cur;
     uint32_t *counts;
     uint64_t *bases;
+    uint64_t *status;
 };
 
-// Layout for `nranges` ranges: 64-byte header, counts, bases.
+constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
+
+// Layout for `nranges` ranges: 64-byte header, counts, bases, tile status.
 DEV DecodeWs ws_view(void *ws, uint32_t nranges)
 {
     DecodeWs w;
@@ -1165,6 +1172,7 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.fd_cur = (uint64_t *) (p + 8);
     w.counts = (uint32_t *) (p + 64);
     w.bases = (uint64_t *) (p + 64 + ((uint64_t) nranges * 4 + 7) / 8 * 8);
+    w.status = w.bases + nranges;
     return w;
 }
 
@@ -1362,6 +1370,186 @@ __global__ __launch_bounds__(1024) void k_decode_scan(
         }
         if (lane == 0)
             for (int j = 0; j < 4; j++) res->tail[j] = got[j];
+    }
+}
+
+// The stream's last V mod 4 alphabet characters (as sextets) into
+// res->tail, scanning backwards from the end; one wave.
+DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, uint64_t V,
+                           b64x_dec_result *res)
+{
+    const uint32_t lane = lane_id();
+    int need = (int) (V & 3);
+    uint8_t got[4] = {0, 0, 0, 0};
+    uint64_t end = n;
+    while (need > 0 && end > 0) {
+        uint64_t beg = end >= 64 ? end - 64 : 0;
+        uint64_t p = beg + lane;
+        uint32_t t = p < end ? tab[in[p]] : 0xFFu;
+        uint64_t bm = __ballot(t < 64u);
+        while (need > 0 && bm) {
+            int hi = 63 - __clzll(bm);
+            got[--need] = (uint8_t) __shfl(t, hi, 64);
+            bm &= ~(1ull << hi);
+        }
+        end = beg;
+    }
+    if (lane == 0)
+        for (int j = 0; j < 4; j++) res->tail[j] = got[j];
+}
+
+DEV void write_result(b64x_dec_result *res, uint64_t V, uint32_t hold)
+{
+    res->valid = V;
+    res->tail_n = (uint32_t) (V & 3);
+    res->out_len = hold ? V / 4 * 3 : V * 6 / 8;
+}
+
+// Block-wide exclusive scan of one u64 per thread (256 threads); returns
+// the exclusive prefix, `total` the block sum.
+DEV uint64_t block_excl_scan256(uint64_t x, uint64_t *wtot, uint64_t &total)
+{
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    uint64_t v = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t) d) v += y;
+    }
+    if (lane == 63) wtot[wave] = v;
+    __syncthreads();
+    uint64_t before = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kWavesPerBlock; i++) {
+        if (i < wave) before += wtot[i];
+        total += wtot[i];
+    }
+    return before + v - x;
+}
+
+constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62;
+constexpr uint64_t kStVal = (1ull << 62) - 1;
+
+// Tile status words are written and read with relaxed device-scope atomics
+// (one 64-bit word carries flag and value, so no fence orders a value
+// against its flag: a release here would write back the whole L2).
+DEV void st_store(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+DEV uint64_t st_load(uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Scan, device-wide (replaces the one-block k_decode_scan), one block per
+// tile of 1024 ranges.  Clean call (no first-dirty record): block 0 alone
+// computes V from the last range's count and the result record; every
+// other block returns at once.  Dirty call: a single-pass scan of
+// counts[r0 ..] with decoupled look-back and no atomic read-modify-write --
+// tile t is block t (workgroups are dispatched in order and the grid, at
+// most 1024 blocks, fits on the chip at once, so a tile's predecessors are
+// resident or done); each tile publishes its aggregate, looks back over its
+// predecessors 64 at a time (one wave) until an inclusive prefix,
+// publishes its own and writes the bases of its ranges.  The last tile
+// writes the result record and the tail sextets, waits until every tile
+// has published its inclusive prefix (so no look-back is still reading),
+// clears the status words and re-arms the workspace (fd -> fd_cur).
+template <int PRICE>
+__global__ __launch_bounds__(kThreads) void k_decode_scan2(
+    const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
+    DecAlpha a, void *ws, b64x_dec_result *res, uint32_t hold)
+{
+    __shared__ uint8_t tab[256];
+    __shared__ uint64_t wtot[kWavesPerBlock];
+    __shared__ uint64_t s_excl;
+    DecodeWs w = ws_view(ws, nranges);
+    const uint64_t packed = *(volatile uint64_t *) w.fd;
+    if (packed == 0) {
+        if (blockIdx.x != 0) return;
+        build_dec_table(tab, a);
+        __syncthreads();
+        const uint64_t V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
+        if (threadIdx.x == 0) {
+            *w.fd_cur = 0;
+            write_result(res, V, hold);
+        }
+        if (threadIdx.x < 64) find_tail_sextets(tab, in, n, V, res);
+        return;
+    }
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t ntiles = (nranges - r0 + kScanTile - 1) / kScanTile;
+    const uint32_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    build_dec_table(tab, a);
+    const uint32_t base = r0 + t * kScanTile + 4 * threadIdx.x;
+    uint32_t c[4];
+    uint64_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        c[j] = base + j < nranges ? w.counts[base + j] : 0u;
+        mine += c[j];
+    }
+    uint64_t agg;
+    const uint64_t ex = block_excl_scan256(mine, wtot, agg);
+    const uint32_t lane = lane_id();
+    if (threadIdx.x < 64) {
+        uint64_t excl = (uint64_t) r0 * R;
+        if (t > 0 && PRICE == 0) {
+            if (lane == 0) st_store(&w.status[t], kStAgg | agg);
+            excl = 0;
+            int64_t p = (int64_t) t - 1;
+            for (;;) {
+                const int64_t q = p - lane;
+                const uint64_t v = q >= 0 ? st_load(&w.status[q]) : kStIncl;  // before tile 0: 0
+                const uint32_t f = (uint32_t) (v >> 62);
+                const uint64_t inc = __ballot(f == 2);
+                const uint32_t k = inc ? (uint32_t) __ffsll((unsigned long long) inc) - 1 : 63u;
+                if (!__all(lane > k || f != 0)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t part = lane <= k ? (v & kStVal) : 0;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
+                excl += part;
+                if (inc) break;
+                p -= 64;
+            }
+        }
+        if (lane == 0) {
+            st_store(&w.status[t], kStIncl | (excl + agg));
+            s_excl = excl;
+        }
+    }
+    __syncthreads();
+    uint64_t run = s_excl + ex;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (base + j < nranges) w.bases[base + j] = run;
+        run += c[j];
+    }
+    if (t == ntiles - 1 && threadIdx.x < 64) {
+        const uint64_t V = s_excl + agg;
+        if (lane == 0) write_result(res, V, hold);
+        find_tail_sextets(tab, in, n, V, res);
+        if (PRICE == 0) {
+            // every tile inclusive -> every look-back is over
+            for (;;) {
+                bool all = true;
+                for (uint32_t i = lane; i < ntiles; i += 64)
+                    all = all && (st_load(&w.status[i]) >> 62) == 2;
+                if (__all(all)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.status[i], 0);
+        if (lane == 0) {
+            *w.fd_cur = packed;
+            *w.fd = 0;
+        }
     }
 }
 
@@ -2320,7 +2508,7 @@ uint64_t b64x_decode_workspace_size(uint64_t nchars)
     // nchars (ranges are at least one chunk; 0 = the largest input)
     uint64_t nr = nchars ? (nchars + kChunk - 1) / kChunk : kMaxRanges;
     if (nr > kMaxRanges) nr = kMaxRanges;
-    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8;
+    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8 + (nr + kScanTile - 1) / kScanTile * 8;
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
@@ -2531,8 +2719,14 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
               p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
-    hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
-                       nchars, p.R, p.nranges, a, ws, d_res, hold);
+    if (g_tune[8] == 1)  // the first-form one-block scan (A/B only)
+        hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
+                           nchars, p.R, p.nranges, a, ws, d_res, hold);
+    else
+        hipLaunchKernelGGL(g_tune[8] == 2 ? k_decode_scan2<1> : k_decode_scan2<0>,
+                           dim3((p.nranges + kScanTile - 1) / kScanTile),
+                           dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges,
+                           a, ws, d_res, hold);
     if ((err = launch_status())) return err;
     if (p.R <= kP2Range && g_tune[5] == 0) {
         const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 8);
@@ -3020,7 +3214,7 @@ int b64x_lane_wait(b64x_lane *l)
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)
 {
-    if (idx < 0 || idx >= 8) return -EINVAL;
+    if (idx < 0 || idx >= 9) return -EINVAL;
     int old = g_tune[idx];
     g_tune[idx] = value;
     return old;
