@@ -1195,6 +1195,47 @@ DEV uint4 ld16(const uint8_t *p)
 
 constexpr uint32_t kNoDirty = 0xFFFFFFFFu;
 
+// Alphabet characters among a lane's first `nin` characters.
+DEV uint32_t count_valid(const uint8_t *tab, uint4 w, uint32_t nin)
+{
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 4; g++)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            c += (tab[(dw[g] >> (8 * j)) & 0xFFu] < 64u && 4 * g + j < nin) ? 1u : 0u;
+    return c;
+}
+
+// Pass 1's step for one chunk at stream position `pos` of range [rb, re):
+// while the range is still clean, the fast paths (an all-alphabet chunk;
+// the stream's final chunk in the prefix shape); the first chunk that fits
+// neither becomes the range's dirty offset; from then on the range only
+// counts.
+DEV void p1_chunk(const uint8_t *tab, uint4 w, uint32_t nin, uint64_t pos, uint64_t rb,
+                  uint64_t re, bool last, uint32_t hold, uint8_t *o, uint32_t &dirty,
+                  uint32_t &cnt)
+{
+    if (dirty != kNoDirty) {
+        cnt += count_valid(tab, w, nin);
+        return;
+    }
+    uint32_t G[4], bad;
+    map_fast(tab, w, nin, G, bad);
+    if (__all(bad == 0)) {
+        cnt += 16;
+        emit_full(G, o + (pos - rb) / 4 * 3);
+        return;
+    }
+    LaneChunk lc;
+    map_chunk_lds(tab, w, nin, lc);
+    cnt += __popc(lc.vmask);
+    const bool final = last && pos + kChunk >= re;
+    if (!final || fast_prefix(lc, hold != 0, o + (pos - rb) / 4 * 3) < 0)
+        dirty = (uint32_t) (pos - rb);
+}
+
 // Pass 1 (fast paths only), one wave per range; each range assumes every
 // earlier range was all alphabet.  The hot loop takes groups of U full
 // chunks while every chunk is all alphabet (no per-lane guards, scalar loop
@@ -1204,7 +1245,8 @@ constexpr uint32_t kNoDirty = 0xFFFFFFFFu;
 // that chunk is published (atomicMax of the complemented (range, offset))
 // and the range only counts from then on.
 template <int U, bool PIPE, bool NT>
-__global__ __launch_bounds__(kThreads) void k_decode_pass1(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7)))
+void k_decode_pass1(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
 {
@@ -1220,6 +1262,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
     const bool last = r + 1 == nranges;
     uint8_t *o = out + rb / 4 * 3;
     uint32_t cnt = 0;  // per lane; summed over the wave at the end
+    uint32_t dirty = kNoDirty;
     uint64_t pos = rb;
     const uint64_t hot_end = re - (re - rb) % ((uint64_t) kChunk * U);
     if (((((uintptr_t) in) | ((uintptr_t) o)) & 3) == 0 && pos < hot_end) {
@@ -1246,6 +1289,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
             }
             cnt += 16 * u;
             if (u < U) {
+                // the rest of the range in the loop below (re-loading keeps
+                // this loop's registers -- and its occupancy -- at the
+                // fast path's)
                 pos += (uint64_t) u * kChunk;
                 break;
             }
@@ -1256,28 +1302,21 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass1(
                 cur[v] = PIPE ? nxt[v] : ld16<NT>(in + pos + (uint64_t) v * kChunk + 16 * lane);
         }
     }
-    uint32_t dirty = kNoDirty;
-    for (; pos < re; pos += kChunk) {
-        const uint64_t p = pos + 16 * lane;
-        const uint32_t nin = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-        const uint4 w = nin ? load_chars(in + p, nin) : make_uint4(0, 0, 0, 0);
-        if (dirty == kNoDirty) {
-            uint32_t G[4], bad;
-            map_fast(tab, w, nin, G, bad);
-            if (__all(bad == 0)) {
-                cnt += 16;
-                emit_full(G, o + (pos - rb) / 4 * 3);
-                continue;
-            }
+    for (; pos < re; pos += 2 * (uint64_t) kChunk) {
+        // two chunks' loads in flight, then each chunk in order
+        uint4 w[2];
+        uint32_t nin[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t p = pos + (uint64_t) h * kChunk + 16 * lane;
+            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+            w[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
         }
-        LaneChunk lc;
-        map_chunk_lds(tab, w, nin, lc);
-        cnt += __popc(lc.vmask);
-        if (dirty == kNoDirty) {
-            const bool final = last && pos + kChunk >= re;
-            if (!final || fast_prefix(lc, hold != 0, o + (pos - rb) / 4 * 3) < 0)
-                dirty = (uint32_t) (pos - rb);
-        }
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            if (pos + (uint64_t) h * kChunk < re)
+                p1_chunk(tab, w[h], nin[h], pos + (uint64_t) h * kChunk, rb, re, last, hold, o,
+                         dirty, cnt);
     }
     cnt = wave_sum(cnt);
     if (lane == 0) {
