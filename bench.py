@@ -284,8 +284,8 @@ def main():
             "data": "synthetic: splitmix64(0x5EED) bytes generated in HBM; round trip "
                     "verified bit-exact before timing",
             "config": {
-                "workload": "cfg2: one 1 GiB buffer per GPU, encode (std alphabet, pad) "
-                            "then decode, device-resident",
+                "workload": f"cfg2: one {N / 2**30:g} GiB buffer per GPU, encode (std "
+                            "alphabet, pad) then decode, device-resident",
                 "bytes_per_gpu": N,
                 "chars_per_gpu": E,
                 "parallelism": f"independent buffers x{world} (no data-path collective)",
@@ -305,7 +305,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(knames),
+                # the committed PMC summary is for the 1 GiB workload
+                "traffic": load_traffic(knames) if N == 1 << 30 else None,
             },
             "cpu_baseline": cpu,
             "batch_cfg4": batch,
