@@ -1195,17 +1195,22 @@ DEV uint4 ld16(const uint8_t *p)
 
 constexpr uint32_t kNoDirty = 0xFFFFFFFFu;
 
-// Alphabet characters among a lane's first `nin` characters.
+// Alphabet characters among a lane's first `nin` characters: the table
+// values packed 4 per dword, non-alphabet ones have bit 7 set.
 DEV uint32_t count_valid(const uint8_t *tab, uint4 w, uint32_t nin)
 {
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
-    uint32_t c = 0;
+    uint32_t bad = 0;
 #pragma unroll
-    for (uint32_t g = 0; g < 4; g++)
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++)
-            c += (tab[(dw[g] >> (8 * j)) & 0xFFu] < 64u && 4 * g + j < nin) ? 1u : 0u;
-    return c;
+    for (uint32_t g = 0; g < 4; g++) {
+        uint32_t P = tab[dw[g] & 0xFFu] | ((uint32_t) tab[(dw[g] >> 8) & 0xFFu] << 8) |
+                     ((uint32_t) tab[(dw[g] >> 16) & 0xFFu] << 16) |
+                     ((uint32_t) tab[dw[g] >> 24] << 24);
+        const uint32_t in_g = nin > 4 * g ? nin - 4 * g : 0u;
+        P |= in_g >= 4 ? 0u : ~0u << (8 * in_g);
+        bad += __popc(P & 0x80808080u);
+    }
+    return 16u - bad;
 }
 
 // Pass 1's step for one chunk at stream position `pos` of range [rb, re):
@@ -1228,12 +1233,16 @@ DEV void p1_chunk(const uint8_t *tab, uint4 w, uint32_t nin, uint64_t pos, uint6
         emit_full(G, o + (pos - rb) / 4 * 3);
         return;
     }
+    const bool final = last && pos + kChunk >= re;
+    if (!final) {
+        cnt += count_valid(tab, w, nin);
+        dirty = (uint32_t) (pos - rb);
+        return;
+    }
     LaneChunk lc;
     map_chunk_lds(tab, w, nin, lc);
     cnt += __popc(lc.vmask);
-    const bool final = last && pos + kChunk >= re;
-    if (!final || fast_prefix(lc, hold != 0, o + (pos - rb) / 4 * 3) < 0)
-        dirty = (uint32_t) (pos - rb);
+    if (fast_prefix(lc, hold != 0, o + (pos - rb) / 4 * 3) < 0) dirty = (uint32_t) (pos - rb);
 }
 
 // Pass 1 (fast paths only), one wave per range; each range assumes every
@@ -1289,10 +1298,18 @@ void k_decode_pass1(
             }
             cnt += 16 * u;
             if (u < U) {
-                // the rest of the range in the loop below (re-loading keeps
-                // this loop's registers -- and its occupancy -- at the
-                // fast path's)
-                pos += (uint64_t) u * kChunk;
+                const uint64_t cpos = pos + (uint64_t) u * kChunk;
+                if (!(last && cpos + kChunk >= re)) {
+                    // chunk u is the range's first dirty one: count it and
+                    // the rest of the tile from the registers they are in
+                    dirty = (uint32_t) (cpos - rb);
+#pragma unroll
+                    for (int v = 0; v < U; v++)
+                        if (v >= u) cnt += count_valid(tab, cur[v], 16);
+                    pos = np;
+                } else {
+                    pos = cpos;  // the stream's final chunk: prefix rule below
+                }
                 break;
             }
             pos = np;
@@ -1793,6 +1810,168 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2b(
             wave_lds_order();
             store_realigned(bb, 3 * ng, ob);
             if (rem && at_end && !hold) emit_partial(sx + 4 * ng, ob + 3 * ng, (int) rem);
+        }
+        wave_lds_order();  // the next range reuses sx and bb
+    }
+}
+
+// ---- pass 2, one-shot per range, scatter form ----------------------------
+//
+// k_decode_pass2b spends ~700 VALU per 2 KiB range (PMC), most of it in
+// map_chunk (per character: a compare pair, two selects and two shift-ors
+// to build zeroed groups and a valid mask) and in a branchy per-character
+// scatter.  Here a lane's 16 table values are packed as bytes (the value
+// of an alphabet character *is* its sextet; 0xFF otherwise), its valid
+// count is 16 - popc(P & 0x80808080) per dword, and the scatter is
+// branch-free: every character is written, the non-alphabet ones to a
+// dummy byte.  The wave's sextet buffer starts 16 bytes in, so the 0-3
+// sextets skipped at a range start land in the head instead of needing a
+// bounds test.
+constexpr uint32_t kP2cHead = 16;
+
+constexpr uint32_t kP2cPhys = kP2cHead + kP2Sx + 16;  // bytes per wave
+
+// Identity (a 4-per-128-byte pad swizzle against the scatter's bank
+// conflicts measured slower: 997 vs 928 us on dirty 1 GiB).
+DEV uint32_t swz(uint32_t p) { return p; }
+
+struct __attribute__((aligned(16))) P2cSmem {
+    uint8_t tab[256];
+    uint8_t sx[kWavesPerBlock][kP2cPhys];
+    uint32_t bb[kWavesPerBlock][kP2Bb / 4];
+};
+
+// The 16 table values of a lane's characters, packed 4 per dword; the
+// characters at and past `nin` read as non-alphabet.
+DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
+{
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (uint32_t g = 0; g < 4; g++) {
+        const uint32_t t0 = tab[dw[g] & 0xFFu];
+        const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
+        const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
+        const uint32_t t3 = tab[dw[g] >> 24];
+        P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
+    }
+    if (nin < 16) {
+#pragma unroll
+        for (uint32_t g = 0; g < 4; g++) {
+            const uint32_t in_g = nin > 4 * g ? nin - 4 * g : 0u;
+            P[g] |= in_g >= 4 ? 0u : ~0u << (8 * in_g);
+        }
+    }
+}
+
+DEV uint32_t lane_valid_count(const uint32_t P[4])
+{
+    return 16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
+           __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_pass2c(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
+{
+    DecodeWs w = ws_view(ws, nranges);
+    const uint64_t packed = *w.fd_cur;
+    if (packed == 0) return;
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t off0 = (uint32_t) ~packed;
+    __shared__ P2cSmem sm;
+    build_dec_table(sm.tab, a);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *sxh = sm.sx[wv];  // logical byte p at sxh[swz(p)]; skipped sextets land
+                               // in the head, the range's first owned one at kP2cHead
+    const uint32_t dummy = swz(kP2cHead + kP2Sx + 8);  // target of non-alphabet bytes
+    uint32_t *bb = sm.bb[wv];
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges, first = r == r0;
+        const uint64_t start = first ? rb + off0 : rb;
+        const uint64_t B = w.bases[r];
+        uint4 c[2];
+        uint32_t nin[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+        }
+        const bool la_ok = !last && re + lane < n;
+        uint32_t la = la_ok ? in[re + lane] : 0u;
+        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
+        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            uint32_t P[4];
+            lane_values(sm.tab, c[h], nin[h], P);
+            uint32_t tot;
+            const uint32_t ex = wave_scan_small(lane_valid_count(P), tot);
+            uint32_t cur = (uint32_t) ((int) kP2cHead + T + (int) ex);
+#pragma unroll
+            for (uint32_t g = 0; g < 4; g++) {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
+                    const bool ok = b < 64u;
+                    sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
+                    cur += ok ? 1u : 0u;
+                }
+            }
+            T += (int) tot;
+        }
+        bool at_end = last;
+        if (!last && T > 0 && (T & 3)) {
+            // complete the range's last group from the characters after it
+            bool ok = la_ok;
+            for (uint64_t q = re;;) {
+                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+                const bool v = t < 64u;
+                const uint64_t m = __ballot(v);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                const int need = 4 - (T & 3);
+                if (v && (int) rank < need) sxh[swz(kP2cHead + T + rank)] = (uint8_t) t;
+                const int got = __popcll(m);
+                if (got >= need) {
+                    T += need;
+                    break;
+                }
+                T += got;
+                q += 64;
+                if (q >= n) {
+                    at_end = true;  // the stream's final, incomplete group
+                    break;
+                }
+                ok = q + lane < n;
+                la = ok ? in[q + lane] : 0u;
+            }
+        }
+        wave_lds_order();
+        if (T > 0) {
+            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
+            for (uint32_t L = lane; 4 * L < ng; L += 64) {
+                const uint32_t *q4 = (const uint32_t *) (sxh + swz(kP2cHead + 16 * L));
+                const uint4 sv = make_uint4(q4[0], q4[1], q4[2], q4[3]);
+                uint32_t o0, o1, o2;
+                groups_to_bytes(group_of_bytes(sv.x), group_of_bytes(sv.y),
+                                group_of_bytes(sv.z), group_of_bytes(sv.w), o0, o1, o2);
+                bb[3 * L] = o0;
+                bb[3 * L + 1] = o1;
+                bb[3 * L + 2] = o2;
+            }
+            wave_lds_order();
+            store_realigned(bb, 3 * ng, ob);
+            if (rem && at_end && !hold && lane == 0) {
+                uint8_t tl[3];
+                for (uint32_t j = 0; j < rem; j++) tl[j] = sxh[swz(kP2cHead + 4 * ng + j)];
+                emit_partial(tl, ob + 3 * ng, (int) rem);
+            }
         }
         wave_lds_order();  // the next range reuses sx and bb
     }
@@ -2767,9 +2946,10 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges,
                            a, ws, d_res, hold);
     if ((err = launch_status())) return err;
-    if (p.R <= kP2Range && g_tune[5] == 0) {
+    if (p.R <= kP2Range && g_tune[5] != 1) {
         const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 8);
-        hipLaunchKernelGGL(k_decode_pass2b, dim3(b2), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(g_tune[5] == 2 ? k_decode_pass2b : k_decode_pass2c, dim3(b2),
+                           dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
                            a, ws, hold);
         return launch_status();
