@@ -1837,6 +1837,7 @@ DEV uint32_t swz(uint32_t p) { return p; }
 
 struct __attribute__((aligned(16))) P2cSmem {
     uint8_t tab[256];
+    uint32_t sel[16];  // v_perm selector compacting a dword's alphabet bytes, by invalid mask
     uint8_t sx[kWavesPerBlock][kP2cPhys];
     uint32_t bb[kWavesPerBlock][kP2Bb / 4];
 };
@@ -1869,6 +1870,14 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
 }
 
+// SCAT = 1 (measured a little slower, kept for A/B): each dword's alphabet
+// bytes are compacted in the register with
+// one v_perm (selector from a 16-entry table by the dword's invalid mask,
+// computed with a multiply that gathers the four bit-7s) and written with
+// byte stores at immediate offsets from one per-dword address, each
+// predicated on its index < the dword's count; 0: one store per character,
+// the non-alphabet ones to a dummy byte.
+template <int SCAT>
 __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
@@ -1880,6 +1889,15 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
     const uint32_t off0 = (uint32_t) ~packed;
     __shared__ P2cSmem sm;
     build_dec_table(sm.tab, a);
+    if (threadIdx.x < 16) {
+        uint32_t sel = 0x0C0C0C0Cu, k = 0;
+        for (uint32_t j = 0; j < 4; j++)
+            if (!((threadIdx.x >> j) & 1u)) {
+                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
+                k++;
+            }
+        sm.sel[threadIdx.x] = sel;
+    }
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1888,22 +1906,13 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
     const uint32_t dummy = swz(kP2cHead + kP2Sx + 8);  // target of non-alphabet bytes
     uint32_t *bb = sm.bb[wv];
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
+    // One range: chunks c[] (nin[] characters of each lane in range), the
+    // lookahead byte la (valid if la_ok), its base B.
+    auto process = [&](uint32_t r, const uint4 *c, const uint32_t *nin, uint32_t la, bool la_ok,
+                       uint64_t B) {
         const uint64_t rb = (uint64_t) r * R;
         const uint64_t re = rb + R < n ? rb + R : n;
         const bool last = r + 1 == nranges, first = r == r0;
-        const uint64_t start = first ? rb + off0 : rb;
-        const uint64_t B = w.bases[r];
-        uint4 c[2];
-        uint32_t nin[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
-        }
-        const bool la_ok = !last && re + lane < n;
-        uint32_t la = la_ok ? in[re + lane] : 0u;
         int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
         uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
 #pragma unroll
@@ -1913,14 +1922,30 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
             uint32_t tot;
             const uint32_t ex = wave_scan_small(lane_valid_count(P), tot);
             uint32_t cur = (uint32_t) ((int) kP2cHead + T + (int) ex);
+            if (SCAT) {
 #pragma unroll
-            for (uint32_t g = 0; g < 4; g++) {
+                for (uint32_t g = 0; g < 4; g++) {
+                    const uint32_t inv = P[g] & 0x80808080u;
+                    const uint32_t m = ((inv >> 7) * 0x01020408u) >> 24;  // bit j: byte j bad
+                    const uint32_t c = 4u - __popc(inv);
+                    const uint32_t D = __builtin_amdgcn_perm(0u, P[g], sm.sel[m & 15u]);
+                    uint8_t *q = sxh + cur;
+                    if (c > 0) q[0] = (uint8_t) D;
+                    if (c > 1) q[1] = (uint8_t) (D >> 8);
+                    if (c > 2) q[2] = (uint8_t) (D >> 16);
+                    if (c > 3) q[3] = (uint8_t) (D >> 24);
+                    cur += c;
+                }
+            } else {
 #pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
-                    const bool ok = b < 64u;
-                    sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
-                    cur += ok ? 1u : 0u;
+                for (uint32_t g = 0; g < 4; g++) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
+                        const bool ok = b < 64u;
+                        sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
+                        cur += ok ? 1u : 0u;
+                    }
                 }
             }
             T += (int) tot;
@@ -1974,7 +1999,60 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
             }
         }
         wave_lds_order();  // the next range reuses sx and bb
+    };
+    auto load_generic = [&](uint32_t r) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges, first = r == r0;
+        const uint64_t start = first ? rb + off0 : rb;
+        uint4 c[2];
+        uint32_t nin[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+        }
+        const bool la_ok = !last && re + lane < n;
+        const uint32_t la = la_ok ? in[re + lane] : 0u;
+        process(r, c, nin, la, la_ok, w.bases[r]);
+    };
+    uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
+    if (r == r0 && r < nranges) {
+        load_generic(r);
+        r += nw;
     }
+    // Middle ranges (whole, neither first nor last): the next range's loads
+    // -- both chunks, the lookahead bytes (address clamped into the stream)
+    // and its base -- are issued before this range is processed.
+    const uint32_t mid_end = nranges - 1;
+    if (R == 2 * kChunk && r < mid_end && (((uintptr_t) in) & 3) == 0) {
+        const uint32_t full[2] = {16u, 16u};
+        auto ld_la = [&](uint32_t rr) {
+            const uint64_t q = (uint64_t) (rr + 1) * R + lane;
+            return (uint32_t) in[q < n ? q : n - 1];
+        };
+        uint4 c[2];
+        c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
+        c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
+        uint32_t la = ld_la(r);
+        uint64_t B = w.bases[r];
+        while (r < mid_end) {
+            const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
+            uint4 cn[2];
+            cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
+            cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
+            const uint32_t lan = ld_la(rn);
+            const uint64_t Bn = w.bases[rn];
+            process(r, c, full, la, (uint64_t) (r + 1) * R + lane < n, B);
+            r += nw;
+            c[0] = cn[0];
+            c[1] = cn[1];
+            la = lan;
+            B = Bn;
+        }
+    }
+    for (; r < nranges; r += nw) load_generic(r);
 }
 
 // Batches: buffer b is in[ioff(b) .. +len(b)) -> out + ooff(b).
@@ -2947,9 +3025,14 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                            a, ws, d_res, hold);
     if ((err = launch_status())) return err;
     if (p.R <= kP2Range && g_tune[5] != 1) {
-        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 8);
-        hipLaunchKernelGGL(g_tune[5] == 2 ? k_decode_pass2b : k_decode_pass2c, dim3(b2),
-                           dim3(kThreads), 0, s,
+        // grid-stride over the ranges with exactly the resident blocks (a
+        // second partial round of blocks would trail the rest)
+        auto k2 = g_tune[5] == 2 ? k_decode_pass2b
+                : g_tune[5] == 3 ? k_decode_pass2c<1> : k_decode_pass2c<0>;
+        static const int occ2c = occupancy_of(k_decode_pass2c<0>);
+        const int occ = g_tune[5] == 0 ? occ2c : 8;
+        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ);
+        hipLaunchKernelGGL(k2, dim3(b2), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
                            a, ws, hold);
         return launch_status();
