@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // bit 1 cached loads, any bit: not the tight/row kernels), 5 = 1: the
 // chunk-by-chunk pass 2, 6 = 1: the first-form tight/row batch kernels,
 // 7 = lanes' slots per batch-kernel tile (2 or 4), 8 = 1: the one-block
-// decode scan.
+// decode scan (2: look-back priced out, 3: tiles by block index).
 int g_tune[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 template <bool NT>
@@ -1148,6 +1148,8 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
 //   fd      ~((range << 32) | offset) of the first chunk pass 1 could not
 //           take on a fast path, combined with atomicMax over the waves that
 //           hit one; 0 = none.  The scan moves it to fd_cur and zeroes it.
+//   ticket  the scan's tile ticket (blocks take tiles in the order they
+//           start; zero between calls)
 //   counts  alphabet characters per range (pass 1, every range)
 //   bases   exclusive prefix of counts (scan, dirty calls only)
 //   status  per scan tile: flag (bits 63..62: 1 aggregate, 2 inclusive
@@ -1156,6 +1158,7 @@ DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
 struct DecodeWs {
     uint64_t *fd;
     uint64_t *fd_cur;
+    uint32_t *ticket;
     uint32_t *counts;
     uint64_t *bases;
     uint64_t *status;
@@ -1170,6 +1173,7 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     uint8_t *p = (uint8_t *) ws;
     w.fd = (uint64_t *) p;
     w.fd_cur = (uint64_t *) (p + 8);
+    w.ticket = (uint32_t *) (p + 16);
     w.counts = (uint32_t *) (p + 64);
     w.bases = (uint64_t *) (p + 64 + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     w.status = w.bases + nranges;
@@ -1504,16 +1508,19 @@ DEV uint64_t st_load(uint64_t *p)
 // tile of 1024 ranges.  Clean call (no first-dirty record): block 0 alone
 // computes V from the last range's count and the result record; every
 // other block returns at once.  Dirty call: a single-pass scan of
-// counts[r0 ..] with decoupled look-back and no atomic read-modify-write --
-// tile t is block t (workgroups are dispatched in order and the grid, at
-// most 1024 blocks, fits on the chip at once, so a tile's predecessors are
-// resident or done); each tile publishes its aggregate, looks back over its
+// counts[r0 ..] with decoupled look-back.  With TK (the default) blocks
+// take tiles from a ticket in the order they start, so a tile's
+// predecessors are always running or done and the look-back cannot wait on
+// a block that is not yet dispatched, whatever else shares the GPU (+6 us
+// on 1 GiB; TK = 0, tile = block index, relies on in-order dispatch across
+// the XCDs).  Each tile publishes its aggregate, looks back over its
 // predecessors 64 at a time (one wave) until an inclusive prefix,
 // publishes its own and writes the bases of its ranges.  The last tile
 // writes the result record and the tail sextets, waits until every tile
-// has published its inclusive prefix (so no look-back is still reading),
-// clears the status words and re-arms the workspace (fd -> fd_cur).
-template <int PRICE>
+// has published its inclusive prefix (so no look-back is still reading)
+// and every block has its ticket, then clears the status words and the
+// ticket and re-arms the workspace (fd -> fd_cur).
+template <int PRICE, int TK>
 __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
     DecAlpha a, void *ws, b64x_dec_result *res, uint32_t hold)
@@ -1521,6 +1528,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     __shared__ uint8_t tab[256];
     __shared__ uint64_t wtot[kWavesPerBlock];
     __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_tile;
     DecodeWs w = ws_view(ws, nranges);
     const uint64_t packed = *(volatile uint64_t *) w.fd;
     if (packed == 0) {
@@ -1537,7 +1545,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     }
     const uint32_t r0 = (uint32_t) (~packed >> 32);
     const uint32_t ntiles = (nranges - r0 + kScanTile - 1) / kScanTile;
-    const uint32_t t = blockIdx.x;
+    uint32_t t = blockIdx.x;
+    if (TK) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(w.ticket, 1u);
+        __syncthreads();
+        t = s_tile;
+    }
     if (t >= ntiles) return;
     build_dec_table(tab, a);
     const uint32_t base = r0 + t * kScanTile + 4 * threadIdx.x;
@@ -1603,6 +1616,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
         }
         for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.status[i], 0);
         if (lane == 0) {
+            if (TK) {  // every block has its ticket -> re-arm the counter
+                while (__hip_atomic_load(w.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       gridDim.x)
+                    __builtin_amdgcn_s_sleep(1);
+                __hip_atomic_store(w.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             *w.fd_cur = packed;
             *w.fd = 0;
         }
@@ -3019,10 +3038,14 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
         hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
                            nchars, p.R, p.nranges, a, ws, d_res, hold);
     else
-        hipLaunchKernelGGL(g_tune[8] == 2 ? k_decode_scan2<1> : k_decode_scan2<0>,
+    {
+        auto ks = g_tune[8] == 2 ? k_decode_scan2<1, 0>
+                : g_tune[8] == 3 ? k_decode_scan2<0, 0> : k_decode_scan2<0, 1>;
+        hipLaunchKernelGGL(ks,
                            dim3((p.nranges + kScanTile - 1) / kScanTile),
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges,
                            a, ws, d_res, hold);
+    }
     if ((err = launch_status())) return err;
     if (p.R <= kP2Range && g_tune[5] != 1) {
         // grid-stride over the ranges with exactly the resident blocks (a
