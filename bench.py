@@ -17,7 +17,8 @@ Also reported on the same JSON line:
                 PMC summary (profiles/pmc_<round>.json) when present;
   cpu_baseline  the oracle's scalar C restatement of the reference
                 (oracle/, "port"), 1 thread, on a bounded sample of the same
-                data, rank 0 at N=1 only;
+                data, rank 0 at N=1 only; `all_core`: the same oracle over
+                config 4's shape on up to 16 threads (the box's CPU share);
   batch_cfg4    BASELINE config 4: 1,048,576 x 1 KiB buffers split across
                 the ranks by index range, strided encode + decode, plus the
                 one exchange step (allgather of per-rank output totals).
@@ -54,6 +55,12 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=512 << 20,
                     help="bytes of the CPU baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int,
+                    default=min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                                else (os.cpu_count() or 1)),
+                    help="threads of the all-core CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-batch-bufs", type=int, default=1 << 18,
+                    help="1 KiB buffers in the all-core CPU baseline sample")
     ap.add_argument("--no-batch", action="store_true")
     ap.add_argument("--batch-steps", type=int, default=20)
     ap.add_argument("--backend", default="nccl",
@@ -210,6 +217,51 @@ def bench_batch(args, world, rank, b64):
     }
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_batch(args):
+    """The same oracle over config 4's shape (independent 1 KiB buffers, one
+    reference stage each), one thread per core of this process's CPU share
+    (ctypes drops the GIL), on a bounded sample of the batch."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    from oracle import pyoracle
+
+    threads = args.cpu_threads
+    nbuf, L = args.cpu_batch_bufs, 1024
+    E = (L + 2) // 3 * 4
+    rows = np.random.default_rng(0x5EED).integers(0, 256, (nbuf, L), dtype=np.uint8)
+    enc = np.empty((nbuf, E), dtype=np.uint8)
+    dec = np.empty((nbuf, (E + 3) // 4 * 3), dtype=np.uint8)
+    enc.fill(0)  # fault the pages in outside the timed region
+    dec.fill(0)
+    sl = [slice(i * nbuf // threads, (i + 1) * nbuf // threads) for i in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda q: pyoracle.encode_rows(rows[q], enc[q]), sl))
+        t1 = time.perf_counter()
+        list(ex.map(lambda q: pyoracle.decode_rows(enc[q], dec[q]), sl))
+        t2 = time.perf_counter()
+    if not np.array_equal(dec[:, :L], rows):
+        raise SystemExit("cpu batch baseline round trip mismatch")
+    b = nbuf * L
+    return {"value": b / (t2 - t0) / 2**30, "unit": "GiB/s", "cores": threads,
+            "sample": f"cfg4 shape, {nbuf} x 1 KiB buffers ({b >> 20} MiB), "
+                      f"encode {b / (t1 - t0) / 2**30:.2f} GiB/s, "
+                      f"decode {b / (t2 - t1) / 2**30:.2f} GiB/s"}
+
+
 def cpu_baseline(args, b64):
     import numpy as np
 
@@ -231,6 +283,8 @@ def cpu_baseline(args, b64):
         "unit": "GiB/s",
         "cores": 1,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "all_core": cpu_baseline_batch(args),
         "sample": f"first {n >> 20} MiB of the cfg2 buffer: oracle/b64_oracle.c "
                   f"(scalar restatement of src/base64encoder.c + src/base64decoder.c, "
                   f"-O2, 1 thread), encode {n / (t1 - t0) / 2**30:.3f} GiB/s, "

@@ -616,3 +616,33 @@ ssize_t orc_encode_counts(const uint8_t *in, size_t n, size_t src_chunk,
         return -1;
     return (ssize_t) t.n;
 }
+
+/* Row batches (bench.py's all-core CPU baseline: one call per thread over
+ * its slice of independent buffers, one reference stage per buffer, read
+ * with one read the size of the buffer's output -- a multiple of 4, so
+ * outside the reference's assert domain, base64encoder.c:124,140). */
+size_t orc_encode_rows(const uint8_t *in, size_t len, size_t nbuf, uint8_t *out,
+                       size_t out_stride)
+{
+    const size_t cap = (len + 2) / 3 * 4;
+    size_t tot = 0;
+    for (size_t i = 0; i < nbuf; i++) {
+        ssize_t r = orc_encode_stream(in + i * len, len, 0, 0, cap ? cap : 4, (char) -1,
+                                      (char) -1, 1, (char) -1, out + i * out_stride, cap, NULL);
+        tot += r < 0 ? 0 : (size_t) r;
+    }
+    return tot;
+}
+
+size_t orc_decode_rows(const uint8_t *in, size_t len, size_t nbuf, uint8_t *out,
+                       size_t out_stride)
+{
+    const size_t cap = (len + 3) / 4 * 3;
+    size_t tot = 0;
+    for (size_t i = 0; i < nbuf; i++) {
+        ssize_t r = orc_decode_stream(in + i * len, len, 0, 0, len > 4 ? len : 4, (char) -1,
+                                      (char) -1, out + i * out_stride, cap ? cap : 1);
+        tot += r < 0 ? 0 : (size_t) r;
+    }
+    return tot;
+}

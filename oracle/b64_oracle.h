@@ -30,6 +30,14 @@ size_t orc_encode(const uint8_t *in, size_t n, char pos62, char pos63, int pad,
 size_t orc_decode(const uint8_t *in, size_t n, char pos62, char pos63,
                   uint8_t *out);
 
+/* nbuf independent rows of `len` bytes/characters at in + i*len, each
+ * encoded (default alphabet, padding) or decoded to out + i*out_stride;
+ * return the total bytes written. */
+size_t orc_encode_rows(const uint8_t *in, size_t len, size_t nbuf, uint8_t *out,
+                       size_t out_stride);
+size_t orc_decode_rows(const uint8_t *in, size_t len, size_t nbuf, uint8_t *out,
+                       size_t out_stride);
+
 /* Pull-model simulations with the reference's read pattern:
  *  - the source hands out at most `src_chunk` bytes per read (0 = no
  *    limit);

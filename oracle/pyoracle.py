@@ -48,6 +48,10 @@ def lib() -> ctypes.CDLL:
         L.orc_encode_counts.argtypes = [_vp, _sz, _sz, _sz, _sz, _ch, _ch, ctypes.c_int, _ch,
                                         _vp, _sz]
         L.orc_encode_counts.restype = _ssz
+        L.orc_encode_rows.argtypes = [_vp, _sz, _sz, _vp, _sz]
+        L.orc_encode_rows.restype = _sz
+        L.orc_decode_rows.argtypes = [_vp, _sz, _sz, _vp, _sz]
+        L.orc_decode_rows.restype = _sz
         _lib = L
     return _lib
 
@@ -76,6 +80,17 @@ def encode(data, pos62=-1, pos63=-1, pad=True, padchar=-1, as_array=False):
     n = lib().orc_encode(_p(a), a.size, _c(pos62), _c(pos63), int(bool(pad)),
                          _c(padchar), out.ctypes.data)
     return out[:n] if as_array else out[:n].tobytes()
+
+
+def encode_rows(rows: np.ndarray, out: np.ndarray) -> int:
+    """Encode each row of `rows` (nbuf x len, uint8, C-contiguous) into the
+    matching row of `out` (nbuf x >= E); default alphabet, padding.  Runs
+    without the GIL (ctypes), so threads over row slices run in parallel."""
+    return lib().orc_encode_rows(_p(rows), rows.shape[1], rows.shape[0], _p(out), out.shape[1])
+
+
+def decode_rows(rows: np.ndarray, out: np.ndarray) -> int:
+    return lib().orc_decode_rows(_p(rows), rows.shape[1], rows.shape[0], _p(out), out.shape[1])
 
 
 def decode(data, pos62=-1, pos63=-1, as_array=False):
