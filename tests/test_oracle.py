@@ -130,3 +130,25 @@ def test_decode_table_rules():
     assert t[ord("A")] == 0 and t[ord("*")] == 63
     t = orc.decode_table("*", "*")          # 62 wins
     assert t[ord("*")] == 62
+
+
+def test_oracle_rows_match_stdlib():
+    """The oracle's row-batch entry points (bench.py's all-core CPU
+    baseline) agree with the single-buffer ones and with stdlib base64."""
+    import base64
+
+    import numpy as np
+
+    from oracle import pyoracle
+
+    rng = np.random.default_rng(3)
+    for L in (1, 2, 3, 4, 1023, 1024, 1025):
+        rows = rng.integers(0, 256, (37, L), dtype=np.uint8)
+        E = (L + 2) // 3 * 4
+        enc = np.zeros((37, E + 5), np.uint8)
+        assert pyoracle.encode_rows(rows, enc) == 37 * E
+        for i in (0, 17, 36):
+            assert enc[i, :E].tobytes() == base64.b64encode(rows[i].tobytes())
+        dec = np.zeros((37, (E + 3) // 4 * 3), np.uint8)
+        assert pyoracle.decode_rows(np.ascontiguousarray(enc[:, :E]), dec) == 37 * L
+        assert np.array_equal(dec[:, :L], rows)
