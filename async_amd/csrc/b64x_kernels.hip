@@ -42,7 +42,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "b64x.h"
 
@@ -2654,7 +2656,9 @@ constexpr int kMaxDevices = 64;
 std::mutex g_mu;
 DeviceInfo g_info[kMaxDevices];
 bool g_info_done[kMaxDevices];
-void *g_ws[kMaxDevices];
+// Library-owned decode workspaces, one per (device, stream): a workspace
+// carries state from pass 1 to pass 2, so streams must not share one.
+std::map<std::pair<int, void *>, void *> g_ws;
 
 const DeviceInfo *device_info()
 {
@@ -2989,7 +2993,7 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
     return launch_status();
 }
 
-static void *library_workspace(int *err)
+static void *library_workspace(void *stream, int *err)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
@@ -2997,18 +3001,20 @@ static void *library_workspace(int *err)
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ws[dev]) {
+    void *&ws = g_ws[{dev, stream}];
+    if (!ws) {
         void *p = nullptr;
         hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
         if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
         if (e != hipSuccess) {
+            if (p) (void) hipFree(p);
             *err = hip_err(e);
             return nullptr;
         }
-        g_ws[dev] = p;
+        ws = p;
     }
     *err = 0;
-    return g_ws[dev];
+    return ws;
 }
 
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
@@ -3024,7 +3030,7 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     if (nchars == 0)
         return hip_err(hipMemsetAsync(d_res, 0, sizeof(b64x_dec_result), s));
     int err = 0;
-    void *ws = d_workspace ? d_workspace : library_workspace(&err);
+    void *ws = d_workspace ? d_workspace : library_workspace(stream, &err);
     if (!ws) return err;
     const Pass1Launch p1 = pass1_variant(g_tune[1]);
     const RangePlan p = plan_ranges(nchars);

@@ -97,8 +97,8 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * d_workspace: b64x_decode_workspace_size(nchars) bytes of device memory,
  * zero-filled before its first use (each call leaves it ready for the
  * next; one workspace per stream), or NULL to use a library-owned one
- * (allocated on first use: not capture-safe on that first call, and not
- * safe to share between concurrent streams). */
+ * per (device, stream) (allocated on the first such call for that stream:
+ * that call is not capture-safe). */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);

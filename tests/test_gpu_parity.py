@@ -380,3 +380,39 @@ def test_fill_splitmix64():
     b64.fill_splitmix64(x, 0x5EED)
     assert np.array_equal(x.cpu().numpy(), util.splitmix64(0x5EED, 4099))
     assert x[:16].cpu().numpy().tobytes().hex() == d["splitmix64_head"]["first16"]
+
+
+def test_library_workspace_per_stream():
+    """d_workspace = NULL on two streams at once: each stream gets its own
+    library workspace, so concurrent dirty decodes (pass 1 -> scan -> pass 2
+    state lives in the workspace) do not trample each other."""
+    import ctypes
+
+    from async_amd import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = []
+    for k in range(2):
+        raw = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+        chars = orc.encode(raw)
+        dirty = _junk(rng, chars, 0.01 * (k + 1))
+        x = dev(dirty)
+        out = torch.empty(b64.decoded_cap(len(dirty)), dtype=torch.uint8, device=DEV)
+        res = torch.zeros(24, dtype=torch.uint8, device=DEV)
+        jobs.append((x, out, res, raw))
+    a = b64._abc(None)
+    torch.cuda.synchronize()
+    for rep in range(4):  # interleave the two streams' launches
+        for (x, out, res, _), st in zip(jobs, streams):
+            rc = lib.b64x_decode_dev(ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                     ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(res.data_ptr()), ctypes.byref(a), 0,
+                                     None, ctypes.c_void_p(st.cuda_stream))
+            assert rc == 0
+    torch.cuda.synchronize()
+    for x, out, res, raw in jobs:
+        info = b64.Decoded(out, res).info()
+        assert info.out_len == raw.size
+        assert np.array_equal(out[: raw.size].cpu().numpy(), raw)
