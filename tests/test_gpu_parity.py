@@ -416,3 +416,26 @@ def test_library_workspace_per_stream():
         info = b64.Decoded(out, res).info()
         assert info.out_len == raw.size
         assert np.array_equal(out[: raw.size].cpu().numpy(), raw)
+
+
+@pytest.mark.parametrize("fmt", ["crlf76", "lf64", "cr_lf_lf60", "crlf76_broken", "lf17",
+                                 "lf16", "crlf300"])
+def test_decode_line_structured(fmt):
+    """Line-wrapped text (MIME CRLF-76, PEM LF-64, odd separators, a line of
+    a different length mid-stream, line lengths at the fast path's limits):
+    the line-structured ranges of pass 2 and their fall-backs, vs the oracle."""
+    rng = np.random.default_rng(len(fmt))
+    host = rng.integers(0, 256, 700_001, dtype=np.uint8)
+    chars = orc.encode(host)
+    Lc, sep = {"crlf76": (76, b"\r\n"), "lf64": (64, b"\n"), "cr_lf_lf60": (60, b"\r\n\n"),
+               "crlf76_broken": (76, b"\r\n"), "lf17": (17, b"\n"), "lf16": (16, b"\n"),
+               "crlf300": (300, b"\r\n")}[fmt]
+    lines = [chars[i:i + Lc] for i in range(0, len(chars), Lc)]
+    if fmt == "crlf76_broken":
+        lines[5000] = lines[5000][:40]  # one short line mid-stream
+    dirty = sep.join(lines) + sep
+    got, info = gdec(dirty)
+    want = orc.decode(dirty)
+    assert got == want, fmt
+    if fmt != "crlf76_broken":
+        assert got == host.tobytes()
