@@ -17,11 +17,13 @@
  *
  * Semantics: the produced character stream is the reference's, byte for
  * byte (standard base64, chars 62/63 = pos62/pos63, optional padding with
- * padchar, no line breaks; (char) -1 selects '+', '/', '=').  Documented
- * divergences: a read() may return fewer characters
- * than the reference would at the same point (never 0 before EOF), and
- * the reference's assert at src/base64encoder.c:140 for read counts not
- * divisible by 4 is not reproduced -- every count works here.
+ * padchar, no line breaks; (char) -1 selects '+', '/', '=').  So are the
+ * read counts: `count` whenever upstream keeps up, the full
+ * sextets of a partial group in the same read, finalize()'s characters in
+ * a read of their own -- except that a read answers -1/EAGAIN while its
+ * block is still on the GPU (a callback follows).  The reference's assert
+ * at src/base64encoder.c:140 for read counts not divisible by 4 is not
+ * reproduced: every count works here.
  */
 #ifndef ASYNC_AMD_BASE64ENCODER_H
 #define ASYNC_AMD_BASE64ENCODER_H
