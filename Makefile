@@ -56,7 +56,8 @@ $(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h
 
 $(HARNESS): tests/csrc/stage_harness.c $(LIB) $(HEADERS)
 	$(CC) $(CFLAGS) -shared -o $@ tests/csrc/stage_harness.c \
-	    -Lasync_amd -lasync_b64 -Wl,-rpath,'$$ORIGIN/../../async_amd'
+	    -Lasync_amd -lasync_b64 -Wl,-rpath,'$$ORIGIN/../../async_amd' \
+	    -L/opt/rocm/lib -lamdhip64 -lpthread
 
 clean:
 	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS)

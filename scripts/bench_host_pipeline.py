@@ -185,10 +185,12 @@ def run_egress(n_msgs: int, thread_counts=(1, 4, 8, 16)):
     nbytes = int(lens.sum())
     offs = np.concatenate([[0], np.cumsum(lens)])
     util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
+    ndev = util.device_count()
     for T in thread_counts:
         times = np.zeros(2)
+        gpus = min(T, ndev)  # loop t on GPU t mod gpus (8 on a full node)
         res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times, raw=True,
-                                      threads=T)
+                                      threads=T, devices=gpus)
         dt = float(times.sum())
         out, out_off, out_len = res
         idx = list(range(0, n_msgs, max(1, n_msgs // 64)))
@@ -199,7 +201,8 @@ def run_egress(n_msgs: int, thread_counts=(1, 4, 8, 16)):
         framed_total = int(out_len.sum())
         del out, res
         cpu_dt = _oracle_stack_rate(payload, lens, T)
-        print(json.dumps({"measure": "egress_config5", "threads": T, "messages": n_msgs,
+        print(json.dumps({"measure": "egress_config5", "threads": T, "gpus": gpus,
+                          "messages": n_msgs,
                           "bytes": nbytes, "framed_bytes": framed_total, "seconds": dt,
                           "setup_s": float(times[0]), "loop_s": float(times[1]),
                           "GiB_s": nbytes / dt / 2**30, "msgs_per_s": n_msgs / dt,

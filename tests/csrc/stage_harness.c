@@ -455,12 +455,28 @@ typedef struct {
     uint64_t *out_len;
     int err;
     double times[2];
+    int device;  /* -1: the calling thread's current device */
 } egress_share;
+
+/* HIP runtime entry points (C linkage; hipError_t is an int-sized enum):
+ * the threaded driver can put each event loop on its own GPU. */
+extern int hipSetDevice(int device);
+extern int hipGetDeviceCount(int *count);
+
+int h_device_count(void)
+{
+    int n = 0;
+    return hipGetDeviceCount(&n) == 0 ? n : 0;
+}
 
 static void *egress_thread(void *arg)
 {
     egress_share *e = arg;
     size_t f = e->first;
+    if (e->device >= 0 && hipSetDevice(e->device) != 0) {
+        e->err = ENODEV;
+        return NULL;
+    }
     /* out pointers are absolute; shift offsets to this share */
     e->err = 0;
     if (h_egress_stacks(e->in, e->in_off + f, e->count, e->max_chunk, e->read_size,
@@ -473,11 +489,29 @@ static void *egress_thread(void *arg)
 
 #include <pthread.h>
 
+/* Config 5 over `nthreads` event loops; with ndevices > 1 loop t runs on
+ * GPU t mod ndevices (every stage of a loop uses its loop's GPU). */
+int h_egress_stacks_mt_dev(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                           size_t max_chunk, size_t read_size, char pos62, char pos63,
+                           int pad, char padchar, uint8_t *out, const uint64_t *out_off,
+                           uint64_t *out_len, int *err_out, double *times,
+                           size_t nthreads, int ndevices);
+
 int h_egress_stacks_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
                        size_t max_chunk, size_t read_size, char pos62, char pos63,
                        int pad, char padchar, uint8_t *out, const uint64_t *out_off,
                        uint64_t *out_len, int *err_out, double *times,
                        size_t nthreads)
+{
+    return h_egress_stacks_mt_dev(in, in_off, nmsg, max_chunk, read_size, pos62, pos63, pad,
+                                  padchar, out, out_off, out_len, err_out, times, nthreads, 1);
+}
+
+int h_egress_stacks_mt_dev(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                           size_t max_chunk, size_t read_size, char pos62, char pos63,
+                           int pad, char padchar, uint8_t *out, const uint64_t *out_off,
+                           uint64_t *out_len, int *err_out, double *times,
+                           size_t nthreads, int ndevices)
 {
     if (nthreads < 1)
         nthreads = 1;
@@ -497,7 +531,11 @@ int h_egress_stacks_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
                 last++;
         sh[t] = (egress_share) { in, in_off, first, last - first, max_chunk, read_size,
                                  pos62, pos63, padchar, pad, out, out_off, out_len, 0,
-                                 { 0, 0 } };
+                                 { 0, 0 }, -1 };
+        if (ndevices > 1) {  /* loop t on GPU t mod ndevices (mod what exists) */
+            const int have = h_device_count();
+            sh[t].device = have > 0 ? (int) (t % (size_t) ndevices) % have : 0;
+        }
         first = last;
     }
     double t0 = now_s();

@@ -98,13 +98,16 @@ def test_config5_full():
         assert framed[i] == orc.chunked_encode(msg, max_chunk=1 << 20), i
 
 
-@pytest.mark.parametrize("threads", [2, 5])
-def test_egress_stacks_threads(threads):
-    """Several event loops (one per thread, each with its own hub) on one
-    GPU, sharing the messages."""
+@pytest.mark.parametrize("threads,devices", [(2, 1), (5, 1), (4, 2)])
+def test_egress_stacks_threads(threads, devices):
+    """Several event loops (one per thread, each with its own hub) sharing
+    the messages; devices > 1: each loop pinned to GPU t mod devices (on a
+    one-GPU box every loop lands on GPU 0, through the same hipSetDevice
+    path a full node takes)."""
     lens = util.zipf_lengths()[:400]
     payload = util.splitmix64(0x5EED, int(lens.sum()))
-    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240, threads=threads)
+    framed, err = util.egress_stacks(payload, lens, 1 << 20, 10240, threads=threads,
+                                     devices=devices)
     assert err == 0
     off = 0
     for i, L in enumerate(lens.tolist()):

@@ -68,6 +68,10 @@ def harness() -> ctypes.CDLL:
         L.h_egress_stacks.restype = ctypes.c_int
         L.h_egress_stacks_mt.argtypes = L.h_egress_stacks.argtypes + [sz]
         L.h_egress_stacks_mt.restype = ctypes.c_int
+        L.h_egress_stacks_mt_dev.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
+        L.h_egress_stacks_mt_dev.restype = ctypes.c_int
+        L.h_device_count.argtypes = []
+        L.h_device_count.restype = ctypes.c_int
         _harness = L
     return _harness
 
@@ -174,9 +178,15 @@ def framed_cap(n: int, max_chunk: int) -> int:
     return chars + (chars // max(max_chunk, 2) + 3) * 16 + 16
 
 
+def device_count() -> int:
+    return int(harness().h_device_count())
+
+
 def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos62=-1,
-                  pos63=-1, pad=True, padchar=-1, times=None, raw=False, threads=1):
-    """Run len(lens) GPU egress stacks on one loop; returns
+                  pos63=-1, pad=True, padchar=-1, times=None, raw=False, threads=1,
+                  devices=1):
+    """Run len(lens) GPU egress stacks on `threads` loops (loop t on GPU
+    t mod `devices` when devices > 1); returns
     (list of framed bytes | None, errno).  `times` (a float64[2] array)
     receives the C-side setup and loop seconds; raw=True returns
     (out, out_off, out_len) instead of a list."""
@@ -195,7 +205,9 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
     args = (src.ctypes.data, in_off.ctypes.data, lens.size, max_chunk, read_size, cch(pos62),
             cch(pos63), int(bool(pad)), cch(padchar), out.ctypes.data, out_off.ctypes.data,
             out_len.ctypes.data, ctypes.byref(err), tp)
-    if threads > 1:
+    if devices > 1:
+        rc = harness().h_egress_stacks_mt_dev(*args, max(threads, 1), devices)
+    elif threads > 1:
         rc = harness().h_egress_stacks_mt(*args, threads)
     else:
         rc = harness().h_egress_stacks(*args)
