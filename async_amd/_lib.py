@@ -76,6 +76,8 @@ SIGNATURES = {
     "b64x_decode_batch": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp]),
     "b64x_session_open": (_vp, [_u64]),
     "b64x_session_close": (None, [_vp]),
+    "b64x_session_acquire": (_vp, [_u64]),
+    "b64x_session_release": (None, [_vp]),
     "b64x_session_capacity": (_u64, [_vp]),
     "b64x_session_host_in": (_vp, [_vp]),
     "b64x_session_host_out": (_vp, [_vp]),

@@ -200,11 +200,11 @@ static int stage_start(stage *st, size_t count)
         st->efd = -1;
         return -e;
     }
-    for (int i = 0; i < NSLOTS; i++) {
-        st->slots[i].sess = b64x_session_open(st->cap);
-        if (!st->slots[i].sess)
-            return -(errno ? errno : ENODEV);
-    }
+    /* sessions come from the process-wide pool as slots are first used
+     * (a short message needs one, not NSLOTS) */
+    int rc = b64x_device_check(); /* fail loudly: no CPU path */
+    if (rc)
+        return rc;
     st->started = true;
     return 0;
 }
@@ -220,8 +220,7 @@ static void stage_stop(stage *st)
     }
     for (int i = 0; i < NSLOTS; i++) {
         if (st->slots[i].sess) {
-            (void) b64x_session_wait(st->slots[i].sess);
-            b64x_session_close(st->slots[i].sess);
+            b64x_session_release(st->slots[i].sess); /* waits, then pools */
             st->slots[i].sess = NULL;
         }
     }
@@ -373,6 +372,11 @@ static int top_up_decoder(stage *st)
                          ? &st->slots[(st->head + st->nbusy + NSLOTS - 1) %
                                       NSLOTS]
                          : NULL;
+        if (!sl->sess) {
+            sl->sess = b64x_session_acquire(st->cap);
+            if (!sl->sess)
+                return -(errno ? errno : ENOMEM);
+        }
         bool eof;
         int uerr;
         size_t got = gather(st, b64x_session_host_in(sl->sess), st->cap, &eof,

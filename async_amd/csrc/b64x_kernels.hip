@@ -3332,6 +3332,50 @@ void b64x_session_close(b64x_session *s)
 }
 
 uint64_t b64x_session_capacity(const b64x_session *s) { return s ? s->cap : 0; }
+
+// Idle sessions, any device / capacity; at most kPoolMax kept.
+static std::mutex g_pool_mu;
+static b64x_session *g_pool[64];
+static int g_npool;
+constexpr int kPoolMax = 64;
+
+static bool pool_enabled()
+{
+    static const bool on = [] {
+        const char *v = getenv("ASYNC_B64_SESSION_POOL");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
+b64x_session *b64x_session_acquire(uint64_t capacity)
+{
+    int dev = 0;
+    if (pool_enabled() && hipGetDevice(&dev) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (int i = g_npool - 1; i >= 0; i--) {
+            b64x_session *s = g_pool[i];
+            if (s->device == dev && s->cap == capacity) {
+                g_pool[i] = g_pool[--g_npool];
+                return s;
+            }
+        }
+    }
+    return b64x_session_open(capacity);
+}
+
+void b64x_session_release(b64x_session *s)
+{
+    if (!s) return;
+    if (pool_enabled() && b64x_session_wait(s) == 0) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_npool < kPoolMax) {
+            g_pool[g_npool++] = s;
+            return;
+        }
+    }
+    b64x_session_close(s);
+}
 uint8_t *b64x_session_host_in(b64x_session *s) { return s ? s->h_in : nullptr; }
 uint8_t *b64x_session_host_out(b64x_session *s) { return s ? s->h_out : nullptr; }
 

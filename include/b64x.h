@@ -139,6 +139,14 @@ typedef struct b64x_session b64x_session;
 b64x_session *b64x_session_open(uint64_t capacity);
 void b64x_session_close(b64x_session *s);
 uint64_t b64x_session_capacity(const b64x_session *s);
+/* Pooled form: acquire takes an idle session of this capacity on the
+ * current device from a process-wide pool (opening one if there is none);
+ * release waits for the session's queued work and returns it to the pool
+ * (closing it when the pool is full).  Opening a session costs pinned
+ * allocations and a HIP stream -- milliseconds -- so stages that come and
+ * go per message reuse them. */
+b64x_session *b64x_session_acquire(uint64_t capacity);
+void b64x_session_release(b64x_session *s);
 /* Pinned host staging areas: fill host_in, read results from host_out. */
 uint8_t *b64x_session_host_in(b64x_session *s);
 uint8_t *b64x_session_host_out(b64x_session *s);
