@@ -240,7 +240,7 @@ static void launch_ready(b64_hub *h)
         h->running[i] = b;
         h->inflight++;
         int rc = 0;
-        if (!h->lanes[i] && !(h->lanes[i] = b64x_lane_open()))
+        if (!h->lanes[i] && !(h->lanes[i] = b64x_lane_acquire()))
             rc = -(errno ? errno : ENODEV);
         if (!rc)
             rc = b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
@@ -471,7 +471,7 @@ static void hub_destroy(b64_hub *h)
             batch_put(h->running[i]);
             h->running[i] = NULL;
         }
-        b64x_lane_close(h->lanes[i]);
+        b64x_lane_release(h->lanes[i]);
     }
     if (h->filling)
         batch_put(h->filling);

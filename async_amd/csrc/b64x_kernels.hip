@@ -3531,6 +3531,38 @@ void b64x_lane_close(b64x_lane *l)
     free(l);
 }
 
+static b64x_lane *g_lane_pool[64];
+static int g_nlane_pool;
+
+b64x_lane *b64x_lane_acquire(void)
+{
+    int dev = 0;
+    if (pool_enabled() && hipGetDevice(&dev) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (int i = g_nlane_pool - 1; i >= 0; i--) {
+            b64x_lane *l = g_lane_pool[i];
+            if (l->device == dev) {
+                g_lane_pool[i] = g_lane_pool[--g_nlane_pool];
+                return l;
+            }
+        }
+    }
+    return b64x_lane_open();
+}
+
+void b64x_lane_release(b64x_lane *l)
+{
+    if (!l) return;
+    if (pool_enabled() && b64x_lane_wait(l) == 0) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_nlane_pool < kPoolMax) {
+            g_lane_pool[g_nlane_pool++] = l;
+            return;
+        }
+    }
+    b64x_lane_close(l);
+}
+
 // Grow a device buffer to at least `need` (rounded up: growth is rare).
 static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need)
 {

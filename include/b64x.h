@@ -204,6 +204,11 @@ typedef struct b64x_lane b64x_lane;
 
 b64x_lane *b64x_lane_open(void);
 void b64x_lane_close(b64x_lane *l);
+/* Pooled form (see b64x_session_acquire): an idle lane of the current
+ * device from the process-wide pool, or a new one; release waits for the
+ * lane's queued work and pools it. */
+b64x_lane *b64x_lane_acquire(void);
+void b64x_lane_release(b64x_lane *l);
 /* Encode njobs buffers: buffer i is h_in[h_in_off[i] .. h_in_off[i+1])
  * and its b64x_encoded_len(len, abc->pad) characters go to
  * h_out + h_out_off[i] (both offset arrays hold njobs+1 monotone entries
