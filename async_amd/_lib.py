@@ -94,6 +94,7 @@ SIGNATURES = {
     "b64x_lane_acquire": (_vp, []),
     "b64x_lane_release": (None, [_vp]),
     "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp, _vp]),
+    "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _ap, _vp, _vp]),
     "b64x_lane_wait": (_int, [_vp]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),

@@ -1,5 +1,6 @@
 /*
- * b64_hub.c -- cross-stream batching of encoder blocks (see b64_hub.h).
+ * b64_hub.c -- cross-stream batching of encoder blocks and short decoder
+ * streams (see b64_hub.h).
  *
  * Life of an arena ("batch"):
  *
@@ -39,6 +40,8 @@ struct b64_batch {
     b64_batch *next;             /* ready / free list */
     uint8_t *h_in, *h_out;       /* pinned arenas */
     uint64_t *h_in_off, *h_out_off; /* pinned, HUB_JOBS + 1 each */
+    uint64_t *h_outlen;          /* pinned, HUB_JOBS: decode byte counts */
+    b64_hub_kind kind;
     b64_ticket **jobs;
     size_t in_cap, out_cap;
     size_t in_used, out_used;
@@ -111,6 +114,7 @@ static void batch_free(b64_batch *b)
     b64x_host_free(b->h_out);
     b64x_host_free(b->h_in_off);
     b64x_host_free(b->h_out_off);
+    b64x_host_free(b->h_outlen);
     free(b->jobs);
     free(b);
 }
@@ -128,8 +132,9 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     b->h_out = b64x_host_alloc(b->out_cap);
     b->h_in_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
     b->h_out_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
+    b->h_outlen = b64x_host_alloc(HUB_JOBS * sizeof(uint64_t));
     b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
-    if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->jobs) {
+    if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_outlen || !b->jobs) {
         batch_free(b);
         errno = ENOMEM;
         return NULL;
@@ -243,8 +248,12 @@ static void launch_ready(b64_hub *h)
         if (!h->lanes[i] && !(h->lanes[i] = b64x_lane_acquire()))
             rc = -(errno ? errno : ENODEV);
         if (!rc)
-            rc = b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
-                                        b->h_out, b->h_out_off, &b->abc, batch_done, b);
+            rc = b->kind == B64_HUB_DECODE
+                     ? b64x_lane_decode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
+                                              b->h_out, b->h_out_off, b->h_outlen, &b->abc,
+                                              batch_done, b)
+                     : b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
+                                              b->h_out, b->h_out_off, &b->abc, batch_done, b);
         if (rc) { /* report through the normal completion path */
             b->err = rc;
             batch_done(b);
@@ -366,6 +375,8 @@ static void complete(b64_hub *h, b64_batch *b, bool collect)
         if (!t)
             continue;
         t->out = b->h_out + b->h_out_off[j];
+        if (b->kind == B64_HUB_DECODE)
+            t->out_len = b->err ? 0 : (size_t) b->h_outlen[j];
         t->err = b->err;
         atomic_store_explicit(&t->done, 1, memory_order_release);
         if (collect)
@@ -453,10 +464,11 @@ static void hub_destroy(b64_hub *h)
     if (h->tr.on)
         fprintf(stderr,
                 "b64_hub: batches %lu jobs %lu in %llu out %llu allocs %lu "
-                "max_ready %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f\n",
+                "max_ready %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f "
+                "first %.6f last %.6f\n",
                 h->tr.batches, h->tr.jobs, h->tr.in_bytes, h->tr.out_bytes,
                 h->tr.allocs, h->tr.max_ready, h->tr.wake_calls, h->tr.wake_s,
-                h->tr.launch_s, h->tr.t_last - h->tr.t_first);
+                h->tr.launch_s, h->tr.t_last - h->tr.t_first, h->tr.t_first, h->tr.t_last);
     pthread_mutex_lock(&registry_lock);
     for (b64_hub **p = &registry; *p; p = &(*p)->next_hub) {
         if (*p == h) {
@@ -512,20 +524,20 @@ void b64_hub_forget(b64_hub *h, void *obj)
 
 /* -------------------------------------------------------------- the API */
 
-uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
-                         size_t min_room, size_t *granted, action_1 waiter)
+uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
+                         size_t room, size_t min_room, size_t *granted, action_1 waiter)
 {
     if (min_room > room)
         min_room = room;
     b64_batch *b = h->filling;
-    if (b && (memcmp(&b->abc, abc, sizeof *abc) || b->njobs == HUB_JOBS ||
+    if (b && (b->kind != kind || memcmp(&b->abc, abc, sizeof *abc) || b->njobs == HUB_JOBS ||
               b->in_cap - b->in_used < (min_room ? min_room : 1))) {
         if (b->njobs) {
             seal(h);
             launch_ready(h);
         }
         b = h->filling; /* NULL after seal; kept if it was empty */
-        if (b && (b->in_cap < room || memcmp(&b->abc, abc, sizeof *abc))) {
+        if (b && (b->in_cap < room || b->kind != kind || memcmp(&b->abc, abc, sizeof *abc))) {
             h->filling = NULL;
             batch_put(b);
             h->live--;
@@ -551,6 +563,7 @@ uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
             return NULL;
         b->state = B_FILLING;
         b->abc = *abc;
+        b->kind = kind;
         h->filling = b;
     }
     size_t avail = b->in_cap - b->in_used;
@@ -575,6 +588,7 @@ void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
     t->index = j;
     t->err = 0;
     t->out = NULL;
+    t->out_len = 0;
     t->wake = wake;
     atomic_store_explicit(&t->done, 0, memory_order_relaxed);
     schedule_flush(h);

@@ -1,6 +1,6 @@
 /*
- * b64_hub.h -- internal: cross-stream batching of encoder blocks for one
- * event loop.
+ * b64_hub.h -- internal: cross-stream batching of encoder blocks, and of
+ * short decoder streams, for one event loop.
  *
  * Every base64 encoder stage on an async_t shares one hub.  A stage
  * reserves room in the hub's open pinned arena, reads its upstream
@@ -35,9 +35,13 @@ typedef struct {
     uint32_t index;        /* job index in the batch */
     atomic_int done;       /* output ready (or err set) */
     int err;               /* negative errno if the batch failed */
-    const uint8_t *out;    /* the block's characters, valid once done */
+    const uint8_t *out;    /* the block's output, valid once done */
+    size_t out_len;        /* decode jobs: the bytes decoded (device count) */
     action_1 wake;         /* performed on the loop when done */
 } b64_ticket;
+
+/* What a batch does with its jobs. */
+typedef enum { B64_HUB_ENCODE = 0, B64_HUB_DECODE = 1 } b64_hub_kind;
 
 /* The hub for `async` (created on first use); NULL + errno on failure. */
 b64_hub *b64_hub_acquire(async_t *async);
@@ -54,11 +58,14 @@ void b64_hub_release(b64_hub *h);
  * the waiter is performed once an arena is recycled; NULL_ACTION_1-like
  * {.act = NULL} callers (stages holding data, which must make progress)
  * are always served. */
-uint8_t *b64_hub_reserve(b64_hub *h, const b64x_alphabet *abc, size_t room,
-                         size_t min_room, size_t *granted, action_1 waiter);
+uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
+                         size_t room, size_t min_room, size_t *granted, action_1 waiter);
 /* Drop any waiter whose object is `obj` (its stage is closing). */
 void b64_hub_forget(b64_hub *h, void *obj);
-/* Turn the reservation into a job of n bytes -> out_len characters. */
+/* Turn the reservation into a job of n bytes -> out_len characters
+ * (encode) or of n characters -> at most out_len bytes (decode: a whole
+ * stream, its final partial group emitted; the count lands in
+ * ticket->out_len). */
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
                     action_1 wake);
 void b64_hub_cancel(b64_hub *h);

@@ -75,7 +75,9 @@ typedef struct stage stage;
 typedef struct {
     stage *owner;
     b64x_session *sess; /* decoder: this slot's session */
-    b64_ticket ticket;  /* encoder: this slot's job in a hub batch */
+    b64_ticket ticket;  /* encoder, and a short decoder stream: this slot's
+                           job in a hub batch */
+    bool hubbed;        /* decoder: the slot's block went through the hub */
     atomic_int done;    /* decoder: set by the HIP host function */
     bool resolved;    /* out_len/body_end valid (decoder: after done) */
     size_t out_pos;
@@ -93,7 +95,9 @@ struct stage {
     direction dir;
     b64x_alphabet abc;
     size_t cap, min_pull, max_cap;
-    b64_hub *hub;       /* encoder: the loop's batching hub */
+    b64_hub *hub;       /* the loop's batching hub */
+    bool hub_first;     /* decoder: the first block may go through the hub
+                           (a stream that ends inside it is one job) */
     int efd;            /* decoder: GPU completion -> loop */
     bool started;       /* hub / sessions + eventfd exist */
     int err;            /* sticky failure errno, 0 while healthy */
@@ -153,6 +157,23 @@ static void stage_wake(stage *st)
     action_1_perf(st->cb);
 }
 
+/* The session path's completion eventfd, created on first use. */
+static int stage_efd(stage *st)
+{
+    if (st->efd >= 0)
+        return 0;
+    int fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (fd < 0)
+        return -errno;
+    if (async_register(st->async, fd, (action_1) { st, (act_1) stage_wake }) < 0) {
+        int e = errno ? errno : EIO;
+        close(fd);
+        return -e;
+    }
+    st->efd = fd;
+    return 0;
+}
+
 /* HIP runtime thread: publish, then signal. */
 static void slot_done(void *arg)
 {
@@ -190,21 +211,17 @@ static int stage_start(stage *st, size_t count)
         st->started = true;
         return 0;
     }
-    st->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    if (st->efd < 0)
-        return -errno;
-    if (async_register(st->async, st->efd,
-                       (action_1) { st, (act_1) stage_wake }) < 0) {
-        int e = errno ? errno : EIO;
-        close(st->efd);
-        st->efd = -1;
-        return -e;
-    }
-    /* sessions come from the process-wide pool as slots are first used
-     * (a short message needs one, not NSLOTS) */
+    /* A stream that ends inside its first block is decoded as one job of
+     * a hub batch (many short streams, one launch); longer streams take
+     * sessions, from the process-wide pool as slots are first used, and
+     * only they need a completion eventfd (each new descriptor can cost
+     * the process an fd-table expansion: thousands of short streams on a
+     * loop must not pay that). */
     int rc = b64x_device_check(); /* fail loudly: no CPU path */
     if (rc)
         return rc;
+    st->hub = b64_hub_acquire(st->async);
+    st->hub_first = st->hub != NULL;
     st->started = true;
     return 0;
 }
@@ -315,7 +332,7 @@ static int top_up_encoder(stage *st)
         action_1 waiter = { NULL, NULL };
         if (!must_progress)
             waiter = (action_1) { st, (act_1) stage_notify };
-        uint8_t *in = b64_hub_reserve(st->hub, &st->abc, st->cap,
+        uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_ENCODE, &st->abc, st->cap,
                                       st->ncarry + 4096, &room, waiter);
         if (!in)
             return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
@@ -364,23 +381,83 @@ static int top_up_encoder(stage *st)
     return 0;
 }
 
+/* The first block of a decoder stream through the hub: a stream that
+ * ends inside it is one job (its final partial group emitted, like the
+ * reference at EOF); one that does not moves what was gathered into a
+ * session and continues on sessions.  Returns as top_up does, or 1 when
+ * the caller should launch `*moved` bytes already in sl's session. */
+static int decoder_first_via_hub(stage *st, slot *sl, size_t *moved)
+{
+    *moved = 0;
+    action_1 waiter = { st, (act_1) stage_notify };
+    size_t room;
+    uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_DECODE, &st->abc, st->cap, 4096, &room,
+                                  waiter);
+    if (!in)
+        return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
+    bool eof;
+    int uerr;
+    size_t got = gather(st, in, room, &eof, &uerr);
+    if (eof) {
+        st->final_queued = true;
+        st->hub_first = false;
+        if (got == 0) {
+            b64_hub_cancel(st->hub);
+            return 0;
+        }
+        slot_arm(st, sl);
+        sl->hubbed = true;
+        b64_hub_commit(st->hub, &sl->ticket, got, (got + 3) / 4 * 3,
+                       (action_1) { st, (act_1) stage_notify });
+        st->launched_any = true;
+        return 0;
+    }
+    if (got == 0) {
+        b64_hub_cancel(st->hub);
+        return uerr ? uerr : EAGAIN;
+    }
+    /* more than a block, or upstream paused: the session path from here */
+    st->hub_first = false;
+    if (!sl->sess && !(sl->sess = b64x_session_acquire(st->cap))) {
+        b64_hub_cancel(st->hub);
+        return -(errno ? errno : ENOMEM);
+    }
+    memcpy(b64x_session_host_in(sl->sess), in, got);
+    b64_hub_cancel(st->hub);
+    *moved = got;
+    return 1;
+}
+
 static int top_up_decoder(stage *st)
 {
     slot *sl;
     while ((sl = next_launch_slot(st))) {
+        size_t moved = 0;
+        if (st->hub_first && !st->launched_any) {
+            int rc = decoder_first_via_hub(st, sl, &moved);
+            if (rc != 1) {
+                if (rc)
+                    return rc;
+                continue;
+            }
+        }
         slot *prev = st->launched_any
                          ? &st->slots[(st->head + st->nbusy + NSLOTS - 1) %
                                       NSLOTS]
                          : NULL;
+        int frc = stage_efd(st);
+        if (frc)
+            return frc;
         if (!sl->sess) {
             sl->sess = b64x_session_acquire(st->cap);
             if (!sl->sess)
                 return -(errno ? errno : ENOMEM);
         }
-        bool eof;
-        int uerr;
-        size_t got = gather(st, b64x_session_host_in(sl->sess), st->cap, &eof,
-                            &uerr);
+        bool eof = false;
+        int uerr = 0;
+        size_t got = moved;
+        if (!moved)
+            got = gather(st, b64x_session_host_in(sl->sess), st->cap, &eof, &uerr);
         unsigned flags = B64X_DEC_HOLD_TAIL;
         if (eof) {
             st->final_queued = true;
@@ -391,6 +468,7 @@ static int top_up_decoder(stage *st)
             return uerr ? uerr : EAGAIN;
         }
         slot_arm(st, sl);
+        sl->hubbed = false;
         int rc = b64x_session_decode_async(sl->sess, got, &st->abc, flags,
                                            prev ? prev->sess : NULL, slot_done,
                                            sl);
@@ -413,6 +491,16 @@ static bool slot_ready(slot *sl)
 {
     if (sl->owner->dir == DIR_ENCODE)
         return atomic_load_explicit(&sl->ticket.done, memory_order_acquire);
+    if (sl->hubbed) {
+        if (!atomic_load_explicit(&sl->ticket.done, memory_order_acquire))
+            return false;
+        if (!sl->resolved) {
+            sl->out_len = sl->ticket.out_len;
+            sl->body_end = sl->out_len;
+            sl->resolved = true;
+        }
+        return true;
+    }
     if (!atomic_load_explicit(&sl->done, memory_order_acquire))
         return false;
     if (!sl->resolved) {
@@ -425,8 +513,8 @@ static bool slot_ready(slot *sl)
 
 static const uint8_t *slot_out(slot *sl)
 {
-    return sl->owner->dir == DIR_ENCODE ? sl->ticket.out
-                                        : b64x_session_host_out(sl->sess);
+    return sl->owner->dir == DIR_ENCODE || sl->hubbed ? sl->ticket.out
+                                                      : b64x_session_host_out(sl->sess);
 }
 
 static void retire_head(stage *st)

@@ -3611,6 +3611,45 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     return 0;
 }
 
+int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
+                           const uint64_t *h_in_off, uint8_t *h_out,
+                           const uint64_t *h_out_off, uint64_t *h_outlen,
+                           const b64x_alphabet *abc, b64x_done_fn done, void *arg)
+{
+    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off || !h_outlen)))
+        return -EINVAL;
+    int err;
+    if ((err = hip_err(hipSetDevice(l->device)))) return err;
+    if (njobs) {
+        const uint64_t in_bytes = h_in_off[njobs], out_bytes = h_out_off[njobs];
+        const uint64_t words = (uint64_t) njobs + 1;
+        if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_out, &l->out_cap, out_bytes + 64))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, 3 * words * 8))) return err;
+        uint64_t *d_in_off = l->d_offs, *d_out_off = l->d_offs + words,
+                 *d_outlen = l->d_offs + 2 * words;
+        if ((err = hip_err(hipMemcpyAsync(d_in_off, h_in_off, words * 8, hipMemcpyHostToDevice,
+                                          l->stream))) ||
+            (err = hip_err(hipMemcpyAsync(d_out_off, h_out_off, words * 8,
+                                          hipMemcpyHostToDevice, l->stream))))
+            return err;
+        if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
+                                                      hipMemcpyHostToDevice, l->stream))))
+            return err;
+        if ((err = b64x_decode_batch(in_bytes ? l->d_in : l->d_out, d_in_off, njobs, l->d_out,
+                                     d_out_off, d_outlen, abc, l->stream)))
+            return err;
+        if (out_bytes && (err = hip_err(hipMemcpyAsync(h_out, l->d_out, out_bytes,
+                                                       hipMemcpyDeviceToHost, l->stream))))
+            return err;
+        if ((err = hip_err(hipMemcpyAsync(h_outlen, d_outlen, (uint64_t) njobs * 8,
+                                          hipMemcpyDeviceToHost, l->stream))))
+            return err;
+    }
+    if (done) return hip_err(hipLaunchHostFunc(l->stream, done, arg));
+    return 0;
+}
+
 int b64x_lane_wait(b64x_lane *l)
 {
     if (!l) return -EINVAL;

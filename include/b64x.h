@@ -220,6 +220,16 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const b64x_alphabet *abc,
                            b64x_done_fn done, void *arg);
+/* Decode njobs independent, complete character buffers (each one whole
+ * stream: its final partial group is emitted): buffer i is
+ * h_in[h_in_off[i] .. h_in_off[i+1]) and decodes to h_out + h_out_off[i]
+ * (capacity h_out_off[i+1] - h_out_off[i] >= b64x_decoded_cap(len));
+ * h_outlen[i] receives its byte count.  Pinned host buffers, as for
+ * b64x_lane_encode_async. */
+int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
+                           const uint64_t *h_in_off, uint8_t *h_out,
+                           const uint64_t *h_out_off, uint64_t *h_outlen,
+                           const b64x_alphabet *abc, b64x_done_fn done, void *arg);
 /* Wait for everything queued on the lane. */
 int b64x_lane_wait(b64x_lane *l);
 

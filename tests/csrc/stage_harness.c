@@ -441,6 +441,60 @@ int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
     return err ? -1 : 0;
 }
 
+/* The ingress mirror of config 5: `nmsg` decoder stacks
+ * queuestream(encoded message) -> base64_decode (GPU) on one loop, each
+ * drained `read_size` at a time into out + out_off[i].  Short streams are
+ * decoded as jobs of shared hub batches. */
+int h_ingress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                     size_t read_size, char pos62, char pos63, uint8_t *out,
+                     const uint64_t *out_off, uint64_t *out_len, int *err_out,
+                     double *times)
+{
+    double t0 = now_s();
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    consumer *cs = calloc(nmsg ? nmsg : 1, sizeof *cs);
+    size_t live = nmsg;
+    for (size_t i = 0; i < nmsg; i++) {
+        queuestream_t *q = make_queuestream(async);
+        queuestream_enqueue_bytes(q, in + in_off[i], in_off[i + 1] - in_off[i]);
+        queuestream_terminate(q);
+        base64decoder_t *d =
+            base64_decode(async, queuestream_as_bytestream_1(q), pos62, pos63);
+        consumer *c = &cs[i];
+        c->async = async;
+        c->material = base64decoder_as_bytestream_1(d);
+        c->read_size = read_size;
+        c->out = out + out_off[i];
+        c->cap = out_off[i + 1] - out_off[i];
+        c->live = &live;
+        action_1 cb = { c, (act_1) consume };
+        bytestream_1_register_callback(c->material, cb);
+        async_execute(async, cb);
+    }
+    double t1 = now_s();
+    int rc = nmsg ? async_loop(async) : 0;
+    int err = rc < 0 ? errno : 0;
+    double t2 = now_s();
+    if (times) {
+        times[0] = t1 - t0;
+        times[1] = t2 - t1;
+    }
+    for (size_t i = 0; i < nmsg; i++) {
+        out_len[i] = cs[i].len;
+        if (!err && cs[i].err)
+            err = cs[i].err;
+        if (!cs[i].done && !err)
+            err = EPIPE;
+    }
+    destroy_async(async);
+    free(cs);
+    if (err_out)
+        *err_out = err;
+    return err ? -1 : 0;
+}
+
 /* Config 5 over `nthreads` event loops (one per thread, each with its own
  * hub): messages are split into contiguous ranges of about equal bytes.
  * times[0] = slowest thread's setup, times[1] = wall time of the loops. */

@@ -56,3 +56,30 @@ def test_decoder_stage_vs_oracle(read_size, burst):
         assert got == orc.decode_stream(dirty, 0, 0, 200), n
         if n not in (1000,):
             assert got == data
+
+
+@pytest.mark.parametrize("abc", [(-1, -1), (".", "_")])
+def test_many_short_decoder_streams_on_one_loop(abc):
+    """Short decoder streams (each ends inside its first block) are decoded
+    as jobs of shared hub batches: every stream's bytes equal the oracle's,
+    including dirty, padded-in-the-middle, ragged and empty messages."""
+    rng = np.random.default_rng(17 + len(str(abc)))
+    msgs = []
+    for i in range(700):
+        n = int(rng.integers(0, 3000)) if i % 50 else 0
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        chars = orc.encode(data, abc[0], abc[1], bool(i % 3), -1)
+        if i % 4 == 1:
+            chars = b"\r\n".join(chars[j:j + 76] for j in range(0, len(chars), 76))
+        if i % 7 == 2:
+            chars = b"QU=" + chars + b"*Q"
+        if i % 11 == 3:
+            chars = chars[:max(len(chars) - int(rng.integers(0, 4)), 0)]
+        msgs.append(chars)
+    for big in (70000, 300000):  # whole message still inside one block
+        msgs.append(orc.encode(rng.integers(0, 256, big, dtype=np.uint8).tobytes(),
+                               abc[0], abc[1], True, -1))
+    got, err = util.ingress_stacks(msgs, 200, *abc)
+    assert err == 0
+    for i, m in enumerate(msgs):
+        assert got[i] == orc.decode_stream(m, 0, 0, 200, *abc), i

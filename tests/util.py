@@ -70,6 +70,8 @@ def harness() -> ctypes.CDLL:
         L.h_egress_stacks_mt.restype = ctypes.c_int
         L.h_egress_stacks_mt_dev.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
         L.h_egress_stacks_mt_dev.restype = ctypes.c_int
+        L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
+        L.h_ingress_stacks.restype = ctypes.c_int
         L.h_device_count.argtypes = []
         L.h_device_count.restype = ctypes.c_int
         _harness = L
@@ -215,5 +217,29 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
         return None, err.value
     if raw:
         return (out, out_off, out_len), 0
+    return [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
+            for i in range(lens.size)], 0
+
+
+def ingress_stacks(msgs, read_size: int, pos62=-1, pos63=-1, times=None):
+    """Run len(msgs) GPU decoder stacks (queuestream -> base64_decode) on one
+    loop; returns (list of decoded bytes | None, errno)."""
+    lens = np.array([len(m) for m in msgs], np.uint64)
+    in_off = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(lens, out=in_off[1:])
+    src = np.frombuffer(b"".join(msgs) or b"\0", np.uint8)
+    caps = lens // 4 * 3 + 3
+    out_off = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(caps, out=out_off[1:])
+    out = np.zeros(int(out_off[-1]) or 1, np.uint8)
+    out_len = np.zeros(max(lens.size, 1), np.uint64)
+    err = ctypes.c_int(0)
+    tp = times.ctypes.data if times is not None else None
+    rc = harness().h_ingress_stacks(src.ctypes.data, in_off.ctypes.data, lens.size, read_size,
+                                    cch(pos62), cch(pos63), out.ctypes.data,
+                                    out_off.ctypes.data, out_len.ctypes.data,
+                                    ctypes.byref(err), tp)
+    if rc != 0:
+        return None, err.value
     return [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
             for i in range(lens.size)], 0
