@@ -9,7 +9,9 @@
  * Python calls these through ctypes (tests/test_stages_gpu.py).
  */
 #define _GNU_SOURCE
+#define _GNU_SOURCE
 #include <errno.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -614,4 +616,94 @@ int h_egress_stacks_mt_dev(const uint8_t *in, const uint64_t *in_off, size_t nms
     if (err_out)
         *err_out = err;
     return err ? -1 : 0;
+}
+
+/* ---- a small sampling profiler (SIGPROF, process CPU time) ---------------
+ * h_prof_start(hz) / h_prof_stop(path): a histogram of interrupted program
+ * counters, resolved with dladdr to "object symbol+offset", written as
+ * "count symbol" lines (test infrastructure: host-side profiles of the loop
+ * without perf, which the GPU image lacks). */
+#include <dlfcn.h>
+#include <signal.h>
+#include <stdatomic.h>
+#include <sys/time.h>
+#include <ucontext.h>
+
+enum { PROF_MAX = 1 << 20 };
+static uintptr_t *prof_pc;
+static atomic_size_t prof_n;
+
+static void prof_handler(int sig, siginfo_t *si, void *uc_)
+{
+    (void) sig;
+    (void) si;
+    ucontext_t *uc = uc_;
+    size_t i = atomic_fetch_add_explicit(&prof_n, 1, memory_order_relaxed);
+    if (i < PROF_MAX)
+        prof_pc[i] = (uintptr_t) uc->uc_mcontext.gregs[REG_RIP];
+}
+
+int h_prof_start(int hz)
+{
+    if (!prof_pc && !(prof_pc = malloc(PROF_MAX * sizeof *prof_pc)))
+        return -1;
+    atomic_store(&prof_n, 0);
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = prof_handler;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(SIGPROF, &sa, NULL) < 0)
+        return -1;
+    struct itimerval it = { { 0, 1000000 / hz }, { 0, 1000000 / hz } };
+    return setitimer(ITIMER_PROF, &it, NULL);
+}
+
+static int cmp_uptr(const void *a, const void *b)
+{
+    uintptr_t x = *(const uintptr_t *) a, y = *(const uintptr_t *) b;
+    return x < y ? -1 : x > y;
+}
+
+int h_prof_stop(const char *path)
+{
+    struct itimerval it;
+    memset(&it, 0, sizeof it);
+    setitimer(ITIMER_PROF, &it, NULL);
+    signal(SIGPROF, SIG_IGN);
+    size_t n = atomic_load(&prof_n);
+    if (n > PROF_MAX)
+        n = PROF_MAX;
+    /* map each pc to its symbol start, then count per symbol */
+    for (size_t i = 0; i < n; i++) {
+        Dl_info d;
+        if (dladdr((void *) prof_pc[i], &d) && d.dli_saddr && d.dli_sname)
+            prof_pc[i] = (uintptr_t) d.dli_saddr;
+    }
+    qsort(prof_pc, n, sizeof *prof_pc, cmp_uptr);
+    FILE *f = fopen(path, "w");
+    if (!f)
+        return -1;
+    fprintf(f, "%zu samples\n", n);
+    for (size_t i = 0; i < n;) {
+        size_t j = i;
+        while (j < n && prof_pc[j] == prof_pc[i])
+            j++;
+        Dl_info d;
+        const char *sym = "?", *obj = "?";
+        uintptr_t off = prof_pc[i];
+        if (dladdr((void *) prof_pc[i], &d)) {
+            if (d.dli_sname)
+                sym = d.dli_sname;
+            if (d.dli_fname)
+                obj = d.dli_fname;
+            off -= (uintptr_t) d.dli_fbase;
+        }
+        /* object-relative offset: scripts/prof_resolve.py names the
+         * static functions with nm */
+        fprintf(f, "%zu %s %s %#lx\n", j - i, obj, sym, (unsigned long) off);
+        i = j;
+    }
+    fclose(f);
+    return 0;
 }

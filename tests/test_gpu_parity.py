@@ -439,3 +439,106 @@ def test_decode_line_structured(fmt):
     assert got == want, fmt
     if fmt != "crlf76_broken":
         assert got == host.tobytes()
+
+
+def _windows_match(x, enc, starts, width=3 * 4096):
+    """enc[4k/3 ...] against the oracle's encoding of x[k ...] for windows
+    starting at the input offsets `starts` (each rounded down to a group)."""
+    n = x.numel()
+    for s in starts:
+        a = max(0, min(s, n - 1)) // 3 * 3
+        b = min(n, a + width)
+        want = orc.encode(x[a:b].cpu().numpy())
+        if b < n:  # an inner window: no padding
+            want = want[:(b - a) // 3 * 4]
+        got = enc[a // 3 * 4:a // 3 * 4 + len(want)].cpu().numpy().tobytes()
+        assert got == want, s
+
+
+@pytest.mark.slow
+def test_beyond_32bit_sizes():
+    """Maximum sizes: a 5 GiB + 5 byte buffer (6.7 GB of characters), so
+    every 32-bit byte, group and range index wraps.  Windows across the
+    2^31/2^32/2^33 offsets match the oracle; the round trip is exact; and
+    junk inserted at character offsets around 2^32 leaves the decoded
+    bytes unchanged (the decoder skips it, base64decoder.c:48-60)."""
+    n = (5 << 30) + 5
+    x = torch.empty(n, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0xB16)
+    enc = b64.encode(x)
+    assert enc.numel() == b64.encoded_len(n)
+    marks = [0, (1 << 31) - 7, (1 << 32) - 7, (1 << 32) // 4 * 3 - 7, (1 << 33) // 4 * 3 - 9,
+             n - 5000]
+    _windows_match(x, enc, marks)
+    dd = b64.decode(enc)
+    assert dd.info().out_len == n
+    assert torch.equal(dd.out[:n], x)
+    del dd
+    cuts = [(1 << 32) - 3, (1 << 32) + 1, (1 << 33) - 2]
+    junk = [torch.tensor(list(b"\r\n"), dtype=torch.uint8, device=DEV),
+            torch.full((5000,), ord("*"), dtype=torch.uint8, device=DEV),
+            torch.tensor(list(b"\x00\xff="), dtype=torch.uint8, device=DEV)]
+    pieces, prev = [], 0
+    for c, j in zip(cuts, junk):
+        pieces += [enc[prev:c], j]
+        prev = c
+    pieces.append(enc[prev:])
+    dirty = torch.cat(pieces)
+    del enc, pieces
+    dd = b64.decode(dirty)
+    assert dd.info().out_len == n
+    assert torch.equal(dd.out[:n], x)
+
+
+@pytest.mark.slow
+def test_beyond_32bit_strided_batch():
+    """A batch whose total input and output pass 4 GiB: 4,194,307 rows of
+    1,100 bytes.  Rows around the 2^32 byte offsets match the oracle and
+    the row round trip is exact."""
+    nbuf, length = (1 << 22) + 3, 1100
+    E = b64.encoded_len(length)
+    x = torch.empty(nbuf * length, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0x5EED)
+    enc = torch.empty(nbuf * E, dtype=torch.uint8, device=DEV)
+    b64.encode_strided(x, length, length, nbuf, enc, E)
+    for i in (0, (1 << 32) // length - 1, (1 << 32) // length, (1 << 32) // E,
+              (1 << 32) // E + 1, nbuf - 1):
+        row = x[i * length:(i + 1) * length].cpu().numpy()
+        assert enc[i * E:(i + 1) * E].cpu().numpy().tobytes() == orc.encode(row), i
+    cap = (b64.decoded_cap(E) + 15) // 16 * 16
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(enc, E, E, nbuf, dec, cap, outlen)
+    assert int(outlen.min()) == length and int(outlen.max()) == length
+    assert torch.equal(dec.view(nbuf, cap)[:, :length], x.view(nbuf, length))
+
+
+@pytest.mark.slow
+def test_beyond_32bit_ragged_batch():
+    """Ragged batch with a job longer than 4 GiB and offsets past 2^32:
+    windows of every job match the oracle, the round trip is exact."""
+    lens = [5, (1 << 32) + 100, 7, 3 << 29, 1000]
+    in_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    elens = [b64.encoded_len(n) for n in lens]
+    out_off = np.concatenate([[0], np.cumsum(elens)[:-1]]).astype(np.int64)
+    x = torch.empty(int(in_off[-1]), dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0xACE)
+    enc = torch.zeros(int(sum(elens)), dtype=torch.uint8, device=DEV)
+    b64.encode_batch(x, torch.from_numpy(in_off).to(DEV), enc,
+                     torch.from_numpy(out_off).to(DEV))
+    for i, n in enumerate(lens):
+        xi = x[int(in_off[i]):int(in_off[i + 1])]
+        ei = enc[int(out_off[i]):int(out_off[i]) + elens[i]]
+        _windows_match(xi, ei, [0, (1 << 31) - 4, (1 << 32) // 4 * 3 - 5, (1 << 32) - 2,
+                                n - 3000])
+    caps = [b64.decoded_cap(n) for n in elens]
+    dout_off = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+    dec = torch.empty(int(sum(caps)), dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(len(lens), dtype=torch.int64, device=DEV)
+    ein_off = np.concatenate([[0], np.cumsum(elens)]).astype(np.int64)
+    b64.decode_batch(enc, torch.from_numpy(ein_off).to(DEV), dec,
+                     torch.from_numpy(dout_off).to(DEV), outlen)
+    assert outlen.cpu().tolist() == lens
+    for i, n in enumerate(lens):
+        assert torch.equal(dec[int(dout_off[i]):int(dout_off[i]) + n],
+                           x[int(in_off[i]):int(in_off[i + 1])]), i

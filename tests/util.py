@@ -72,6 +72,8 @@ def harness() -> ctypes.CDLL:
         L.h_egress_stacks_mt_dev.restype = ctypes.c_int
         L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
         L.h_ingress_stacks.restype = ctypes.c_int
+        L.h_prof_start.argtypes = [ctypes.c_int]
+        L.h_prof_stop.argtypes = [ctypes.c_char_p]
         L.h_device_count.argtypes = []
         L.h_device_count.restype = ctypes.c_int
         _harness = L
