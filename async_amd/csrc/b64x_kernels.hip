@@ -374,11 +374,28 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // Runtime tuning knobs (scripts/bench_variants.py; not part of the public
 // ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
 // chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
-// bit 1 cached loads, any bit: not the tight/row kernels), 5 = 1: the
-// chunk-by-chunk pass 2, 6 = 1: the first-form tight/row batch kernels,
+// bit 1 cached loads, any bit: not the tight/row kernels), 5 = pass 2 of
+// the exact decode (0 bit-stream pass2d, 1 chunk-by-chunk, 2 pass2b, 3/4
+// pass2c with the register/scatter compaction), 6 = 1: the first-form
+// tight/row batch kernels,
 // 7 = lanes' slots per batch-kernel tile (2 or 4), 8 = 1: the one-block
 // decode scan (2: look-back priced out, 3: tiles by block index).
 int g_tune[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+// ASYNC_B64_TUNE="i=v,i=v": kernel-variant knobs for A/B runs of the whole
+// test suite or bench (the same knobs b64x__tune sets).
+__attribute__((constructor)) void tune_from_env()
+{
+    const char *v = getenv("ASYNC_B64_TUNE");
+    while (v && *v) {
+        char *end;
+        const long i = strtol(v, &end, 10);
+        if (*end != '=') break;
+        const long x = strtol(end + 1, &end, 10);
+        if (i >= 0 && i < 9) g_tune[i] = (int) x;
+        v = *end == ',' ? end + 1 : nullptr;
+    }
+}
 
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
@@ -1850,6 +1867,15 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2b(
 // bounds test.
 constexpr uint32_t kP2cHead = 16;
 
+// A wave-uniform 64-bit load through the scalar cache (s_load, counted by
+// lgkmcnt): a vector load of a per-range base that is then made scalar
+// forces an s_waitcnt vmcnt that also drains every store the wave issued
+// before it, once per range.  Only for data written by an earlier kernel.
+DEV uint64_t scalar_load_u64(const uint64_t *p)
+{
+    return *(const __attribute__((address_space(4))) uint64_t *) p;
+}
+
 constexpr uint32_t kP2cPhys = kP2cHead + kP2Sx + 16;  // bytes per wave
 
 // Identity (a 4-per-128-byte pad swizzle against the scatter's bank
@@ -2057,14 +2083,272 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
         c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
         c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
         uint32_t la = ld_la(r);
-        uint64_t B = w.bases[r];
+        uint64_t B = scalar_load_u64(w.bases + r);
         while (r < mid_end) {
             const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
             uint4 cn[2];
             cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
             cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
             const uint32_t lan = ld_la(rn);
-            const uint64_t Bn = w.bases[rn];
+            const uint64_t Bn = scalar_load_u64(w.bases + rn);
+            process(r, c, full, la, (uint64_t) (r + 1) * R + lane < n, B);
+            r += nw;
+            c[0] = cn[0];
+            c[1] = cn[1];
+            la = lan;
+            B = Bn;
+        }
+    }
+    for (; r < nranges; r += nw) load_generic(r);
+}
+
+// ---- pass 2, bit-stream form ----------------------------------------------
+//
+// k_decode_pass2c spends most of its ~520 VALU per range on the per-character
+// scatter of sextets into LDS, the read-back and group conversion, and the
+// realigning store (PMC).  Here the range's output is built in LDS directly
+// as the decoded BIT stream: each lane compacts every dword of its table
+// values (v_perm, selector by the dword's invalid mask), turns the 0-4
+// surviving sextets into one left-aligned 24-bit field (two v_dot4), and
+// ORs that field into the wave's zeroed LDS buffer at bit 6 x (its sextet
+// index) -- the bytes of that buffer ARE the output bytes.  The buffer is
+// laid out so that LDS byte 4 + (ob & 3) is output byte ob: its dwords map
+// onto aligned output dwords, and the store is a straight copy with byte
+// stores only for the first and last partial dwords.
+constexpr uint32_t kP2dBytes = 4 + 3 + kP2Range / 4 * 3 + 16;          // head, skew, out, slack
+constexpr uint32_t kP2dBlocks = (kP2dBytes + 15) / 16;                  // uint4 per wave
+
+struct __attribute__((aligned(16))) P2dSmem {
+    uint8_t tab[256];
+    uint32_t sel[16];
+    uint4 bits[kWavesPerBlock][kP2dBlocks];
+};
+
+DEV uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
+
+// OR a left-aligned field (bits 23..24-w of F; the rest zero) into the
+// big-endian bit stream held little-endian-per-byte in `bits` (dwords), its
+// first bit at stream bit p.
+DEV void or_field(uint32_t *bits, uint32_t p, uint32_t F)
+{
+    const uint32_t k = p >> 5, o = p & 31u;
+    const uint64_t W = (uint64_t) F << (40u - o);
+    __hip_atomic_fetch_or(bits + k, bswap32((uint32_t) (W >> 32)), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(bits + k + 1, bswap32((uint32_t) W), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// Sextets in bytes 0..3 of D (stream order; absent ones zero) -> the
+// 24-bit group s0 s1 s2 s3.
+DEV uint32_t group_dot(uint32_t D)
+{
+    const uint32_t x = __builtin_amdgcn_udot4(D, 0x00000140u, 0u, false);  // s0*64 + s1
+    const uint32_t y = __builtin_amdgcn_udot4(D, 0x01400000u, 0u, false);  // s2*64 + s3
+    return (x << 12) | y;
+}
+
+// Copy LDS bytes [lo, hi) of `b` (a wave's buffer) to dst0 + [lo, hi),
+// where dst0 = the output address of LDS byte 0 (dword aligned; bytes
+// below lo are never written).
+DEV void store_bits(const uint32_t *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t klo = (lo + 3) >> 2, khi = hi >> 2;  // whole dwords [klo, khi)
+    if (klo < khi) {
+        for (uint32_t k0 = klo + 4 * lane; k0 < khi; k0 += 256) {
+            const uint32_t d0 = b[k0], d1 = b[k0 + 1], d2 = b[k0 + 2], d3 = b[k0 + 3];
+            uint32_t *q = (uint32_t *) (dst0 + 4 * (uint64_t) k0);
+            if (k0 + 4 <= khi) {
+                *(u32x4a4 *) q = u32x4a4{d0, d1, d2, d3};
+            } else {
+                q[0] = d0;
+                if (k0 + 1 < khi) q[1] = d1;
+                if (k0 + 2 < khi) q[2] = d2;
+            }
+        }
+    }
+    // partial dwords: the head bytes [lo, 4 klo) by lane 0, the tail bytes
+    // [4 khi, hi) by lane 1 (when the range lies inside one dword, lane 0)
+    const uint8_t *bb = (const uint8_t *) b;
+    uint32_t from = 0, to = 0;
+    if (lane == 0) {
+        from = lo;
+        to = 4 * klo < hi ? 4 * klo : hi;
+    } else if (lane == 1 && klo <= khi) {
+        from = 4 * khi > lo ? 4 * khi : lo;
+        to = hi;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 3; i++)  // at most 3 bytes each
+        if (from + i < to) dst0[from + i] = bb[from + i];
+}
+
+// Inclusive prefix sum over the wave with DPP (row shifts, then the two
+// row broadcasts of gfx9): six full-rate adds instead of a ballot per bit
+// plane; x may pack independent 16-bit counts.
+DEV uint32_t wave_incl_scan_dpp(uint32_t x)
+{
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_pass2d(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
+    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
+{
+    DecodeWs w = ws_view(ws, nranges);
+    const uint64_t packed = *w.fd_cur;
+    if (packed == 0) return;
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t off0 = (uint32_t) ~packed;
+    __shared__ P2dSmem sm;
+    build_dec_table(sm.tab, a);
+    if (threadIdx.x < 16) {
+        uint32_t sel = 0x0C0C0C0Cu, k = 0;
+        for (uint32_t j = 0; j < 4; j++)
+            if (!((threadIdx.x >> j) & 1u)) {
+                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
+                k++;
+            }
+        sm.sel[threadIdx.x] = sel;
+    }
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *bq = sm.bits[wv];
+    uint32_t *bits = (uint32_t *) bq;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    auto process = [&](uint32_t r, const uint4 *c, const uint32_t *nin, uint32_t la, bool la_ok,
+                       uint64_t B) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges, first = r == r0;
+        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
+        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
+        const uint32_t skew = (uint32_t) ((uintptr_t) ob & 3);
+        const int pb0 = 8 * (4 + (int) skew);  // stream bit of relative sextet 0
+        static_assert(kP2dBlocks > 64 && kP2dBlocks <= 128, "two zeroing stores per lane");
+        bq[lane] = make_uint4(0, 0, 0, 0);
+        if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+        wave_lds_order();
+        // per dword: table values, the v_perm compaction selector (by the
+        // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
+        // non-alphabet bytes; both chunks' counts in one packed DPP scan
+        uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            lane_values(sm.tab, c[h], nin[h], P[h]);
+            uint32_t nb = 0;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
+                const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
+                sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
+                bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
+                nb += bad[h][g];
+            }
+            cnt |= (16u - nb) << (16 * h);
+        }
+        const uint32_t incl = wave_incl_scan_dpp(cnt);
+        const uint32_t ex = incl - cnt;
+        const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int before = h ? (int) (tot & 0xFFFFu) : 0;
+            uint32_t p = (uint32_t) (pb0 + 6 * (T + before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
+                or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
+                p += 24u - 6u * bad[h][g];
+            }
+        }
+        T += (int) ((tot & 0xFFFFu) + (tot >> 16));
+        bool at_end = last;
+        if (!last && T > 0 && (T & 3)) {
+            // complete the range's last group from the characters after it
+            bool ok = la_ok;
+            for (uint64_t q = re;;) {
+                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+                const bool v = t < 64u;
+                const uint64_t m = __ballot(v);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                const int need = 4 - (T & 3);
+                if (v && (int) rank < need)
+                    or_field(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
+                const int got = __popcll(m);
+                if (got >= need) {
+                    T += need;
+                    break;
+                }
+                T += got;
+                q += 64;
+                if (q >= n) {
+                    at_end = true;  // the stream's final, incomplete group
+                    break;
+                }
+                ok = q + lane < n;
+                la = ok ? in[q + lane] : 0u;
+            }
+        }
+        wave_lds_order();
+        if (T > 0) {
+            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
+            // the final partial group (emit_partial): 2 sextets -> 1 byte, 3 -> 2
+            const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
+            const uint32_t lo = 4 + skew;
+            store_bits(bits, lo, lo + 3 * ng + tail, ob - lo);
+        }
+        wave_lds_order();  // the next range re-zeroes the buffer
+    };
+    auto load_generic = [&](uint32_t r) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges, first = r == r0;
+        const uint64_t start = first ? rb + off0 : rb;
+        uint4 c[2];
+        uint32_t nin[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+        }
+        const bool la_ok = !last && re + lane < n;
+        const uint32_t la = la_ok ? in[re + lane] : 0u;
+        process(r, c, nin, la, la_ok, scalar_load_u64(w.bases + r));
+    };
+    uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
+    if (r == r0 && r < nranges) {
+        load_generic(r);
+        r += nw;
+    }
+    const uint32_t mid_end = nranges - 1;
+    if (R == 2 * kChunk && r < mid_end && (((uintptr_t) in) & 3) == 0) {
+        const uint32_t full[2] = {16u, 16u};
+        auto ld_la = [&](uint32_t rr) {
+            const uint64_t q = (uint64_t) (rr + 1) * R + lane;
+            return (uint32_t) in[q < n ? q : n - 1];
+        };
+        uint4 c[2];
+        c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
+        c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
+        uint32_t la = ld_la(r);
+        uint64_t B = scalar_load_u64(w.bases + r);
+        while (r < mid_end) {
+            const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
+            uint4 cn[2];
+            cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
+            cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
+            const uint32_t lan = ld_la(rn);
+            const uint64_t Bn = scalar_load_u64(w.bases + rn);
             process(r, c, full, la, (uint64_t) (r + 1) * R + lane < n, B);
             r += nw;
             c[0] = cn[0];
@@ -3057,9 +3341,11 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
         // grid-stride over the ranges with exactly the resident blocks (a
         // second partial round of blocks would trail the rest)
         auto k2 = g_tune[5] == 2 ? k_decode_pass2b
-                : g_tune[5] == 3 ? k_decode_pass2c<1> : k_decode_pass2c<0>;
+                : g_tune[5] == 3 ? k_decode_pass2c<1>
+                : g_tune[5] == 4 ? k_decode_pass2c<0> : k_decode_pass2d;
         static const int occ2c = occupancy_of(k_decode_pass2c<0>);
-        const int occ = g_tune[5] == 0 ? occ2c : 8;
+        static const int occ2d = occupancy_of(k_decode_pass2d);
+        const int occ = g_tune[5] == 0 ? occ2d : g_tune[5] == 4 ? occ2c : 8;
         const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ);
         hipLaunchKernelGGL(k2, dim3(b2), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,

@@ -335,7 +335,7 @@ def main():
         dom_ms = max(r["enc_ms"], r["dec_ms"])
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         knames = ["k_encode_flat"] if dom == "encode" else \
-            ["k_decode_pass1", "k_decode_scan2", "k_decode_pass2c"]
+            ["k_decode_pass1", "k_decode_scan2", "k_decode_pass2d"]
         out = {
             "metric": METRIC,
             "value": world * N * K / r["wall"] / 2**30,
