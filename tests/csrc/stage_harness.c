@@ -138,17 +138,25 @@ static void consumer_finish(consumer *c)
         async_quit_loop(c->async);
 }
 
+/* Reads `read_size` at a time straight into the destination (the way a
+ * socket writer reads into the buffer it sends from); a scratch buffer
+ * only when fewer than read_size bytes of room are left, so that an
+ * overlong stream is still detected. */
 static void consume(consumer *c)
 {
     if (c->done)
         return;
-    uint8_t *buf = malloc(c->read_size);
-    if (!buf)
-        abort();
+    uint8_t *scratch = NULL, *buf = c->out + c->len;
+    if (c->cap - c->len < c->read_size) {
+        scratch = malloc(c->read_size);
+        if (!scratch)
+            abort();
+        buf = scratch;
+    }
     ssize_t n = bytestream_1_read(c->material, buf, c->read_size);
     c->reads++;
     if (n < 0) {
-        free(buf);
+        free(scratch);
         if (errno == EAGAIN) {
             c->eagains++;
             return; /* the registered callback brings us back */
@@ -158,22 +166,24 @@ static void consume(consumer *c)
         return;
     }
     if (n == 0) {
-        free(buf);
+        free(scratch);
         consumer_finish(c);
         return;
     }
     if (c->len + (size_t) n > c->cap) {
-        free(buf);
+        free(scratch);
         c->err = ENOSPC;
         consumer_finish(c);
         return;
     }
-    memcpy(c->out + c->len, buf, (size_t) n);
+    if (scratch) {
+        memcpy(c->out + c->len, scratch, (size_t) n);
+        free(scratch);
+    }
     c->len += (size_t) n;
     if (c->counts && c->ncounts < c->max_counts)
         c->counts[c->ncounts] = n;
     c->ncounts++;
-    free(buf);
     async_execute(c->async, (action_1) { c, (act_1) consume });
 }
 
