@@ -72,6 +72,11 @@ struct b64_hub {
     size_t nwaiters, waiters_cap;
     action_1 *kicking;           /* the list hub_kick() is working through */
     size_t nkicking;
+    pthread_mutex_t post_lock;   /* guards posted: HIP callback threads push */
+    action_1 *posted;
+    size_t nposted, posted_cap;
+    action_1 *draining;          /* the posted list hub_wake() is running */
+    size_t ndraining;
     struct {                     /* ASYNC_B64_HUB_TRACE=1: printed at teardown */
         bool on;
         unsigned long batches, jobs, allocs, wake_calls, max_ready;
@@ -410,6 +415,21 @@ static void hub_wake(b64_hub *h)
     size_t n = h->nwakes;
     for (size_t i = 0; i < n; i++)
         action_1_perf(h->wakes[i]);
+    /* actions posted from other threads (session completions) */
+    pthread_mutex_lock(&h->post_lock);
+    action_1 *p = h->posted;
+    size_t np = h->nposted;
+    h->posted = NULL;
+    h->nposted = h->posted_cap = 0;
+    pthread_mutex_unlock(&h->post_lock);
+    h->draining = p;
+    h->ndraining = np;
+    for (size_t i = 0; i < np && !h->doomed; i++)
+        if (p[i].act) /* NULL: forgotten, its stage closed meanwhile */
+            action_1_perf(p[i]);
+    h->draining = NULL;
+    h->ndraining = 0;
+    free(p);
     h->in_wake = false;
     if (h->tr.on) {
         h->tr.wake_calls++;
@@ -452,6 +472,7 @@ b64_hub *b64_hub_acquire(async_t *async)
         errno = e;
         return NULL;
     }
+    pthread_mutex_init(&h->post_lock, NULL);
     h->users = 1;
     h->next_hub = registry;
     registry = h;
@@ -496,6 +517,8 @@ static void hub_destroy(b64_hub *h)
     close(h->efd);
     free(h->wakes);
     free(h->waiters);
+    free(h->posted);
+    pthread_mutex_destroy(&h->post_lock);
     free(h);
 }
 
@@ -510,8 +533,34 @@ void b64_hub_release(b64_hub *h)
         hub_destroy(h);
 }
 
+void b64_hub_post(b64_hub *h, action_1 a)
+{
+    pthread_mutex_lock(&h->post_lock);
+    if (h->nposted == h->posted_cap) {
+        size_t cap = h->posted_cap ? 2 * h->posted_cap : 64;
+        action_1 *p = realloc(h->posted, cap * sizeof *p);
+        if (!p)
+            abort();
+        h->posted = p;
+        h->posted_cap = cap;
+    }
+    h->posted[h->nposted++] = a;
+    pthread_mutex_unlock(&h->post_lock);
+    uint64_t one = 1;
+    ssize_t rc = write(h->efd, &one, sizeof one);
+    (void) rc; /* EAGAIN only when the counter is saturated: still readable */
+}
+
 void b64_hub_forget(b64_hub *h, void *obj)
 {
+    pthread_mutex_lock(&h->post_lock);
+    for (size_t i = 0; i < h->nposted; i++)
+        if (h->posted[i].obj == obj)
+            h->posted[i].act = NULL;
+    pthread_mutex_unlock(&h->post_lock);
+    for (size_t i = 0; i < h->ndraining; i++)
+        if (h->draining[i].obj == obj)
+            h->draining[i].act = NULL;
     for (size_t i = 0; i < h->nkicking; i++)
         if (h->kicking[i].obj == obj)
             h->kicking[i].act = NULL;

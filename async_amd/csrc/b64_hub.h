@@ -60,8 +60,12 @@ void b64_hub_release(b64_hub *h);
  * are always served. */
 uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
                          size_t room, size_t min_room, size_t *granted, action_1 waiter);
-/* Drop any waiter whose object is `obj` (its stage is closing). */
+/* Drop any waiter or posted action whose object is `obj` (its stage is
+ * closing). */
 void b64_hub_forget(b64_hub *h, void *obj);
+/* Any thread (a HIP host callback): perform `a` on the loop at the hub's
+ * next wake-up.  The poster must not outlive its b64_hub_forget(). */
+void b64_hub_post(b64_hub *h, action_1 a);
 /* Turn the reservation into a job of n bytes -> out_len characters
  * (encode) or of n characters -> at most out_len bytes (decode: a whole
  * stream, its final partial group emitted; the count lands in

@@ -16,9 +16,10 @@
  *              block's worth of output)
  *          --> nothing finished yet: -1 / EAGAIN.
  *
- *   GPU completion: a HIP host function marks the slot finished and writes
- *   the stage's eventfd; the eventfd is registered with async_register(),
- *   so the loop calls the stage, which calls the consumer's registered
+ *   GPU completion: a HIP host function marks the slot finished and posts
+ *   the stage on the loop's hub, whose one eventfd is registered with
+ *   async_register(), so the loop calls the stage, which calls the
+ *   consumer's registered
  *   callback -- the same "EAGAIN now, callback later" contract every
  *   bytestream_1 in the reference follows.
  *
@@ -59,7 +60,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/eventfd.h>
 #include <unistd.h>
 
 #include "async.h"
@@ -98,8 +98,9 @@ struct stage {
     b64_hub *hub;       /* the loop's batching hub */
     bool hub_first;     /* decoder: the first block may go through the hub
                            (a stream that ends inside it is one job) */
-    int efd;            /* decoder: GPU completion -> loop */
-    bool started;       /* hub / sessions + eventfd exist */
+    atomic_bool wake_posted; /* decoder: a session completion is queued
+                                on the hub for this stage */
+    bool started;       /* the hub (and any sessions) are held */
     int err;            /* sticky failure errno, 0 while healthy */
     slot slots[NSLOTS];
     unsigned head;      /* oldest busy slot */
@@ -136,7 +137,6 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
     st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
     st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
-    st->efd = -1;
     for (int i = 0; i < NSLOTS; i++)
         st->slots[i].owner = st;
 }
@@ -148,40 +148,23 @@ static ssize_t stage_fail(stage *st, int negerr)
     return -1;
 }
 
-/* Loop side of the completion eventfd. */
-static void stage_wake(stage *st)
+/* Loop side of a session completion (posted through the loop's hub: one
+ * eventfd per loop, not one per stage -- thousands of decoder streams
+ * would otherwise hold a descriptor each). */
+static void stage_posted(stage *st)
 {
-    uint64_t v;
-    while (read(st->efd, &v, sizeof v) == (ssize_t) sizeof v)
-        ;
+    atomic_store_explicit(&st->wake_posted, false, memory_order_relaxed);
     action_1_perf(st->cb);
 }
 
-/* The session path's completion eventfd, created on first use. */
-static int stage_efd(stage *st)
-{
-    if (st->efd >= 0)
-        return 0;
-    int fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    if (fd < 0)
-        return -errno;
-    if (async_register(st->async, fd, (action_1) { st, (act_1) stage_wake }) < 0) {
-        int e = errno ? errno : EIO;
-        close(fd);
-        return -e;
-    }
-    st->efd = fd;
-    return 0;
-}
-
-/* HIP runtime thread: publish, then signal. */
+/* HIP runtime thread: publish, then signal (once until the loop runs it). */
 static void slot_done(void *arg)
 {
     slot *sl = arg;
+    stage *st = sl->owner;
     atomic_store_explicit(&sl->done, 1, memory_order_release);
-    uint64_t one = 1;
-    ssize_t rc = write(sl->owner->efd, &one, sizeof one);
-    (void) rc; /* EAGAIN only when the counter is saturated: still readable */
+    if (!atomic_exchange_explicit(&st->wake_posted, true, memory_order_acq_rel))
+        b64_hub_post(st->hub, (action_1) { st, (act_1) stage_posted });
 }
 
 /* Hub completion of one of this stage's blocks (on the loop). */
@@ -213,38 +196,37 @@ static int stage_start(stage *st, size_t count)
     }
     /* A stream that ends inside its first block is decoded as one job of
      * a hub batch (many short streams, one launch); longer streams take
-     * sessions, from the process-wide pool as slots are first used, and
-     * only they need a completion eventfd (each new descriptor can cost
-     * the process an fd-table expansion: thousands of short streams on a
-     * loop must not pay that). */
+     * sessions, from the process-wide pool as slots are first used, whose
+     * completions come back through the hub's eventfd too (a descriptor
+     * per stage would cap a loop at ~1,000 decoder streams and cost
+     * fd-table expansions). */
     int rc = b64x_device_check(); /* fail loudly: no CPU path */
     if (rc)
         return rc;
     st->hub = b64_hub_acquire(st->async);
-    st->hub_first = st->hub != NULL;
+    if (!st->hub)
+        return -(errno ? errno : ENODEV);
+    st->hub_first = true;
     st->started = true;
     return 0;
 }
 
 static void stage_stop(stage *st)
 {
-    if (st->hub) {
-        b64_hub_forget(st->hub, st);
-        for (int i = 0; i < NSLOTS; i++)
-            b64_ticket_release(&st->slots[i].ticket);
-        b64_hub_release(st->hub);
-        st->hub = NULL;
-    }
+    /* sessions first: a release waits for the session's work, so no
+     * completion can be posted for this stage after the forget below */
     for (int i = 0; i < NSLOTS; i++) {
         if (st->slots[i].sess) {
             b64x_session_release(st->slots[i].sess); /* waits, then pools */
             st->slots[i].sess = NULL;
         }
     }
-    if (st->efd >= 0) {
-        (void) async_unregister(st->async, st->efd);
-        close(st->efd);
-        st->efd = -1;
+    if (st->hub) {
+        b64_hub_forget(st->hub, st);
+        for (int i = 0; i < NSLOTS; i++)
+            b64_ticket_release(&st->slots[i].ticket);
+        b64_hub_release(st->hub);
+        st->hub = NULL;
     }
     st->started = false;
 }
@@ -445,9 +427,6 @@ static int top_up_decoder(stage *st)
                          ? &st->slots[(st->head + st->nbusy + NSLOTS - 1) %
                                       NSLOTS]
                          : NULL;
-        int frc = stage_efd(st);
-        if (frc)
-            return frc;
         if (!sl->sess) {
             sl->sess = b64x_session_acquire(st->cap);
             if (!sl->sess)
@@ -624,7 +603,7 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
             return (ssize_t) n;
         }
         if (blocked) {
-            errno = EAGAIN; /* the eventfd brings the consumer back */
+            errno = EAGAIN; /* the completion brings the consumer back */
             return -1;
         }
         if (st->nbusy) { /* finished slots with nothing left to serve */

@@ -83,3 +83,18 @@ def test_many_short_decoder_streams_on_one_loop(abc):
     assert err == 0
     for i, m in enumerate(msgs):
         assert got[i] == orc.decode_stream(m, 0, 0, 200, *abc), i
+
+
+def test_many_long_decoder_streams_on_one_loop(monkeypatch):
+    """600 decoder streams that each outgrow their first block (1 KiB
+    staging, so they continue on chained sessions) on one loop: their
+    completions all come back through the loop's one hub eventfd."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", "1024")
+    rng = np.random.default_rng(23)
+    msgs = [orc.encode(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes())
+            for n in rng.integers(1500, 5000, 600)]
+    msgs[7] = b"\r\n".join(msgs[7][i:i + 76] for i in range(0, len(msgs[7]), 76))
+    got, err = util.ingress_stacks(msgs, 4096)
+    assert err == 0
+    for i, m in enumerate(msgs):
+        assert got[i] == orc.decode(m), i
