@@ -42,7 +42,7 @@ $(OBJDIR):
 $(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h | $(OBJDIR)
+$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h | $(OBJDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)

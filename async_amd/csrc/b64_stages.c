@@ -64,6 +64,7 @@
 
 #include "async.h"
 #include "b64_hub.h"
+#include "b64_lend.h"
 #include "b64x.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
@@ -111,6 +112,8 @@ struct stage {
                            since the staged output last ran out */
     uint8_t carry[2];   /* encoder: bytes of the incomplete group */
     size_t ncarry;
+    bool lend_want;     /* this read may lend instead of copy (b64_lend.h) */
+    const uint8_t *lent;/* what the last read lent, until returned */
 };
 
 static size_t env_size(const char *name, size_t dflt, size_t lo)
@@ -524,6 +527,14 @@ static size_t staged_body(stage *st, bool *blocked)
 
 static size_t serve_body(stage *st, uint8_t *dst, size_t n)
 {
+    slot *h = &st->slots[st->head];
+    if (st->lend_want && st->nbusy && h->body_end - h->out_pos >= n) {
+        /* all n in the head block: lend them; the slot stays busy (and its
+         * arena held) until the bytes are returned */
+        st->lent = slot_out(h) + h->out_pos;
+        h->out_pos += n;
+        return n;
+    }
     size_t done = 0;
     while (done < n && st->nbusy) {
         slot *sl = &st->slots[st->head];
@@ -554,8 +565,20 @@ static size_t serve_body(stage *st, uint8_t *dst, size_t n)
  * counts depend on where junk falls inside each read; no framing wrapper
  * consumes them).
  */
+/* The lent bytes are no longer used: a head block they finished retires. */
+static void stage_return(stage *st)
+{
+    if (!st->lent)
+        return;
+    st->lent = NULL;
+    slot *h = &st->slots[st->head];
+    if (st->nbusy && h->out_pos == h->out_len)
+        retire_head(st);
+}
+
 static ssize_t stage_read(stage *st, void *buf, size_t count)
 {
+    stage_return(st); /* a new read ends any loan */
     if (!count)
         return 0;
     if (st->err) {
@@ -578,6 +601,11 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
             size_t n = h->out_len - h->out_pos;
             if (n > count)
                 n = count;
+            if (st->lend_want) {
+                st->lent = slot_out(h) + h->out_pos;
+                h->out_pos += n;
+                return (ssize_t) n;
+            }
             memcpy(buf, slot_out(h) + h->out_pos, n);
             h->out_pos += n;
             if (h->out_pos == h->out_len)
@@ -622,6 +650,7 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
 
 static void stage_close(stage *st)
 {
+    st->lent = NULL;
     stage_stop(st);
     bytestream_1_close(st->up);
     async_wound(st->async, st);
@@ -697,6 +726,27 @@ static void enc_unreg_vt(void *o)
 static const struct bytestream_1_vt encoder_vt = {
     enc_read_vt, enc_close_vt, enc_reg_vt, enc_unreg_vt
 };
+
+/* b64_lend.h: zero-copy reads for wrappers in this library. */
+ssize_t b64_lend_read(bytestream_1 s, void *fallback, size_t count, const uint8_t **data)
+{
+    *data = NULL;
+    if (s.vt != &encoder_vt)
+        return bytestream_1_read(s, fallback, count);
+    stage *st = &((base64encoder_t *) s.obj)->st;
+    st->lend_want = true;
+    ssize_t n = stage_read(st, fallback, count);
+    st->lend_want = false;
+    if (n > 0)
+        *data = st->lent; /* NULL: copied into fallback */
+    return n;
+}
+
+void b64_lend_return(bytestream_1 s)
+{
+    if (s.vt == &encoder_vt)
+        stage_return(&((base64encoder_t *) s.obj)->st);
+}
 
 bytestream_1 base64encoder_as_bytestream_1(base64encoder_t *e)
 {

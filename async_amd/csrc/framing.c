@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "b64_lend.h"
 #include "blobstream.h"
 #include "chunkencoder.h"
 #include "queuestream.h"
@@ -249,6 +250,8 @@ struct chunkencoder {
     size_t max_chunk;
     chunkencoder_termination_t termination;
     uint8_t *frame;    /* CHUNK_HEAD + max_chunk (+2 for the final CRLF) */
+    const uint8_t *data; /* the chunk's data lent by a GPU encoder stage
+                            (b64_lend.h), or NULL: it is in frame */
     size_t pos, end;   /* unserved part of the current frame */
     size_t chunks;     /* frames started */
     bool last_framed;  /* the zero-length chunk has been built */
@@ -300,9 +303,15 @@ ssize_t chunkencoder_read(chunkencoder_t *c, void *buf, size_t count)
     if (!count)
         return 0;
     if (c->pos == c->end) {
+        if (c->data) { /* the lent chunk has been served */
+            b64_lend_return(c->up);
+            c->data = NULL;
+        }
         if (c->last_framed)
             return 0;
-        ssize_t n = bytestream_1_read(c->up, c->frame + CHUNK_HEAD, c->max_chunk);
+        /* same count as a read into the frame; from the GPU encoder the
+         * data usually stays where the stage has it (one copy fewer) */
+        ssize_t n = b64_lend_read(c->up, c->frame + CHUNK_HEAD, c->max_chunk, &c->data);
         if (n < 0)
             return -1;
         c->pos = chunk_header(c, (size_t) n);
@@ -327,13 +336,23 @@ ssize_t chunkencoder_read(chunkencoder_t *c, void *buf, size_t count)
     size_t n = c->end - c->pos;
     if (n > count)
         n = count;
-    memcpy(buf, c->frame + c->pos, n);
-    c->pos += n;
+    size_t done = 0;
+    if (c->data && c->pos < CHUNK_HEAD) { /* header from the frame */
+        done = CHUNK_HEAD - c->pos < n ? CHUNK_HEAD - c->pos : n;
+        memcpy(buf, c->frame + c->pos, done);
+        c->pos += done;
+    }
+    if (done < n) {
+        const uint8_t *src = c->data ? c->data - CHUNK_HEAD : c->frame;
+        memcpy((uint8_t *) buf + done, src + c->pos, n - done);
+        c->pos += n - done;
+    }
     return (ssize_t) n;
 }
 
 void chunkencoder_close(chunkencoder_t *c)
 {
+    c->data = NULL; /* the stage's close ends the loan */
     bytestream_1_close(c->up);
     free(c->frame);
     c->frame = NULL;
