@@ -2883,6 +2883,132 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix(
     }
 }
 
+// Batch fix-up, bit-stream form (k_decode_pass2d's machinery, one wave per
+// marked buffer, no cross-wave prefix): the buffer's characters are taken
+// 2,048 at a time; their sextets are OR-ed into the wave's LDS window as a
+// bit stream; whole dwords are flushed to the output and the partial last
+// dword moves to the window front.  A buffer of V alphabet characters
+// yields floor(6V/8) bytes -- the reference's final partial group rule
+// (emit_partial) falls out of the bit count.
+// First-step characters of a buffer (chunks 0 and 1 of lane `lane`).
+DEV void buf_first_chunks(const uint8_t *src, uint64_t len, uint4 c[2])
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint64_t q = (uint64_t) h * kChunk + 16 * lane;
+        const uint32_t nin = q >= len ? 0u : (len - q >= 16 ? 16u : (uint32_t) (len - q));
+        c[h] = nin ? load_chars(src + q, nin) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+DEV uint64_t decode_buf_bits(const P2dSmem &sm, uint4 *bq, const uint8_t *src, uint64_t len,
+                             uint8_t *dst, const uint4 first[2])
+{
+    const uint32_t lane = lane_id();
+    uint32_t *bits = (uint32_t *) bq;
+    const uint32_t skew = (uint32_t) ((uintptr_t) dst & 3);
+    uint32_t lo = 4 + skew;   // LDS byte of output byte `done`
+    uint32_t pb = 8 * lo;     // next free bit of the window
+    uint64_t done = 0, V = 0;
+    bq[lane] = make_uint4(0, 0, 0, 0);
+    if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+    wave_lds_order();
+    for (uint64_t p = 0;; p += 2 * kChunk) {
+        uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t q = p + (uint64_t) h * kChunk + 16 * lane;
+            const uint32_t nin = q >= len ? 0u : (len - q >= 16 ? 16u : (uint32_t) (len - q));
+            const uint4 c = p == 0 ? first[h]
+                          : nin ? load_chars(src + q, nin) : make_uint4(0, 0, 0, 0);
+            lane_values(sm.tab, c, nin, P[h]);
+            uint32_t nb = 0;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
+                const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
+                sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
+                bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
+                nb += bad[h][g];
+            }
+            cnt |= (16u - nb) << (16 * h);
+        }
+        const uint32_t incl = wave_incl_scan_dpp(cnt);
+        const uint32_t ex = incl - cnt;
+        const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+        const uint32_t t0 = tot & 0xFFFFu, t1 = tot >> 16;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            uint32_t q = pb + 6u * ((h ? t0 : 0u) + ((ex >> (16 * h)) & 0xFFFFu));
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                or_field(bits, q, group_dot(__builtin_amdgcn_perm(0u, P[h][g], sel[h][g])));
+                q += 24u - 6u * bad[h][g];
+            }
+        }
+        pb += 6u * (t0 + t1);
+        V += t0 + t1;
+        wave_lds_order();
+        const bool last = p + 2 * kChunk >= len;
+        if (last) {
+            store_bits(bits, lo, pb >> 3, dst + done - lo);
+            break;
+        }
+        // flush the whole dwords; the partial one becomes dword 1
+        const uint32_t kcut = (pb >> 3) & ~3u;
+        store_bits(bits, lo, kcut, dst + done - lo);
+        done += kcut - lo;
+        const uint32_t keep = bits[kcut >> 2];
+        wave_lds_order();
+        bq[lane] = make_uint4(0, 0, 0, 0);
+        if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+        wave_lds_order();
+        if (lane == 0) bits[1] = keep;
+        wave_lds_order();
+        pb -= 8 * (kcut - 4);
+        lo = 4;
+    }
+    wave_lds_order();  // the next buffer re-zeroes the window
+    return V;
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
+    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
+{
+    __shared__ P2dSmem sm;
+    build_dec_table(sm.tab, a);
+    if (threadIdx.x < 16) {
+        uint32_t sel = 0x0C0C0C0Cu, k = 0;
+        for (uint32_t j = 0; j < 4; j++)
+            if (!((threadIdx.x >> j) & 1u)) {
+                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
+                k++;
+            }
+        sm.sel[threadIdx.x] = sel;
+    }
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
+    for (uint64_t base = ((uint64_t) blockIdx.x * kWavesPerBlock + wv) * 64; base < nbuf;
+         base += nw * 64) {
+        const uint64_t bl = base + lane;
+        uint64_t m = __ballot(bl < nbuf && outlen[bl] == kNeedsExact);
+        while (m) {
+            const uint32_t b = (uint32_t) (base + __ffsll((unsigned long long) m) - 1);
+            m &= m - 1;
+            uint64_t beg, len, obeg;
+            batch_buf(L, b, beg, len, obeg);
+            uint4 c[2];
+            buf_first_chunks(in + beg, len, c);
+            const uint64_t V = decode_buf_bits(sm, sm.bits[wv], in + beg, len, out + obeg, c);
+            if (lane == 0) outlen[b] = V * 6 / 8;
+        }
+    }
+}
+
 // ------------------------------------------------------------ utilities --
 
 __global__ __launch_bounds__(kThreads) void k_fill_splitmix64(
@@ -3378,7 +3504,7 @@ static int launch_batch_decode(const void *d_in, const BatchLayout &L, uint32_t 
     // all it does.
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(k_decode_batch_fix, dim3(fgrid), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(g_tune[5] == 4 ? k_decode_batch_fix : k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }
@@ -3487,7 +3613,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     }
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(k_decode_batch_fix, dim3(fgrid), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(g_tune[5] == 4 ? k_decode_batch_fix : k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }
@@ -3730,13 +3856,22 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
                                            s->stream))))
         return err;
     if (carry_from) {
-        // The H2D above overlaps carry_from's kernels; the prefix waits.
-        if ((err = hip_err(hipStreamWaitEvent(s->stream, carry_from->decoded, 0)))) return err;
+        // The carry is spelled on carry_from's stream, right after the decode
+        // that produced it, so carry_from's next decode (which overwrites its
+        // result) is ordered after the read by stream order; this session
+        // waits for the spelling.  (Spelled on this stream instead, behind an
+        // event, the read could lose the race against carry_from's next
+        // decode when many streams share the hardware queues.)  The prefix
+        // it writes lies in front of d_in, so it overlaps the H2D above.
         const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
         const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
-        hipLaunchKernelGGL(k_spell_carry, dim3(1), dim3(64), 0, s->stream,
+        if ((err = hip_err(hipSetDevice(carry_from->device)))) return err;
+        hipLaunchKernelGGL(k_spell_carry, dim3(1), dim3(64), 0, carry_from->stream,
                            carry_from->d_res, s->d_in - kCarryHead, p62, p63, skip_char(abc));
         if ((err = launch_status())) return err;
+        if ((err = hip_err(hipEventRecord(carry_from->decoded, carry_from->stream)))) return err;
+        if ((err = hip_err(hipSetDevice(s->device)))) return err;
+        if ((err = hip_err(hipStreamWaitEvent(s->stream, carry_from->decoded, 0)))) return err;
         src -= kCarryHead;
         len += kCarryHead;
     }

@@ -175,10 +175,12 @@ int b64x_session_encode_async(b64x_session *s, uint64_t n,
                               void *arg);
 /* carry_from (NULL = none): another session on the same device whose last
  * call was a decode with B64X_DEC_HOLD_TAIL.  The sextets it held back are
- * prepended on the device, ordered by a HIP event, so a stream of blocks
- * can be queued before the previous block's result reaches the host.
- * Alternate two sessions (A, B, A, ...) each naming the other: a session's
- * next call is then ordered after the chained call that read its result.
+ * prepended on the device, so a stream of blocks can be queued before the
+ * previous block's result reaches the host: a one-wave kernel on
+ * carry_from's stream spells them in front of this session's input, and
+ * this session waits for it with a HIP event.  carry_from's next call is
+ * ordered after that read by its own stream order, so any number of
+ * sessions can be chained round-robin.
  * n == 0 with carry_from flushes the carried sextets alone. */
 int b64x_session_decode_async(b64x_session *s, uint64_t n,
                               const b64x_alphabet *abc, unsigned flags,
