@@ -2563,7 +2563,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
 // is exec-masked.  The last slot of a row over-reads into the next row's
 // characters and over-writes past out_len inside its own row (those bytes
 // are unspecified, include/b64x.h); its length follows the prefix rule.
-// A lane that is not clean marks the row for k_decode_batch_fix, which
+// A lane that is not clean marks the row for the fix-up, which
 // rewrites it exactly.  The caller excludes the last row (its last slot
 // could read past the input) and runs it through k_decode_slots.
 template <int U, bool GUARD>
@@ -2611,12 +2611,19 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(
         }
         uint32_t o0, o1, o2;
         groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-        if (!GUARD || t < nslots) {
+        // one junk mark per row and wave (as in k_decode_rows2)
+        const bool live = !GUARD || t < nslots;
+        const uint64_t junk = __ballot(live && !ok);
+        const uint32_t ln = lane_id();
+        const uint32_t rs = q < ln ? ln - (uint32_t) q : 0u;
+        const bool marker =
+            (uint32_t) __ffsll((unsigned long long) (junk & (~0ull << rs))) - 1 == ln;
+        if (live) {
             __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
                                         (u32x3a4 *) (out + bb[u] * out_stride + 12ull * q));
-            if (!ok)
-                atomicMax(&outlen[bb[u]], (unsigned long long) kNeedsExact);
-            else if (last)
+            if (!ok) {
+                if (marker) atomicMax(&outlen[bb[u]], (unsigned long long) kNeedsExact);
+            } else if (last)
                 atomicMax(&outlen[bb[u]], (unsigned long long) ((16ull * q + k) * 6 / 8));
         }
     }
@@ -2769,11 +2776,20 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows2(
         __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
                                     (u32x3a4 *) (ob + (uint64_t) bl[u] * out_stride + 12 * q));
         unsigned long long *ol = olb + bl[u];
+        // A row's slots sit on consecutive lanes (its first here at lane -
+        // q, or lane 0): only the first junk slot of each row in the wave
+        // marks it -- on MIME-formatted rows (CRLF every 76) that is one
+        // atomic per row and wave instead of one per junk slot.
+        const uint64_t junk = __ballot(!ok);
+        const uint32_t ln = lane_id();
+        const uint32_t rs = q < ln ? ln - q : 0u;
+        const uint64_t row_junk = junk & (~0ull << rs);
+        const bool marker = !ok && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln;
         if (PRICE & 1) {  // benchmark-only pricing of the atomics (racy)
             if (!ok) *ol = kNeedsExact;
             else if (last) *ol = (16ull * q + k) * 6 / 8;
         } else if (!ok) {
-            atomicMax(ol, (unsigned long long) kNeedsExact);
+            if (marker) atomicMax(ol, (unsigned long long) kNeedsExact);
         } else if (last) {
             atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
         }
