@@ -55,11 +55,9 @@ namespace {
 constexpr int kThreads = 256;  // 4 waves of 64
 constexpr int kWavesPerBlock = kThreads / 64;
 constexpr int kChunk = 1024;            // characters per wave step
-constexpr int kSxBytes = 1088;          // per-wave sextet scratch in LDS
 constexpr uint32_t kMaxRanges = 1u << 20; // decode ranges (waves) per call
 constexpr uint64_t kRangeChunks = 2;    // default decode range: 2 KiB
 constexpr int kEncUnroll = 4;           // quads in flight per lane
-constexpr int kDecUnroll = 4;           // chunks in flight per wave
 
 typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -375,11 +373,10 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
 // chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
 // bit 1 cached loads, any bit: not the tight/row kernels), 5 = pass 2 of
-// the exact decode (0 bit-stream pass2d, 1 chunk-by-chunk, 2 pass2b, 3/4
-// pass2c with the register/scatter compaction), 6 = 1: the first-form
-// tight/row batch kernels,
-// 7 = lanes' slots per batch-kernel tile (2 or 4), 8 = 1: the one-block
-// decode scan (2: look-back priced out, 3: tiles by block index).
+// the exact decode (0: bit-stream pass2d, 4: pass2c, the per-character
+// scatter), 6 = 1: the first-form tight/row batch kernels, 7 = lanes'
+// slots per batch-kernel tile (2 or 4), 8 = decode scan (2: look-back
+// priced out, 3: tiles by block index).
 int g_tune[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 // ASYNC_B64_TUNE="i=v,i=v": kernel-variant knobs for A/B runs of the whole
@@ -822,25 +819,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_ragged(
 
 // ----------------------------------------------------------- decode core --
 
-struct __attribute__((aligned(16))) DecSmem {
-    uint8_t tab[256];
-    uint8_t sx[kWavesPerBlock][kSxBytes];
-};
-
 DEV uint32_t lane_id() { return threadIdx.x & 63; }
-
-DEV uint32_t wave_excl_scan(uint32_t x, uint32_t *total)
-{
-    const uint32_t lane = lane_id();
-    uint32_t v = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t) d) v += y;
-    }
-    *total = __shfl(v, 63, 64);
-    return v - x;
-}
 
 // Keep the compiler from moving LDS accesses across this point.  Within
 // one wave the LDS executes DS instructions in issue order, so program
@@ -964,58 +943,6 @@ DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
     lc.vmask = m;
 }
 
-DEV uint32_t sextet(const LaneChunk &lc, int k)
-{
-    return (lc.G[k >> 2] >> (18 - 6 * (k & 3))) & 63u;
-}
-
-struct RangeState {
-    int carry;        // sextets waiting in sx[0..carry); < 0: still to skip
-    uint64_t groups;  // whole groups emitted (3 bytes each) from `out`
-    uint64_t valid;   // alphabet characters seen in the range
-};
-
-// Exact path for one chunk: compact, emit whole groups, keep the rest.
-DEV void exact_chunk(uint8_t *sx, uint8_t *out, const LaneChunk &lc, RangeState &st)
-{
-    const uint32_t lane = lane_id();
-    uint32_t cnt = __popc(lc.vmask), total;
-    uint32_t excl = wave_excl_scan(cnt, &total);
-    int idx = st.carry + (int) excl;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        if ((lc.vmask >> k) & 1u) {
-            if (idx >= 0) sx[idx] = (uint8_t) sextet(lc, k);
-            idx++;
-        }
-    }
-    wave_lds_order();
-    st.valid += total;
-    int T = st.carry + (int) total;
-    if (T >= 4) {
-        uint32_t ng = (uint32_t) T >> 2;
-        uint32_t nlanes = (ng + 3) >> 2;
-        if (lane < nlanes) {
-            uint4 sv = *(const uint4 *) (sx + 16 * lane);
-            uint32_t o0, o1, o2;
-            groups_to_bytes(group_of_bytes(sv.x), group_of_bytes(sv.y),
-                            group_of_bytes(sv.z), group_of_bytes(sv.w), o0, o1, o2);
-            uint32_t gl = ng - 4 * lane;
-            store_bytes12(out + 3 * st.groups + 12 * lane, o0, o1, o2,
-                          3 * (gl < 4 ? gl : 4));
-        }
-        wave_lds_order();
-        int nc = T - 4 * (int) ng;
-        if (lane == 0)
-            for (int j = 0; j < nc; j++) sx[j] = sx[4 * ng + j];
-        wave_lds_order();
-        st.groups += ng;
-        st.carry = nc;
-    } else {
-        st.carry = T;  // sextets (if any) already sit at sx[0..T)
-    }
-}
-
 // Emit the final, incomplete group (1..3 sextets at sx[0..r)):
 // floor(6r/8) bytes, exactly what the reference's accumulator has produced
 // when its upstream reaches EOF (src/base64decoder.c:59-62,71-76).
@@ -1080,86 +1007,6 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
         store_bytes12(out + 12 * lane, o0, o1, o2, nbytes);
     }
     return (int) (16 * f + __shfl(k, (int) f, 64));
-}
-
-// Exact decode of characters [start, re) of the stream in[0..n).  The
-// first `skip` (0..3) alphabet characters complete a group owned by an
-// earlier range and are not emitted.  `out` receives the first group owned
-// here.  Unless `is_last`, the final group is completed with up to 3
-// alphabet characters read past `re` (lookahead).  With `hold` the
-// stream's final incomplete group is not emitted.
-// Returns the number of alphabet characters in [start, re).
-DEV uint64_t decode_range(const uint8_t *tab, uint8_t *sx, const uint8_t *in,
-                          uint64_t n, uint64_t start, uint64_t re, int skip,
-                          uint8_t *out, bool is_last, bool hold)
-{
-    const uint32_t lane = lane_id();
-    RangeState st{-skip, 0, 0};
-    for (uint64_t pos = start; pos < re; pos += (uint64_t) kChunk * kDecUnroll) {
-        uint4 w[kDecUnroll];
-        uint32_t nin[kDecUnroll];
-#pragma unroll
-        for (int u = 0; u < kDecUnroll; u++) {
-            uint64_t p = pos + (uint64_t) u * kChunk + 16 * lane;
-            nin[u] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            w[u] = nin[u] ? load_chars(in + p, nin[u]) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < kDecUnroll; u++) {
-            const uint64_t cpos = pos + (uint64_t) u * kChunk;
-            if (cpos >= re) break;
-            if (st.carry == 0) {
-                uint32_t G[4], bad;
-                map_fast(tab, w[u], nin[u], G, bad);
-                if (__all(bad == 0)) {
-                    emit_full(G, out + 3 * st.groups);
-                    st.groups += kChunk / 4;
-                    st.valid += kChunk;
-                    continue;
-                }
-            }
-            LaneChunk lc;
-            map_chunk_lds(tab, w[u], nin[u], lc);
-            if (st.carry == 0 && is_last && cpos + kChunk >= re) {
-                int got = fast_prefix(lc, hold, out + 3 * st.groups);
-                if (got >= 0) {
-                    st.valid += (uint32_t) got;
-                    continue;  // the stream ends here
-                }
-            }
-            exact_chunk(sx, out, lc, st);
-        }
-    }
-    int r = st.carry;
-    if (!is_last && r > 0) {
-        // Complete the last group from the characters that follow.
-        for (uint64_t q = re; r < 4 && q < n; q += 64) {
-            uint64_t p = q + lane;
-            uint32_t t = p < n ? tab[in[p]] : 0xFFu;
-            bool v = t < 64u;
-            uint64_t m = __ballot(v);
-            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32),
-                            __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-            if (v && (int) rank < 4 - r) sx[r + rank] = (uint8_t) t;
-            int got = __popcll(m);
-            r = r + got > 4 ? 4 : r + got;
-        }
-        wave_lds_order();
-        if (r == 4) {
-            if (lane == 0) {
-                uint32_t G = ((uint32_t) sx[0] << 18) | ((uint32_t) sx[1] << 12) |
-                             ((uint32_t) sx[2] << 6) | sx[3];
-                uint8_t *d = out + 3 * st.groups;
-                d[0] = (uint8_t) (G >> 16);
-                d[1] = (uint8_t) (G >> 8);
-                d[2] = (uint8_t) G;
-            }
-            return st.valid;
-        }
-        // Ran into the end of the stream: this is the final group.
-    }
-    if (r > 0 && !hold) emit_partial(sx, out + 3 * st.groups, r);
-    return st.valid;
 }
 
 // Decode workspace: b64x_decode_workspace_size() bytes, zero-filled before
@@ -1376,82 +1223,6 @@ void k_decode_pass1(
     }
 }
 
-// One block: take (and re-arm) the first-dirty record, compute V and the
-// result record; on a dirty call also the true base of every range from
-// the first dirty one on.  Then the stream's last V mod 4 sextets (for
-// B64X_DEC_HOLD_TAIL callers), scanning backwards.
-__global__ __launch_bounds__(1024) void k_decode_scan(
-    const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
-    DecAlpha a, void *ws, b64x_dec_result *res, uint32_t hold)
-{
-    __shared__ uint8_t tab[256];
-    __shared__ uint64_t wtot[16];
-    build_dec_table(tab, a);
-    DecodeWs w = ws_view(ws, nranges);
-    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    const uint64_t packed = *w.fd;
-    __syncthreads();  // every thread has read fd before it is re-armed
-    uint64_t V;
-    if (packed == 0) {
-        // all ranges but the last were all alphabet
-        V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
-    } else {
-        const uint32_t r0 = (uint32_t) (~packed >> 32);
-        const uint32_t span = nranges - r0;
-        const uint32_t per = (span + 1023) / 1024;
-        const uint32_t q0 = r0 + threadIdx.x * per;
-        uint64_t sum = 0;
-        for (uint32_t i = 0; i < per; i++)
-            if (q0 + i < nranges) sum += w.counts[q0 + i];
-        uint64_t x = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= (uint32_t) d) x += y;
-        }
-        if (lane == 63) wtot[wave] = x;
-        __syncthreads();
-        uint64_t before = 0, tot = 0;
-        for (uint32_t i = 0; i < 16; i++) {
-            if (i < wave) before += wtot[i];
-            tot += wtot[i];
-        }
-        uint64_t run = (uint64_t) r0 * R + before + x - sum;
-        for (uint32_t i = 0; i < per; i++) {
-            if (q0 + i >= nranges) break;
-            w.bases[q0 + i] = run;
-            run += w.counts[q0 + i];
-        }
-        V = (uint64_t) r0 * R + tot;
-    }
-    if (threadIdx.x == 0) {
-        *w.fd_cur = packed;
-        *w.fd = 0;
-        res->valid = V;
-        res->tail_n = (uint32_t) (V & 3);
-        res->out_len = hold ? V / 4 * 3 : V * 6 / 8;
-    }
-    if (wave == 0) {
-        int need = (int) (V & 3);
-        uint8_t got[4] = {0, 0, 0, 0};
-        uint64_t end = n;
-        while (need > 0 && end > 0) {
-            uint64_t beg = end >= 64 ? end - 64 : 0;
-            uint64_t p = beg + lane;
-            uint32_t t = p < end ? tab[in[p]] : 0xFFu;
-            uint64_t bm = __ballot(t < 64u);
-            while (need > 0 && bm) {
-                int hi = 63 - __clzll(bm);
-                got[--need] = (uint8_t) __shfl(t, hi, 64);
-                bm &= ~(1ull << hi);
-            }
-            end = beg;
-        }
-        if (lane == 0)
-            for (int j = 0; j < 4; j++) res->tail[j] = got[j];
-    }
-}
-
 // The stream's last V mod 4 alphabet characters (as sextets) into
 // res->tail, scanning backwards from the end; one wave.
 DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, uint64_t V,
@@ -1523,7 +1294,7 @@ DEV uint64_t st_load(uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Scan, device-wide (replaces the one-block k_decode_scan), one block per
+// Scan, device-wide (it replaced a one-block scan: 2.3 ms dirty), one block per
 // tile of 1024 ranges.  Clean call (no first-dirty record): block 0 alone
 // computes V from the last range's count and the result record; every
 // other block returns at once.  Dirty call: a single-pass scan of
@@ -1647,60 +1418,14 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     }
 }
 
-// Pass 2: exact decode from the first dirty chunk on (grid-stride over
-// ranges; returns at once on a clean call).  The first dirty range resumes
-// at its dirty chunk -- everything before it was alphabet and is already
-// final; every later range re-runs with its true base.
-__global__ __launch_bounds__(kThreads) void k_decode_pass2(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
-{
-    DecodeWs w = ws_view(ws, nranges);
-    const uint64_t packed = *w.fd_cur;
-    if (packed == 0) return;
-    const uint32_t r0 = (uint32_t) (~packed >> 32);
-    const uint32_t off0 = (uint32_t) ~packed;
-    __shared__ DecSmem sm;
-    build_dec_table(sm.tab, a);
-    __syncthreads();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
-        const uint64_t rb = (uint64_t) r * R;
-        const uint64_t re = rb + R < n ? rb + R : n;
-        const uint64_t B = w.bases[r];
-        const bool last = r + 1 == nranges;
-        if (r == r0) {
-            decode_range(sm.tab, sm.sx[wv], in, n, rb + off0, re, 0,
-                         out + (B + off0) / 4 * 3, last, hold != 0);
-        } else {
-            const int skip = (int) ((4 - (B & 3)) & 3);
-            decode_range(sm.tab, sm.sx[wv], in, n, rb, re, skip, out + (B + 3) / 4 * 3,
-                         last, hold != 0);
-        }
-    }
-}
-
-// ---- pass 2, one-shot per range (ranges of at most kP2Range characters) --
+// ---- pass 2: shared pieces ----------------------------------------------
 //
-// k_decode_pass2 works chunk by chunk with a carry through LDS, a 6-step
-// __shfl_up scan, three wave fences per chunk and a dependent lookahead
-// load at the end of every range, on 4 waves per SIMD: latency-bound on
-// input that is dirty everywhere (CRLF-76).  This version issues all of a
-// range's loads at once (its base, both chunks, 64 lookahead bytes),
-// prefix-sums with ballot bit planes, compacts the whole range's sextets
-// into the wave's LDS buffer, converts them to bytes in LDS and stores the
-// bytes with dword stores realigned to the output (v_alignbyte), one
-// fence per stage.
+// Ranges of kP2Range characters; both pass-2 forms issue all of a range's
+// loads at once (its base, both chunks, 64 lookahead bytes) and, for the
+// middle ranges, the next range's before processing this one.
 constexpr uint32_t kP2Range = 2048;
 constexpr uint32_t kP2Sx = kP2Range + 64;        // + lookahead, 16-aligned
 constexpr uint32_t kP2Bb = kP2Range / 4 * 3 + 64;
-
-struct __attribute__((aligned(16))) P2Smem {
-    uint8_t tab[256];
-    uint8_t sx[kWavesPerBlock][kP2Sx];
-    uint32_t bb[kWavesPerBlock][kP2Bb / 4];
-};
 
 // Exclusive prefix over the wave of x < 32, and the total: one ballot per
 // bit plane, no LDS traffic.
@@ -1754,111 +1479,9 @@ DEV void store_realigned(const uint32_t *bb, uint32_t nb, uint8_t *dst)
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_decode_pass2b(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
-{
-    DecodeWs w = ws_view(ws, nranges);
-    const uint64_t packed = *w.fd_cur;
-    if (packed == 0) return;
-    const uint32_t r0 = (uint32_t) (~packed >> 32);
-    const uint32_t off0 = (uint32_t) ~packed;
-    __shared__ P2Smem sm;
-    build_dec_table(sm.tab, a);
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *sx = sm.sx[wv];
-    uint32_t *bb = sm.bb[wv];
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv; r < nranges; r += nw) {
-        const uint64_t rb = (uint64_t) r * R;
-        const uint64_t re = rb + R < n ? rb + R : n;
-        const bool last = r + 1 == nranges, first = r == r0;
-        const uint64_t start = first ? rb + off0 : rb;
-        // every load of the range up front
-        const uint64_t B = w.bases[r];
-        uint4 c[2];
-        uint32_t nin[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
-        }
-        const bool la_ok = !last && re + lane < n;
-        uint32_t la = la_ok ? in[re + lane] : 0u;
-        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
-        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            LaneChunk lc;
-            map_chunk_lds(sm.tab, c[h], nin[h], lc);
-            uint32_t tot;
-            const uint32_t ex = wave_scan_small(__popc(lc.vmask), tot);
-            int pos = T + (int) ex;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if ((lc.vmask >> k) & 1u) {
-                    if (pos >= 0) sx[pos] = (uint8_t) sextet(lc, k);
-                    pos++;
-                }
-            }
-            T += (int) tot;
-        }
-        bool at_end = last;
-        if (!last && T > 0 && (T & 3)) {
-            // complete the range's last group from the characters after it
-            bool ok = la_ok;
-            for (uint64_t q = re;;) {
-                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
-                const bool v = t < 64u;
-                const uint64_t m = __ballot(v);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                const int need = 4 - (T & 3);
-                if (v && (int) rank < need) sx[T + rank] = (uint8_t) t;
-                const int got = __popcll(m);
-                if (got >= need) {
-                    T += need;
-                    break;
-                }
-                T += got;
-                q += 64;
-                if (q >= n) {
-                    at_end = true;  // the stream's final, incomplete group
-                    break;
-                }
-                ok = q + lane < n;
-                la = ok ? in[q + lane] : 0u;
-            }
-        }
-        wave_lds_order();
-        if (T > 0) {
-            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
-            for (uint32_t L = lane; 4 * L < ng; L += 64) {
-                const uint4 sv = *(const uint4 *) (sx + 16 * L);
-                uint32_t o0, o1, o2;
-                groups_to_bytes(group_of_bytes(sv.x), group_of_bytes(sv.y),
-                                group_of_bytes(sv.z), group_of_bytes(sv.w), o0, o1, o2);
-                bb[3 * L] = o0;
-                bb[3 * L + 1] = o1;
-                bb[3 * L + 2] = o2;
-            }
-            wave_lds_order();
-            store_realigned(bb, 3 * ng, ob);
-            if (rem && at_end && !hold) emit_partial(sx + 4 * ng, ob + 3 * ng, (int) rem);
-        }
-        wave_lds_order();  // the next range reuses sx and bb
-    }
-}
-
-// ---- pass 2, one-shot per range, scatter form ----------------------------
+// ---- pass 2, scatter form (the previous default; ASYNC_B64_TUNE=5=4) -----
 //
-// k_decode_pass2b spends ~700 VALU per 2 KiB range (PMC), most of it in
-// map_chunk (per character: a compare pair, two selects and two shift-ors
-// to build zeroed groups and a valid mask) and in a branchy per-character
-// scatter.  Here a lane's 16 table values are packed as bytes (the value
+// A lane's 16 table values are packed as bytes (the value
 // of an alphabet character *is* its sextet; 0xFF otherwise), its valid
 // count is 16 - popc(P & 0x80808080) per dword, and the scatter is
 // branch-free: every character is written, the non-alphabet ones to a
@@ -1884,7 +1507,6 @@ DEV uint32_t swz(uint32_t p) { return p; }
 
 struct __attribute__((aligned(16))) P2cSmem {
     uint8_t tab[256];
-    uint32_t sel[16];  // v_perm selector compacting a dword's alphabet bytes, by invalid mask
     uint8_t sx[kWavesPerBlock][kP2cPhys];
     uint32_t bb[kWavesPerBlock][kP2Bb / 4];
 };
@@ -1917,14 +1539,9 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
 }
 
-// SCAT = 1 (measured a little slower, kept for A/B): each dword's alphabet
-// bytes are compacted in the register with
-// one v_perm (selector from a 16-entry table by the dword's invalid mask,
-// computed with a multiply that gathers the four bit-7s) and written with
-// byte stores at immediate offsets from one per-dword address, each
-// predicated on its index < the dword's count; 0: one store per character,
-// the non-alphabet ones to a dummy byte.
-template <int SCAT>
+// One store per character, the non-alphabet ones to a dummy byte (a
+// per-dword v_perm compaction with predicated byte stores measured a
+// little slower).
 __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
@@ -1936,15 +1553,6 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
     const uint32_t off0 = (uint32_t) ~packed;
     __shared__ P2cSmem sm;
     build_dec_table(sm.tab, a);
-    if (threadIdx.x < 16) {
-        uint32_t sel = 0x0C0C0C0Cu, k = 0;
-        for (uint32_t j = 0; j < 4; j++)
-            if (!((threadIdx.x >> j) & 1u)) {
-                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
-                k++;
-            }
-        sm.sel[threadIdx.x] = sel;
-    }
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1969,30 +1577,14 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2c(
             uint32_t tot;
             const uint32_t ex = wave_scan_small(lane_valid_count(P), tot);
             uint32_t cur = (uint32_t) ((int) kP2cHead + T + (int) ex);
-            if (SCAT) {
 #pragma unroll
-                for (uint32_t g = 0; g < 4; g++) {
-                    const uint32_t inv = P[g] & 0x80808080u;
-                    const uint32_t m = ((inv >> 7) * 0x01020408u) >> 24;  // bit j: byte j bad
-                    const uint32_t c = 4u - __popc(inv);
-                    const uint32_t D = __builtin_amdgcn_perm(0u, P[g], sm.sel[m & 15u]);
-                    uint8_t *q = sxh + cur;
-                    if (c > 0) q[0] = (uint8_t) D;
-                    if (c > 1) q[1] = (uint8_t) (D >> 8);
-                    if (c > 2) q[2] = (uint8_t) (D >> 16);
-                    if (c > 3) q[3] = (uint8_t) (D >> 24);
-                    cur += c;
-                }
-            } else {
+            for (uint32_t g = 0; g < 4; g++) {
 #pragma unroll
-                for (uint32_t g = 0; g < 4; g++) {
-#pragma unroll
-                    for (uint32_t j = 0; j < 4; j++) {
-                        const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
-                        const bool ok = b < 64u;
-                        sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
-                        cur += ok ? 1u : 0u;
-                    }
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
+                    const bool ok = b < 64u;
+                    sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
+                    cur += ok ? 1u : 0u;
                 }
             }
             T += (int) tot;
@@ -2124,6 +1716,21 @@ struct __attribute__((aligned(16))) P2dSmem {
     uint4 bits[kWavesPerBlock][kP2dBlocks];
 };
 
+// sel[m]: the v_perm selector that packs a dword's bytes whose bit j of m
+// is clear (the alphabet ones) into its low bytes, zeros above.
+DEV void build_compact_sel(uint32_t *sel)
+{
+    if (threadIdx.x < 16) {
+        uint32_t v = 0x0C0C0C0Cu, k = 0;
+        for (uint32_t j = 0; j < 4; j++)
+            if (!((threadIdx.x >> j) & 1u)) {
+                v = (v & ~(0xFFu << (8 * k))) | (j << (8 * k));
+                k++;
+            }
+        sel[threadIdx.x] = v;
+    }
+}
+
 DEV uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
 
 // OR a left-aligned field (bits 23..24-w of F; the rest zero) into the
@@ -2209,21 +1816,20 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
     const uint32_t off0 = (uint32_t) ~packed;
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
-    if (threadIdx.x < 16) {
-        uint32_t sel = 0x0C0C0C0Cu, k = 0;
-        for (uint32_t j = 0; j < 4; j++)
-            if (!((threadIdx.x >> j) & 1u)) {
-                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
-                k++;
-            }
-        sm.sel[threadIdx.x] = sel;
-    }
+    build_compact_sel(sm.sel);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
     uint32_t *bits = (uint32_t *) bq;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
+    // One range: the first 2,048 characters' chunks c[] (nin[] characters of
+    // each lane in range), the lookahead byte la (valid if la_ok), its base
+    // B.  A range longer than 2,048 characters (inputs past 2 GiB: the
+    // range count is capped) is taken 2,048 at a time, the window's whole
+    // dwords flushed between steps and its partial dword carried to the
+    // front (as decode_buf_bits does); the bytes flushed early are final
+    // and never reach the next range's output.
     auto process = [&](uint32_t r, const uint4 *c, const uint32_t *nin, uint32_t la, bool la_ok,
                        uint64_t B) {
         const uint64_t rb = (uint64_t) r * R;
@@ -2232,44 +1838,75 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
         int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
         uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
         const uint32_t skew = (uint32_t) ((uintptr_t) ob & 3);
-        const int pb0 = 8 * (4 + (int) skew);  // stream bit of relative sextet 0
+        uint32_t lo = 4 + skew;       // LDS byte of output byte `done`
+        int pb0 = 8 * (int) lo;       // window bit of relative sextet 0
+        uint32_t done = 0;            // bytes flushed by earlier steps
         static_assert(kP2dBlocks > 64 && kP2dBlocks <= 128, "two zeroing stores per lane");
         bq[lane] = make_uint4(0, 0, 0, 0);
         if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
         wave_lds_order();
-        // per dword: table values, the v_perm compaction selector (by the
-        // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
-        // non-alphabet bytes; both chunks' counts in one packed DPP scan
-        uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+        const uint64_t start = first ? rb + off0 : rb;
+        for (uint64_t pos = start;; pos += 2 * kChunk) {
+            // per dword: table values, the v_perm compaction selector (by the
+            // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
+            // non-alphabet bytes; both chunks' counts in one packed DPP scan
+            uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            lane_values(sm.tab, c[h], nin[h], P[h]);
-            uint32_t nb = 0;
+            for (int h = 0; h < 2; h++) {
+                uint4 ch = c[h];
+                uint32_t nh = nin[h];
+                if (pos != start) {
+                    const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
+                    nh = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
+                    ch = nh ? load_chars(in + q, nh) : make_uint4(0, 0, 0, 0);
+                }
+                lane_values(sm.tab, ch, nh, P[h]);
+                uint32_t nb = 0;
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
-                const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
-                sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-                bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
-                nb += bad[h][g];
+                for (int g = 0; g < 4; g++) {
+                    const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
+                    const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
+                    sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
+                    bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
+                    nb += bad[h][g];
+                }
+                cnt |= (16u - nb) << (16 * h);
             }
-            cnt |= (16u - nb) << (16 * h);
-        }
-        const uint32_t incl = wave_incl_scan_dpp(cnt);
-        const uint32_t ex = incl - cnt;
-        const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+            const uint32_t incl = wave_incl_scan_dpp(cnt);
+            const uint32_t ex = incl - cnt;
+            const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int before = h ? (int) (tot & 0xFFFFu) : 0;
-            uint32_t p = (uint32_t) (pb0 + 6 * (T + before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
+            for (int h = 0; h < 2; h++) {
+                const int before = h ? (int) (tot & 0xFFFFu) : 0;
+                uint32_t p =
+                    (uint32_t) (pb0 + 6 * (T + before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
-                or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
-                p += 24u - 6u * bad[h][g];
+                for (int g = 0; g < 4; g++) {
+                    const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
+                    or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
+                    p += 24u - 6u * bad[h][g];
+                }
+            }
+            T += (int) ((tot & 0xFFFFu) + (tot >> 16));
+            if (pos + 2 * kChunk >= re) break;
+            // more of this range to come: flush the window's whole dwords
+            wave_lds_order();
+            const int bit_end = pb0 + 6 * T;
+            const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~3u : 0u;
+            if (kcut > lo) {
+                store_bits(bits, lo, kcut, ob + done - lo);
+                done += kcut - lo;
+                const uint32_t keep = bits[kcut >> 2];
+                wave_lds_order();
+                bq[lane] = make_uint4(0, 0, 0, 0);
+                if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+                wave_lds_order();
+                if (lane == 0) bits[1] = keep;
+                wave_lds_order();
+                pb0 -= 8 * (int) (kcut - 4);
+                lo = 4;
             }
         }
-        T += (int) ((tot & 0xFFFFu) + (tot >> 16));
         bool at_end = last;
         if (!last && T > 0 && (T & 3)) {
             // complete the range's last group from the characters after it
@@ -2303,8 +1940,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
             const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
             // the final partial group (emit_partial): 2 sextets -> 1 byte, 3 -> 2
             const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
-            const uint32_t lo = 4 + skew;
-            store_bits(bits, lo, lo + 3 * ng + tail, ob - lo);
+            const uint32_t total = 3 * ng + tail;
+            if (total > done) store_bits(bits, lo, lo + (total - done), ob + done - lo);
         }
         wave_lds_order();  // the next range re-zeroes the buffer
     };
@@ -2869,36 +2506,6 @@ __global__ __launch_bounds__(kThreads) void k_decode_group(
     }
 }
 
-// Batch fix-up: exact decode of the buffers the fast kernel marked.  Each
-// wave checks 64 outlen[] words at a time (one coalesced load + ballot) and
-// decodes the marked ones, so a clean batch costs one read of outlen[].
-__global__ __launch_bounds__(kThreads) void k_decode_batch_fix(
-    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
-    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
-{
-    __shared__ DecSmem sm;
-    build_dec_table(sm.tab, a);
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
-    for (uint64_t base = ((uint64_t) blockIdx.x * kWavesPerBlock + wv) * 64; base < nbuf;
-         base += nw * 64) {
-        const uint64_t bl = base + lane;
-        uint64_t m = __ballot(bl < nbuf && outlen[bl] == kNeedsExact);
-        while (m) {
-            const uint32_t i = __ffsll((unsigned long long) m) - 1;
-            m &= m - 1;
-            const uint32_t b = (uint32_t) (base + i);
-            uint64_t beg, len, obeg;
-            batch_buf(L, b, beg, len, obeg);
-            uint64_t v = decode_range(sm.tab, sm.sx[wv], in + beg, len, 0, len, 0,
-                                      out + obeg, true, false);
-            if (lane == 0) outlen[b] = v * 6 / 8;
-        }
-    }
-}
-
 // Batch fix-up, bit-stream form (k_decode_pass2d's machinery, one wave per
 // marked buffer, no cross-wave prefix): the buffer's characters are taken
 // 2,048 at a time; their sextets are OR-ed into the wave's LDS window as a
@@ -2995,15 +2602,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
 {
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
-    if (threadIdx.x < 16) {
-        uint32_t sel = 0x0C0C0C0Cu, k = 0;
-        for (uint32_t j = 0; j < 4; j++)
-            if (!((threadIdx.x >> j) & 1u)) {
-                sel = (sel & ~(0xFFu << (8 * k))) | (j << (8 * k));
-                k++;
-            }
-        sm.sel[threadIdx.x] = sel;
-    }
+    build_compact_sel(sm.sel);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3466,10 +3065,6 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
               p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
-    if (g_tune[8] == 1)  // the first-form one-block scan (A/B only)
-        hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, s, (const uint8_t *) d_in,
-                           nchars, p.R, p.nranges, a, ws, d_res, hold);
-    else
     {
         auto ks = g_tune[8] == 2 ? k_decode_scan2<1, 0>
                 : g_tune[8] == 3 ? k_decode_scan2<0, 0> : k_decode_scan2<0, 1>;
@@ -3479,24 +3074,15 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                            a, ws, d_res, hold);
     }
     if ((err = launch_status())) return err;
-    if (p.R <= kP2Range && g_tune[5] != 1) {
-        // grid-stride over the ranges with exactly the resident blocks (a
-        // second partial round of blocks would trail the rest)
-        auto k2 = g_tune[5] == 2 ? k_decode_pass2b
-                : g_tune[5] == 3 ? k_decode_pass2c<1>
-                : g_tune[5] == 4 ? k_decode_pass2c<0> : k_decode_pass2d;
-        static const int occ2c = occupancy_of(k_decode_pass2c<0>);
-        static const int occ2d = occupancy_of(k_decode_pass2d);
-        const int occ = g_tune[5] == 0 ? occ2d : g_tune[5] == 4 ? occ2c : 8;
-        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ);
-        hipLaunchKernelGGL(k2, dim3(b2), dim3(kThreads), 0, s,
-                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                           a, ws, hold);
-        return launch_status();
-    }
-    const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * 4);
-    hipLaunchKernelGGL(k_decode_pass2, dim3(b2), dim3(kThreads), 0, s,
-                       (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+    // grid-stride over the ranges with exactly the resident blocks (a second
+    // partial round of blocks would trail the rest); pass 2c (ranges of at
+    // most kP2Range characters) only for A/B
+    const bool use_2c = g_tune[5] == 4 && p.R <= kP2Range;
+    static const int occ2c = occupancy_of(k_decode_pass2c);
+    static const int occ2d = occupancy_of(k_decode_pass2d);
+    const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * (use_2c ? occ2c : occ2d));
+    hipLaunchKernelGGL(use_2c ? k_decode_pass2c : k_decode_pass2d, dim3(b2), dim3(kThreads),
+                       0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
                        a, ws, hold);
     return launch_status();
 }
@@ -3520,7 +3106,7 @@ static int launch_batch_decode(const void *d_in, const BatchLayout &L, uint32_t 
     // all it does.
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(g_tune[5] == 4 ? k_decode_batch_fix : k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }
@@ -3629,7 +3215,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     }
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(g_tune[5] == 4 ? k_decode_batch_fix : k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }

@@ -542,3 +542,33 @@ def test_beyond_32bit_ragged_batch():
     for i, n in enumerate(lens):
         assert torch.equal(dec[int(dout_off[i]):int(dout_off[i]) + n],
                            x[int(in_off[i]):int(in_off[i + 1])]), i
+
+
+@pytest.mark.parametrize("chunks", [3, 8])
+def test_decode_long_ranges_vs_oracle(chunks):
+    """Ranges longer than one 2,048-character step (what inputs past 2 GiB
+    get, since the range count is capped), forced at small sizes with the
+    range-size knob: the exact pass flushes its window between steps."""
+    import ctypes
+    from async_amd import _lib
+    lib = _lib.load()
+    lib.b64x__tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.b64x__tune(2, chunks)
+    try:
+        rng = np.random.default_rng(chunks)
+        for n in (1, 5000, 3 * 1024 * chunks + 7, 400_000):
+            host = rng.integers(0, 256, n, dtype=np.uint8)
+            chars = orc.encode(host)
+            for dirty in (b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76)),
+                          _junk(rng, chars, 0.3),
+                          _junk(rng, chars, 0, run_every=5000, run_len=3000)):
+                for hold in (False, True):
+                    got, info = gdec(dirty, hold=hold)
+                    want = orc.decode(dirty)
+                    if hold:  # whole groups only; the rest is held back
+                        assert info.out_len == 3 * (info.valid // 4)
+                        assert got == want[:info.out_len], (n, len(dirty))
+                    else:
+                        assert got == want, (n, len(dirty))
+    finally:
+        lib.b64x__tune(2, old)
