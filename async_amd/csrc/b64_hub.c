@@ -551,7 +551,7 @@ void b64_hub_post(b64_hub *h, action_1 a)
     (void) rc; /* EAGAIN only when the counter is saturated: still readable */
 }
 
-void b64_hub_forget(b64_hub *h, void *obj)
+void b64_hub_forget(b64_hub *h, void *obj, bool waiting)
 {
     pthread_mutex_lock(&h->post_lock);
     for (size_t i = 0; i < h->nposted; i++)
@@ -561,6 +561,8 @@ void b64_hub_forget(b64_hub *h, void *obj)
     for (size_t i = 0; i < h->ndraining; i++)
         if (h->draining[i].obj == obj)
             h->draining[i].act = NULL;
+    if (!waiting)
+        return;
     for (size_t i = 0; i < h->nkicking; i++)
         if (h->kicking[i].obj == obj)
             h->kicking[i].act = NULL;

@@ -60,9 +60,11 @@ void b64_hub_release(b64_hub *h);
  * are always served. */
 uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
                          size_t room, size_t min_room, size_t *granted, action_1 waiter);
-/* Drop any waiter or posted action whose object is `obj` (its stage is
- * closing). */
-void b64_hub_forget(b64_hub *h, void *obj);
+/* Drop any posted action -- and, when `waiting` (it may be on the waiter
+ * list), any waiter -- whose object is `obj` (its stage is closing).  The
+ * waiter lists can hold thousands of stages: scanning them on every close
+ * would be quadratic. */
+void b64_hub_forget(b64_hub *h, void *obj, bool waiting);
 /* Any thread (a HIP host callback): perform `a` on the loop at the hub's
  * next wake-up.  The poster must not outlive its b64_hub_forget(). */
 void b64_hub_post(b64_hub *h, action_1 a);

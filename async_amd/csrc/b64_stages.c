@@ -101,6 +101,7 @@ struct stage {
                            (a stream that ends inside it is one job) */
     atomic_bool wake_posted; /* decoder: a session completion is queued
                                 on the hub for this stage */
+    unsigned hub_waits; /* entries on the hub's waiter list (room for a block) */
     bool started;       /* the hub (and any sessions) are held */
     int err;            /* sticky failure errno, 0 while healthy */
     slot slots[NSLOTS];
@@ -149,6 +150,14 @@ static ssize_t stage_fail(stage *st, int negerr)
     st->err = negerr < 0 ? -negerr : EIO;
     errno = st->err;
     return -1;
+}
+
+/* The hub has room again: this stage is off its waiter list. */
+static void stage_kicked(stage *st)
+{
+    if (st->hub_waits)
+        st->hub_waits--;
+    action_1_perf(st->cb);
 }
 
 /* Loop side of a session completion (posted through the loop's hub: one
@@ -225,7 +234,7 @@ static void stage_stop(stage *st)
         }
     }
     if (st->hub) {
-        b64_hub_forget(st->hub, st);
+        b64_hub_forget(st->hub, st, st->hub_waits > 0);
         for (int i = 0; i < NSLOTS; i++)
             b64_ticket_release(&st->slots[i].ticket);
         b64_hub_release(st->hub);
@@ -316,11 +325,14 @@ static int top_up_encoder(stage *st)
                 must_progress = false; /* a completion will wake us */
         action_1 waiter = { NULL, NULL };
         if (!must_progress)
-            waiter = (action_1) { st, (act_1) stage_notify };
+            waiter = (action_1) { st, (act_1) stage_kicked };
         uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_ENCODE, &st->abc, st->cap,
                                       st->ncarry + 4096, &room, waiter);
-        if (!in)
+        if (!in) {
+            if (errno == EAGAIN && waiter.act)
+                st->hub_waits++;
             return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
+        }
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;
@@ -374,12 +386,15 @@ static int top_up_encoder(stage *st)
 static int decoder_first_via_hub(stage *st, slot *sl, size_t *moved)
 {
     *moved = 0;
-    action_1 waiter = { st, (act_1) stage_notify };
+    action_1 waiter = { st, (act_1) stage_kicked };
     size_t room;
     uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_DECODE, &st->abc, st->cap, 4096, &room,
                                   waiter);
-    if (!in)
+    if (!in) {
+        if (errno == EAGAIN)
+            st->hub_waits++;
         return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
+    }
     bool eof;
     int uerr;
     size_t got = gather(st, in, room, &eof, &uerr);
