@@ -25,6 +25,7 @@ from . import _lib
 from ._lib import B64xError, DecResult, alphabet  # noqa: F401
 
 HOLD_TAIL = 1  # B64X_DEC_HOLD_TAIL
+EXPECT_JUNK = 2  # B64X_DEC_EXPECT_JUNK
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -93,8 +94,11 @@ class Decoded:
 
 def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
            hold_tail: bool = False, workspace: torch.Tensor | None = None,
-           result: torch.Tensor | None = None, stream=None) -> Decoded:
-    """Leniently decode a device buffer of base64 characters."""
+           result: torch.Tensor | None = None, stream=None,
+           expect_junk: bool = False) -> Decoded:
+    """Leniently decode a device buffer of base64 characters.
+    expect_junk: the input holds non-alphabet bytes throughout (MIME line
+    breaks) -- decode in one pass (B64X_DEC_EXPECT_JUNK); same result."""
     lib = _lib.load()
     a = _abc(abc)
     _u8(x, "input")
@@ -111,7 +115,8 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
         workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
     _lib.check("b64x_decode_dev", lib.b64x_decode_dev(
         _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a),
-        HOLD_TAIL if hold_tail else 0, _ptr(workspace), _stream(stream)))
+        (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0),
+        _ptr(workspace), _stream(stream)))
     return Decoded(out, result)
 
 

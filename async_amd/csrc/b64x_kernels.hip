@@ -376,8 +376,9 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 // the exact decode (0: bit-stream pass2d, 4: pass2c, the per-character
 // scatter), 6 = 1: the first-form tight/row batch kernels, 7 = lanes'
 // slots per batch-kernel tile (2 or 4), 8 = decode scan (2: look-back
-// priced out, 3: tiles by block index).
-int g_tune[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+// priced out, 3: tiles by block index), 9 = single-pass decode pricing
+// (bit 0: no look-back, bit 1: no decode phase; wrong results, A/B only).
+int g_tune[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 // ASYNC_B64_TUNE="i=v,i=v": kernel-variant knobs for A/B runs of the whole
 // test suite or bench (the same knobs b64x__tune sets).
@@ -389,7 +390,7 @@ __attribute__((constructor)) void tune_from_env()
         const long i = strtol(v, &end, 10);
         if (*end != '=') break;
         const long x = strtol(end + 1, &end, 10);
-        if (i >= 0 && i < 9) g_tune[i] = (int) x;
+        if (i >= 0 && i < 10) g_tune[i] = (int) x;
         v = *end == ',' ? end + 1 : nullptr;
     }
 }
@@ -1025,12 +1026,17 @@ struct DecodeWs {
     uint64_t *fd;
     uint64_t *fd_cur;
     uint32_t *ticket;
+    uint32_t *fticket;   // the single-pass decode's tile ticket (zero between calls)
     uint32_t *counts;
     uint64_t *bases;
     uint64_t *status;
+    uint64_t *fstatus;   // the single-pass decode's tile status words (zero between calls)
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
+constexpr uint32_t kFusePer = 16;     // ranges per wave in the single-pass decode
+constexpr uint32_t kFuseLoad = 4;     // of them loaded at once for counting
+constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
 // Layout for `nranges` ranges: 64-byte header, counts, bases, tile status.
 DEV DecodeWs ws_view(void *ws, uint32_t nranges)
@@ -1043,6 +1049,8 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.counts = (uint32_t *) (p + 64);
     w.bases = (uint64_t *) (p + 64 + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     w.status = w.bases + nranges;
+    w.fstatus = w.status + (nranges + kScanTile - 1) / kScanTile;
+    w.fticket = (uint32_t *) (p + 20);
     return w;
 }
 
@@ -1805,15 +1813,29 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
     return x;
 }
 
-__global__ __launch_bounds__(kThreads) void k_decode_pass2d(
+// FUSED = 1: the single-pass exact decode (B64X_DEC_EXPECT_JUNK), in place
+// of pass 1 + scan + pass 2.  Blocks take tiles of kFuseTile ranges from a
+// ticket (so a tile's predecessors are running or done); each wave counts
+// its kFusePer ranges, the block publishes the tile's count and looks back
+// over its predecessors' status words as k_decode_scan2 does, then each
+// wave decodes its ranges with the same range body as pass 2d, re-reading
+// them (the tile was just read: L2/MALL hits).  The last tile writes the
+// result record, waits until every tile is inclusive and every block has
+// its ticket, and clears the status words and the ticket.
+template <bool FUSED>
+__global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
+    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold,
+    b64x_dec_result *res, uint32_t price = 0)
 {
     DecodeWs w = ws_view(ws, nranges);
-    const uint64_t packed = *w.fd_cur;
-    if (packed == 0) return;
-    const uint32_t r0 = (uint32_t) (~packed >> 32);
-    const uint32_t off0 = (uint32_t) ~packed;
+    uint32_t r0 = 0xFFFFFFFFu, off0 = 0;  // fused: no range resumes mid-way
+    if (!FUSED) {
+        const uint64_t packed = *w.fd_cur;
+        if (packed == 0) return;
+        r0 = (uint32_t) (~packed >> 32);
+        off0 = (uint32_t) ~packed;
+    }
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
@@ -1945,21 +1967,131 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
         }
         wave_lds_order();  // the next range re-zeroes the buffer
     };
-    auto load_generic = [&](uint32_t r) {
+    // the first step's chunks of range r (from `start`) and its lookahead
+    auto load_range = [&](uint32_t r, uint4 *c, uint32_t *nin, uint32_t &la, bool &la_ok) {
         const uint64_t rb = (uint64_t) r * R;
         const uint64_t re = rb + R < n ? rb + R : n;
         const bool last = r + 1 == nranges, first = r == r0;
         const uint64_t start = first ? rb + off0 : rb;
-        uint4 c[2];
-        uint32_t nin[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
             nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
             c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
         }
-        const bool la_ok = !last && re + lane < n;
-        const uint32_t la = la_ok ? in[re + lane] : 0u;
+        la_ok = !last && re + lane < n;
+        la = la_ok ? in[re + lane] : 0u;
+    };
+    if (FUSED) {
+        __shared__ uint32_t s_tile;
+        __shared__ uint32_t s_cnt[kFuseTile];
+        __shared__ uint64_t s_excl, s_agg;
+        const uint32_t ntiles = (nranges + kFuseTile - 1) / kFuseTile;
+        if (threadIdx.x == 0) s_tile = atomicAdd(w.fticket, 1u);
+        __syncthreads();
+        const uint32_t t = s_tile;
+        const uint32_t rw = t * kFuseTile + wv * kFusePer;  // this wave's first range
+        // counts (R is one step: the caller takes this path only then); all
+        // of the wave's loads are issued before any is counted
+        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
+            uint4 c[kFuseLoad][2];
+            uint32_t nin[kFuseLoad][2];
+#pragma unroll
+            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+                const uint32_t j = j0 + jj;
+                const uint64_t rb = (uint64_t) (rw + j) * R;
+                const uint64_t re = rb + R < n ? rb + R : n;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = rb + (uint64_t) h * kChunk + 16 * lane;
+                    nin[jj][h] = rw + j >= nranges || p >= re
+                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                    c[jj][h] =
+                        nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+                uint32_t cnt = 0;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    uint32_t P[4];
+                    lane_values(sm.tab, c[jj][h], nin[jj][h], P);
+                    cnt += lane_valid_count(P);
+                }
+                cnt = wave_sum(cnt);
+                if (lane == 0) s_cnt[wv * kFusePer + j0 + jj] = cnt;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            uint64_t agg = 0;
+            for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
+            uint64_t excl = 0;
+            if (t > 0 && !(price & 1)) {
+                if (lane == 0) st_store(&w.fstatus[t], kStAgg | agg);
+                for (int64_t p = (int64_t) t - 1;;) {
+                    const int64_t q = p - lane;
+                    const uint64_t v = q >= 0 ? st_load(&w.fstatus[q]) : kStIncl;
+                    const uint32_t f = (uint32_t) (v >> 62);
+                    const uint64_t inc = __ballot(f == 2);
+                    const uint32_t k =
+                        inc ? (uint32_t) __ffsll((unsigned long long) inc) - 1 : 63u;
+                    if (!__all(lane > k || f != 0)) {
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    uint64_t part = lane <= k ? (v & kStVal) : 0;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
+                    excl += part;
+                    if (inc) break;
+                    p -= 64;
+                }
+            }
+            if (lane == 0) {
+                st_store(&w.fstatus[t], kStIncl | (excl + agg));
+                s_excl = excl;
+                s_agg = agg;
+            }
+        }
+        __syncthreads();
+        uint64_t B = s_excl;
+        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
+        for (uint32_t j = 0; j < kFusePer && rw + j < nranges && !(price & 2); j++) {
+            uint4 c[2];
+            uint32_t nin[2], la;
+            bool la_ok;
+            load_range(rw + j, c, nin, la, la_ok);
+            process(rw + j, c, nin, la, la_ok, B);
+            B += s_cnt[wv * kFusePer + j];
+        }
+        if (t == ntiles - 1 && wv == 0) {
+            const uint64_t V = s_excl + s_agg;
+            if (lane == 0) write_result(res, V, hold);
+            find_tail_sextets(sm.tab, in, n, V, res);
+            for (;;) {  // every tile inclusive -> every look-back is over
+                bool all = true;
+                for (uint32_t i = lane; i < ntiles; i += 64)
+                    all = all && (st_load(&w.fstatus[i]) >> 62) == 2;
+                if (__all(all)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+            if (lane == 0) {  // every block has its ticket -> re-arm the counter
+                while (__hip_atomic_load(w.fticket, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
+                    __builtin_amdgcn_s_sleep(1);
+                __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        return;
+    }
+    auto load_generic = [&](uint32_t r) {
+        uint4 c[2];
+        uint32_t nin[2], la;
+        bool la_ok;
+        load_range(r, c, nin, la, la_ok);
         process(r, c, nin, la, la_ok, scalar_load_u64(w.bases + r));
     };
     uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
@@ -1996,6 +2128,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
     }
     for (; r < nranges; r += nw) load_generic(r);
 }
+
+constexpr auto k_decode_pass2d = k_decode_pass2d_t<false>;
+constexpr auto k_decode_fused = k_decode_pass2d_t<true>;
 
 // Batches: buffer b is in[ioff(b) .. +len(b)) -> out + ooff(b).
 struct BatchLayout {
@@ -2852,7 +2987,8 @@ uint64_t b64x_decode_workspace_size(uint64_t nchars)
     // nchars (ranges are at least one chunk; 0 = the largest input)
     uint64_t nr = nchars ? (nchars + kChunk - 1) / kChunk : kMaxRanges;
     if (nr > kMaxRanges) nr = kMaxRanges;
-    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8 + (nr + kScanTile - 1) / kScanTile * 8;
+    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8 + (nr + kScanTile - 1) / kScanTile * 8 +
+           (nr + kFuseTile - 1) / kFuseTile * 8;
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
@@ -3047,7 +3183,7 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     unsigned flags, void *d_workspace, void *stream)
 {
     if (!d_res) return -EINVAL;
-    if (flags & ~(unsigned) B64X_DEC_HOLD_TAIL) return -EINVAL;
+    if (flags & ~(unsigned) (B64X_DEC_HOLD_TAIL | B64X_DEC_EXPECT_JUNK)) return -EINVAL;
     if (nchars && (!d_in || !d_out)) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
@@ -3062,6 +3198,14 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     const uint32_t blocks = (p.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const DecAlpha a = dec_alpha(abc);
     const uint32_t hold = flags & B64X_DEC_HOLD_TAIL;
+    if ((flags & B64X_DEC_EXPECT_JUNK) && p.R == 2 * kChunk) {
+        // one pass: a block per tile of kFuseTile ranges, in ticket order
+        const uint32_t tiles = (p.nranges + kFuseTile - 1) / kFuseTile;
+        hipLaunchKernelGGL(k_decode_fused, dim3(tiles), dim3(kThreads), 0, s,
+                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+                           a, ws, hold, d_res, (uint32_t) g_tune[9]);
+        return launch_status();
+    }
     p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
               p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
@@ -3077,13 +3221,19 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     // grid-stride over the ranges with exactly the resident blocks (a second
     // partial round of blocks would trail the rest); pass 2c (ranges of at
     // most kP2Range characters) only for A/B
-    const bool use_2c = g_tune[5] == 4 && p.R <= kP2Range;
-    static const int occ2c = occupancy_of(k_decode_pass2c);
+    if (g_tune[5] == 4 && p.R <= kP2Range) {
+        static const int occ2c = occupancy_of(k_decode_pass2c);
+        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2c);
+        hipLaunchKernelGGL(k_decode_pass2c, dim3(b2), dim3(kThreads), 0, s,
+                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+                           a, ws, hold);
+        return launch_status();
+    }
     static const int occ2d = occupancy_of(k_decode_pass2d);
-    const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * (use_2c ? occ2c : occ2d));
-    hipLaunchKernelGGL(use_2c ? k_decode_pass2c : k_decode_pass2d, dim3(b2), dim3(kThreads),
-                       0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                       a, ws, hold);
+    const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2d);
+    hipLaunchKernelGGL(k_decode_pass2d, dim3(b2), dim3(kThreads), 0, s,
+                       (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
+                       a, ws, hold, (b64x_dec_result *) nullptr, 0u);
     return launch_status();
 }
 
@@ -3683,7 +3833,7 @@ int b64x_lane_wait(b64x_lane *l)
 // deliberately not declared in include/b64x.h).
 int b64x__tune(int idx, int value)
 {
-    if (idx < 0 || idx >= 9) return -EINVAL;
+    if (idx < 0 || idx >= 10) return -EINVAL;
     int old = g_tune[idx];
     g_tune[idx] = value;
     return old;

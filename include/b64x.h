@@ -70,6 +70,12 @@ typedef struct b64x_dec_result {
                                  produce no output.  Used by the streaming
                                  stage, which carries them to its next
                                  call. */
+#define B64X_DEC_EXPECT_JUNK 2u /* a hint that the input holds non-alphabet
+                                   bytes throughout (MIME line breaks):
+                                   decode in one pass (counts, look-back,
+                                   exact decode) instead of the optimistic
+                                   pass that clean input takes.  Same
+                                   result either way. */
 
 /* ---- sizes ------------------------------------------------------------ */
 

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--mib", type=int, nargs="*", default=[64, 1024])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--tune", default="", help="idx:val,... (b64x__tune knobs, A/B only)")
+    ap.add_argument("--expect-junk", action="store_true",
+                    help="B64X_DEC_EXPECT_JUNK: the single-pass decode")
     args = ap.parse_args()
     if args.tune:
         import ctypes
@@ -58,19 +60,20 @@ def main():
         del enc
         ws = torch.zeros(b64.workspace_size(dirty.numel()), dtype=torch.uint8, device="cuda")
         out = torch.empty(b64.decoded_cap(dirty.numel()), dtype=torch.uint8, device="cuda")
-        d = b64.decode(dirty, out=out, workspace=ws)
+        d = b64.decode(dirty, out=out, workspace=ws, expect_junk=args.expect_junk)
         ok = d.info().out_len == n and torch.equal(out[:n], x)
         times = []
         for _ in range(args.steps):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            b64.decode(dirty, out=out, workspace=ws)
+            b64.decode(dirty, out=out, workspace=ws, expect_junk=args.expect_junk)
             b.record()
             b.synchronize()
             times.append(a.elapsed_time(b))
         ms = sorted(times)[len(times) // 2]
         alg = dirty.numel() + n
-        print(json.dumps({"measure": "decode_crlf76", "payload_bytes": n, "chars": dirty.numel(),
+        print(json.dumps({"measure": "decode_crlf76", "expect_junk": args.expect_junk,
+                          "payload_bytes": n, "chars": dirty.numel(),
                           "ms": ms, "GiB_s_payload": n / ms / 1e-3 / 2**30,
                           "alg_TB_s": alg / ms / 1e-3 / 1e12, "exact": bool(ok)}), flush=True)
         del x, dirty, ws, out

@@ -572,3 +572,52 @@ def test_decode_long_ranges_vs_oracle(chunks):
                         assert got == want, (n, len(dirty))
     finally:
         lib.b64x__tune(2, old)
+
+
+def gdec_j(chars, pos62=-1, pos63=-1, hold=False):
+    d = b64.decode(dev(chars), abc=(pos62, pos63, True, -1), hold_tail=hold,
+                   expect_junk=True)
+    return d.bytes().cpu().numpy().tobytes(), d.info()
+
+
+@pytest.mark.parametrize("density", [0.0, 1e-3, 0.05, 0.5])
+def test_single_pass_decode_vs_oracle(density):
+    """B64X_DEC_EXPECT_JUNK (one pass: counts, tile look-back, exact
+    decode) gives the oracle's bytes and result record, with and without
+    HOLD_TAIL, on clean and dirty input, across tile boundaries (16 ranges
+    of 2,048 characters per tile)."""
+    rng = np.random.default_rng(int(density * 1e4) + 11)
+    for n in (0, 1, 2, 5, 1000, 4096 * 3 + 17, 300000, 2_000_000):
+        host = rng.integers(0, 256, n, dtype=np.uint8)
+        chars = orc.encode(host)
+        dirty = _junk(rng, chars, density)
+        want = orc.decode(dirty)
+        got, info = gdec_j(dirty)
+        assert got == want, (n, density)
+        ref, rinfo = gdec(dirty)
+        assert (info.out_len, info.valid) == (rinfo.out_len, rinfo.valid)
+        hgot, hinfo = gdec_j(dirty, hold=True)
+        href, hrinfo = gdec(dirty, hold=True)
+        assert hgot == href and hinfo.tail_n == hrinfo.tail_n, n
+        assert bytes(hinfo.tail)[:hinfo.tail_n] == bytes(hrinfo.tail)[:hrinfo.tail_n], n
+
+
+def test_single_pass_decode_structured_and_alphabets():
+    rng = np.random.default_rng(12)
+    host = rng.integers(0, 256, 1_500_000, dtype=np.uint8)
+    for abc in ((-1, -1), (".", "_"), ("\n", "\r")):
+        chars = orc.encode(host, abc[0], abc[1], True, -1)
+        for dirty in (b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76)),
+                      chars[:100001] + b"==" + chars[100001:],
+                      _junk(rng, chars, 0, run_every=700_001, run_len=300_000),
+                      b"\n" * 5000 + chars + b"=\n" * 9000):
+            got, info = gdec_j(dirty, *abc)
+            assert got == orc.decode(dirty, *abc), abc
+    junk = bytes(rng.integers(0x80, 0x100, 1_000_000, dtype=np.uint8))
+    got, info = gdec_j(junk)
+    assert got == b"" and info.valid == 0 and info.out_len == 0
+    # the workspace is left re-armed: the two paths alternate on one stream
+    for k in range(4):
+        chars = orc.encode(rng.integers(0, 256, 100_000 + k, dtype=np.uint8))
+        d = b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76))
+        assert (gdec_j(d) if k % 2 else gdec(d))[0] == orc.decode(d)
