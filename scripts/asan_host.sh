@@ -9,7 +9,7 @@
 set -e
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 B="$ROOT/build_asan"
-if [ ! -f "$B/async_amd/libasync_b64.so" ]; then
+if [ ! -f "$B/async_amd/libasync_b64.so" ] || [ -n "$(find "$ROOT/async_amd/csrc" "$ROOT/include" "$ROOT/tests/csrc" -newer "$B/async_amd/libasync_b64.so" -name '*.[ch]*' | head -1)" ]; then
   rm -rf "$B" && mkdir -p "$B"
   cp -r "$ROOT/include" "$ROOT/async_amd" "$ROOT/tests" "$ROOT/oracle" "$ROOT/Makefile" "$B/"
   rm -rf "$B/build" "$B"/async_amd/*.so "$B"/oracle/*.so "$B"/tests/csrc/*.so
@@ -18,7 +18,8 @@ if [ ! -f "$B/async_amd/libasync_b64.so" ]; then
 fi
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:protect_shadow_gap=0
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
-PRE="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)"
+# prepended to any preload already in the environment, which stays in place
+PRE="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)${LD_PRELOAD:+:$LD_PRELOAD}"
 cd "$B"
 if [ "$1" = gpu ]; then
   LD_PRELOAD="$PRE" timeout -k 10 600 python -u -m pytest tests/test_stages_gpu.py \
