@@ -15,8 +15,11 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 CC       ?= gcc
 ARCH     ?= gfx950
+# -Wno-pass-failed: k_encode_flat's `#pragma unroll` loops (compile-time trip
+# counts) are reported "not unrolled" after they have already been fully
+# unrolled by an earlier pass; the ISA is the unrolled one.
 HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC \
-            -Wall -Iinclude
+            -Wall -Wno-pass-failed -Iinclude
 CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
 
 LIB      = async_amd/libasync_b64.so
