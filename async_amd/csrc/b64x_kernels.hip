@@ -3567,13 +3567,32 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
     return 0;
 }
 
+// A session's encode reads and writes its pinned host buffers in place over
+// PCIe (zero-copy) instead of H2D, kernel, D2H: each byte crosses PCIe once
+// either way, but one kernel's reads and writes overlap (duplex) and nothing
+// is staged through HBM -- 30 GiB/s of payload against 22 staged for 32 MiB
+// blocks (bench_host_pipeline resident_encode; scripts/bench_zero_copy.py).
+// Not for the hub's ragged batches: one block per job is PCIe-latency-bound
+// in place (a single 1 MiB stream ran at half the staged rate).
+// ASYNC_B64_ZERO_COPY=0 stages sessions too.
+static bool zero_copy_encode()
+{
+    static const bool on = [] {
+        const char *v = getenv("ASYNC_B64_ZERO_COPY");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 int b64x_session_encode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
                               b64x_done_fn done, void *arg)
 {
     if (!s || n > s->cap) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    if (n) {
+    if (n && zero_copy_encode()) {
+        if ((err = b64x_encode_dev(s->h_in, n, s->h_out, abc, s->stream))) return err;
+    } else if (n) {
         const uint64_t m = b64x_encoded_len(n, enc_alpha(abc).pad);
         if ((err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream)))) return err;
         if ((err = b64x_encode_dev(s->d_in, n, s->d_out, abc, s->stream))) return err;
@@ -3759,7 +3778,7 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off))) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(l->device)))) return err;
-    if (njobs) {
+    if (njobs) {  // staged: the ragged kernel's block-per-job form is PCIe-latency-bound in place
         const uint64_t in_bytes = h_in_off[njobs], out_bytes = h_out_off[njobs];
         const uint64_t words = (uint64_t) njobs + 1;
         if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
