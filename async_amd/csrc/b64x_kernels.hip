@@ -1813,6 +1813,49 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
     return x;
 }
 
+// One 2,048-character step of the bit-stream decode: lanes' chunks c[h]
+// (nin[h] characters each) are looked up, compacted per dword, and their
+// sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
+// up to 18 bits past the window's byte 4: skipped sextets land in its
+// head).  Returns the step's alphabet characters.
+DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
+                       const uint32_t nin[2], int bit0)
+{
+    // per dword: table values, the v_perm compaction selector (by the
+    // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
+    // non-alphabet bytes; both chunks' counts in one packed DPP scan
+    uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        lane_values(sm.tab, c[h], nin[h], P[h]);
+        uint32_t nb = 0;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
+            const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
+            sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
+            bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
+            nb += bad[h][g];
+        }
+        cnt |= (16u - nb) << (16 * h);
+    }
+    const uint32_t incl = wave_incl_scan_dpp(cnt);
+    const uint32_t ex = incl - cnt;
+    const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int before = h ? (int) (tot & 0xFFFFu) : 0;
+        uint32_t p = (uint32_t) (bit0 + 6 * (before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
+            or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
+            p += 24u - 6u * bad[h][g];
+        }
+    }
+    return (tot & 0xFFFFu) + (tot >> 16);
+}
+
 // FUSED = 1: the single-pass exact decode (B64X_DEC_EXPECT_JUNK), in place
 // of pass 1 + scan + pass 2.  Blocks take tiles of kFuseTile ranges from a
 // ticket (so a tile's predecessors are running or done); each wave counts
@@ -1869,47 +1912,17 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
         wave_lds_order();
         const uint64_t start = first ? rb + off0 : rb;
         for (uint64_t pos = start;; pos += 2 * kChunk) {
-            // per dword: table values, the v_perm compaction selector (by the
-            // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
-            // non-alphabet bytes; both chunks' counts in one packed DPP scan
-            uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+            uint4 ch[2] = {c[0], c[1]};
+            uint32_t nh[2] = {nin[0], nin[1]};
+            if (pos != start) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                uint4 ch = c[h];
-                uint32_t nh = nin[h];
-                if (pos != start) {
+                for (int h = 0; h < 2; h++) {
                     const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
-                    nh = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
-                    ch = nh ? load_chars(in + q, nh) : make_uint4(0, 0, 0, 0);
-                }
-                lane_values(sm.tab, ch, nh, P[h]);
-                uint32_t nb = 0;
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
-                    const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
-                    sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-                    bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
-                    nb += bad[h][g];
-                }
-                cnt |= (16u - nb) << (16 * h);
-            }
-            const uint32_t incl = wave_incl_scan_dpp(cnt);
-            const uint32_t ex = incl - cnt;
-            const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int before = h ? (int) (tot & 0xFFFFu) : 0;
-                uint32_t p =
-                    (uint32_t) (pb0 + 6 * (T + before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
-                    or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
-                    p += 24u - 6u * bad[h][g];
+                    nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
+                    ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
                 }
             }
-            T += (int) ((tot & 0xFFFFu) + (tot >> 16));
+            T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
             if (pos + 2 * kChunk >= re) break;
             // more of this range to come: flush the window's whole dwords
             wave_lds_order();
@@ -2673,40 +2686,18 @@ DEV uint64_t decode_buf_bits(const P2dSmem &sm, uint4 *bq, const uint8_t *src, u
     if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
     wave_lds_order();
     for (uint64_t p = 0;; p += 2 * kChunk) {
-        uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+        uint4 ch[2];
+        uint32_t nh[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint64_t q = p + (uint64_t) h * kChunk + 16 * lane;
-            const uint32_t nin = q >= len ? 0u : (len - q >= 16 ? 16u : (uint32_t) (len - q));
-            const uint4 c = p == 0 ? first[h]
-                          : nin ? load_chars(src + q, nin) : make_uint4(0, 0, 0, 0);
-            lane_values(sm.tab, c, nin, P[h]);
-            uint32_t nb = 0;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
-                const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
-                sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-                bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
-                nb += bad[h][g];
-            }
-            cnt |= (16u - nb) << (16 * h);
+            nh[h] = q >= len ? 0u : (len - q >= 16 ? 16u : (uint32_t) (len - q));
+            ch[h] = p == 0 ? first[h]
+                  : nh[h] ? load_chars(src + q, nh[h]) : make_uint4(0, 0, 0, 0);
         }
-        const uint32_t incl = wave_incl_scan_dpp(cnt);
-        const uint32_t ex = incl - cnt;
-        const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-        const uint32_t t0 = tot & 0xFFFFu, t1 = tot >> 16;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            uint32_t q = pb + 6u * ((h ? t0 : 0u) + ((ex >> (16 * h)) & 0xFFFFu));
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                or_field(bits, q, group_dot(__builtin_amdgcn_perm(0u, P[h][g], sel[h][g])));
-                q += 24u - 6u * bad[h][g];
-            }
-        }
-        pb += 6u * (t0 + t1);
-        V += t0 + t1;
+        const uint32_t got = bits_step(sm, bits, ch, nh, (int) pb);
+        pb += 6u * got;
+        V += got;
         wave_lds_order();
         const bool last = p + 2 * kChunk >= len;
         if (last) {
