@@ -58,7 +58,7 @@ def test_decoder_stage_vs_oracle(read_size, burst):
             assert got == data
 
 
-@pytest.mark.parametrize("abc", [(-1, -1), (".", "_")])
+@pytest.mark.parametrize("abc", [(-1, -1), (".", "_"), ("\n", "\r")])
 def test_many_short_decoder_streams_on_one_loop(abc):
     """Short decoder streams (each ends inside its first block) are decoded
     as jobs of shared hub batches: every stream's bytes equal the oracle's,
