@@ -8,10 +8,16 @@
  * stage's pinned output, lent until b64_lend_return() (or the stage's next
  * read or close).  *data is NULL when the bytes were copied to `fallback`.
  * For any other stream it is a plain read into `fallback`.
+ *
+ * From a stream for which b64_lend_capable() holds, `fallback` may be
+ * NULL: bytes that span blocks are then gathered into the stage's own
+ * buffer and lent from there, so *data is never NULL when the result is
+ * positive (a wrapper needs no max-size buffer of its own).
  */
 #ifndef ASYNC_AMD_B64_LEND_H
 #define ASYNC_AMD_B64_LEND_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <sys/types.h>
@@ -20,5 +26,6 @@
 
 ssize_t b64_lend_read(bytestream_1 s, void *fallback, size_t count, const uint8_t **data);
 void b64_lend_return(bytestream_1 s);
+bool b64_lend_capable(bytestream_1 s);
 
 #endif

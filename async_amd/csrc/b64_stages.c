@@ -114,6 +114,8 @@ struct stage {
     uint8_t carry[2];   /* encoder: bytes of the incomplete group */
     size_t ncarry;
     bool lend_want;     /* this read may lend instead of copy (b64_lend.h) */
+    uint8_t *spill;     /* lent copy of reads that span blocks (no fallback) */
+    size_t spill_cap;
     const uint8_t *lent;/* what the last read lent, until returned */
 };
 
@@ -550,6 +552,17 @@ static size_t serve_body(stage *st, uint8_t *dst, size_t n)
         h->out_pos += n;
         return n;
     }
+    uint8_t *spill = NULL;
+    if (!dst) { /* a lending read without a fallback: the stage's own buffer */
+        if (st->spill_cap < n) {
+            free(st->spill);
+            st->spill = malloc(n);
+            if (!st->spill)
+                abort(); /* like fsalloc: allocation failure is fatal */
+            st->spill_cap = n;
+        }
+        dst = spill = st->spill;
+    }
     size_t done = 0;
     while (done < n && st->nbusy) {
         slot *sl = &st->slots[st->head];
@@ -564,6 +577,8 @@ static size_t serve_body(stage *st, uint8_t *dst, size_t n)
         else if (sl->out_pos == sl->body_end)
             break;
     }
+    if (spill)
+        st->lent = spill;
     return done;
 }
 
@@ -666,6 +681,9 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
 static void stage_close(stage *st)
 {
     st->lent = NULL;
+    free(st->spill);
+    st->spill = NULL;
+    st->spill_cap = 0;
     stage_stop(st);
     bytestream_1_close(st->up);
     async_wound(st->async, st);
@@ -755,6 +773,11 @@ ssize_t b64_lend_read(bytestream_1 s, void *fallback, size_t count, const uint8_
     if (n > 0)
         *data = st->lent; /* NULL: copied into fallback */
     return n;
+}
+
+bool b64_lend_capable(bytestream_1 s)
+{
+    return s.vt == &encoder_vt;
 }
 
 void b64_lend_return(bytestream_1 s)

@@ -252,6 +252,7 @@ struct chunkencoder {
     uint8_t *frame;    /* CHUNK_HEAD + max_chunk (+2 for the final CRLF) */
     const uint8_t *data; /* the chunk's data lent by a GPU encoder stage
                             (b64_lend.h), or NULL: it is in frame */
+    bool lend;         /* upstream lends every chunk: frame is header-only */
     size_t pos, end;   /* unserved part of the current frame */
     size_t chunks;     /* frames started */
     bool last_framed;  /* the zero-length chunk has been built */
@@ -269,7 +270,10 @@ chunkencoder_t *chunk_encode_2(async_t *async, bytestream_1 stream,
                    : max_chunk_size > CHUNK_MAX ? CHUNK_MAX
                                                 : max_chunk_size;
     c->termination = termination;
-    c->frame = xmalloc(CHUNK_HEAD + c->max_chunk);
+    /* over the GPU encoder the chunk's data is lent (b64_lend.h): the frame
+     * holds only the header and the final CRLF, not max_chunk bytes */
+    c->lend = b64_lend_capable(stream);
+    c->frame = xmalloc(CHUNK_HEAD + (c->lend ? 2 : c->max_chunk));
     return c;
 }
 
@@ -311,7 +315,8 @@ ssize_t chunkencoder_read(chunkencoder_t *c, void *buf, size_t count)
             return 0;
         /* same count as a read into the frame; from the GPU encoder the
          * data usually stays where the stage has it (one copy fewer) */
-        ssize_t n = b64_lend_read(c->up, c->frame + CHUNK_HEAD, c->max_chunk, &c->data);
+        ssize_t n = b64_lend_read(c->up, c->lend ? NULL : c->frame + CHUNK_HEAD,
+                                  c->max_chunk, &c->data);
         if (n < 0)
             return -1;
         c->pos = chunk_header(c, (size_t) n);
