@@ -56,6 +56,25 @@ def test_egress_stacks_vs_oracle(max_chunk):
         assert framed[i] == orc.chunked_encode(msg, max_chunk=max_chunk), (i, L)
 
 
+@pytest.mark.parametrize("cap", [4096, 65536])
+def test_egress_stacks_chunks_spanning_blocks(monkeypatch, cap):
+    """Small stage blocks (a block still holds one whole read, as the stage
+    requires): the chunkencoder's reads often span two blocks, so the lent
+    characters come from the stage's spill buffer (the frame holds only
+    headers).  Framing stays the oracle's."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    lens = util.zipf_lengths()[:200]
+    payload = util.splitmix64(0xC0FFEE, int(lens.sum()))
+    for max_chunk in (30, 100_000):
+        framed, err = util.egress_stacks(payload, lens, max_chunk, 10240)
+        assert err == 0
+        off = 0
+        for i, L in enumerate(lens.tolist()):
+            msg = payload[off:off + L].tobytes()
+            off += L
+            assert framed[i] == orc.chunked_encode(msg, max_chunk=max_chunk), (i, L)
+
+
 def test_egress_stacks_fixture():
     """The first 24 Zipf messages against the committed framed digests."""
     items = FX["stacks"]["items"]
