@@ -10,30 +10,30 @@
 //           256-entry table plus the pos62/pos63 checks (:38-48), skips
 //           non-alphabet bytes and emits a byte per 8 accumulated bits.
 //
-// How it runs here (DESIGN.md §Kernels has the byte budget):
+// How it runs here (DESIGN.md §5 has the byte budget and the rooflines):
 //   * encode is stateless per 3-byte group.  One lane turns 12 input bytes
 //     (one dwordx3 load) into 16 characters (one dwordx4 store); the
-//     64-entry alphabet sits in LDS and is read with ds_read_u8 (the whole
-//     table is 16 dwords, so no two lanes ever hit one bank with different
-//     dwords).  Byte regrouping is v_perm_b32, not shifts.
+//     64-entry alphabet sits in LDS and is read with ds_read_u8.  Byte
+//     regrouping is v_perm_b32, not shifts (k_encode_flat; batches:
+//     k_encode_tight2, k_encode_strided, k_encode_ragged).
 //   * decode is stateful only through the number of alphabet characters
-//     seen so far.  A wave owns a contiguous range of the input and walks
-//     it in 1024-character chunks (16 per lane, one dwordx4 load).  The
-//     fast path -- chunk entirely alphabet, wave aligned to a 4-character
-//     group -- maps through the 256-entry inverse table in LDS and stores
-//     12 bytes per lane (dwordx3).  Anything else (junk, '=', CR/LF, a
-//     partial chunk) takes the exact path: a wave-wide prefix sum of valid
-//     counts compacts the sextets into the wave's LDS scratch, whole
-//     4-sextet groups are emitted and 0-3 sextets carry to the next chunk.
-//   * a single large buffer is split into one range per resident wave.
-//     Pass 1 assumes every earlier range was all-alphabet (true for clean
-//     input) and records each range's valid count; a one-block scan finds
-//     the first range where that assumption broke and the true prefix;
-//     pass 2 re-runs only the ranges after it.  Padding at the end of
-//     clean input never triggers pass 2 (the last range is allowed to be
-//     dirty).
-//   * batches: encode flattens (buffer, 12-byte quad) onto lanes; decode
-//     runs one wave per buffer.
+//     seen so far.  The input is cut into ranges of 2,048 characters, one
+//     wave each.  k_decode_pass1 assumes every earlier range was all
+//     alphabet (true for clean input): it decodes fast-path chunks straight
+//     to their final place, records each range's alphabet count and
+//     publishes the first chunk that is not fast-path.  k_decode_scan2 (a
+//     single-pass decoupled look-back over tiles of 1,024 ranges) turns the
+//     counts into each range's true base when that happened; clean input
+//     exits there.  k_decode_pass2d re-runs the ranges from the first dirty
+//     chunk on: per dword a v_perm compaction of the alphabet bytes, v_dot4
+//     into a left-aligned sextet field, ds_or into the wave's LDS window at
+//     bit 6 x (sextet index) -- the window's bytes are the output bytes --
+//     and a straight copy out.  B64X_DEC_EXPECT_JUNK selects the one-pass
+//     form of the same range body (k_decode_pass2d_t<true>).
+//   * batches: the row kernels (k_decode_rows2 for rows with room) take the
+//     fast paths lane by lane and mark rows with junk once per wave; the
+//     fix-up (k_decode_batch_fix2) decodes the marked rows with pass 2d's
+//     bit-stream step, one wave per row.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
