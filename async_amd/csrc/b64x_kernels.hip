@@ -3392,7 +3392,10 @@ struct b64x_session {
     hipEvent_t decoded;  // recorded after each decode's kernels
     uint64_t cap;
     uint8_t *h_in, *h_out;
+    uint8_t *h_base;     // h_in - kSessionHead (pinned, for in-place decodes)
     uint8_t *d_base;     // d_in - kSessionHead
+    uint64_t last_len;   // characters of the last decode (0: none yet)
+    bool dec_staged;     // the last decode found junk throughout: stage the next
     uint8_t *d_in, *d_out;
     void *d_ws;
     b64x_dec_result *d_res, *h_res;
@@ -3403,6 +3406,10 @@ struct b64x_session {
 // a character the alphabet skips) into the last kCarryHead bytes of it.
 constexpr uint64_t kSessionHead = 256;
 constexpr uint32_t kCarryHead = 16;
+// Pinned slack after host_in: the decode kernels' last vector loads may
+// reach past the input, harmless in a page-rounded hipMalloc, not assumed
+// of host memory read in place.
+constexpr uint64_t kSessionTail = 64;
 
 // One wave: writes the kCarryHead-byte prefix for a decode chained after
 // the HOLD_TAIL decode whose result is *prev (ref base64decoder.c:64-76 --
@@ -3448,7 +3455,8 @@ b64x_session *b64x_session_open(uint64_t capacity)
     const uint64_t ocap = session_out_cap(capacity + kCarryHead);
     const uint64_t wsz = b64x_decode_workspace_size(capacity + kCarryHead);
     bool ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void **) &s->h_in, capacity, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void **) &s->h_base, kSessionHead + capacity + kSessionTail,
+                            hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void **) &s->h_out, ocap, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void **) &s->h_res, sizeof(b64x_dec_result), hipHostMallocDefault) == hipSuccess &&
               hipEventCreateWithFlags(&s->decoded, hipEventDisableTiming) == hipSuccess &&
@@ -3463,6 +3471,7 @@ b64x_session *b64x_session_open(uint64_t capacity)
         return nullptr;
     }
     s->d_in = s->d_base + kSessionHead;
+    s->h_in = s->h_base + kSessionHead;
     return s;
 }
 
@@ -3473,7 +3482,7 @@ void b64x_session_close(b64x_session *s)
     (void) hipGetDevice(&prev);
     (void) hipSetDevice(s->device);
     if (s->stream) (void) hipStreamSynchronize(s->stream);
-    if (s->h_in) (void) hipHostFree(s->h_in);
+    if (s->h_base) (void) hipHostFree(s->h_base);
     if (s->h_out) (void) hipHostFree(s->h_out);
     if (s->h_res) (void) hipHostFree(s->h_res);
     if (s->d_base) (void) hipFree(s->d_base);
@@ -3566,7 +3575,7 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
 // Not for the hub's ragged batches: one block per job is PCIe-latency-bound
 // in place (a single 1 MiB stream ran at half the staged rate).
 // ASYNC_B64_ZERO_COPY=0 stages sessions too.
-static bool zero_copy_encode()
+static bool zero_copy_sessions()
 {
     static const bool on = [] {
         const char *v = getenv("ASYNC_B64_ZERO_COPY");
@@ -3581,7 +3590,7 @@ int b64x_session_encode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
     if (!s || n > s->cap) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    if (n && zero_copy_encode()) {
+    if (n && zero_copy_sessions()) {
         if ((err = b64x_encode_dev(s->h_in, n, s->h_out, abc, s->stream))) return err;
     } else if (n) {
         const uint64_t m = b64x_encoded_len(n, enc_alpha(abc).pad);
@@ -3604,6 +3613,34 @@ static uint8_t skip_char(const b64x_alphabet *abc)
     return '\n';  // unreachable: two characters cannot shadow three
 }
 
+// A session's decode reads host_in and writes host_out in place over PCIe
+// too, unless its last decode found junk throughout (MIME line breaks):
+// pass 2 re-reads the input and pass-1 output where junk is, which in place
+// means a second PCIe crossing.  Clean 256 MiB blocks 22.6 -> 34.5 GiB/s,
+// CRLF-76 ones 21.6 staged against 17.7 in place (scripts/bench_zero_copy.py).
+// The result of the last decode is consulted only once the session's stream
+// has drained, so the policy never waits and never reads a result in flight.
+// A chained decode reads in place only when its carry is already known to be
+// empty (carry_from's stream has drained): the spelled carry head's skip
+// characters displace every range, so pass 2 rewrites the whole block, which
+// in place re-reads all of it over PCIe (32 MiB chained blocks: 13.8 GiB/s in
+// place against 16-36 staged, profiles/r01_host_pipeline_v9.jsonl).  With
+// the carry known empty there is no head at all.
+// ASYNC_B64_ZERO_COPY=0 stages every decode as well.
+constexpr uint64_t kZeroCopyJunk = 64;  // skipped characters beyond the carry head
+
+static bool decode_in_place(b64x_session *s)
+{
+    if (!zero_copy_sessions()) return false;
+    if (s->last_len && hipStreamQuery(s->stream) == hipSuccess) {
+        const uint64_t junk = s->last_len - (s->h_res->valid < s->last_len ? s->h_res->valid
+                                                                            : s->last_len);
+        s->dec_staged = junk > kCarryHead + kZeroCopyJunk;
+        s->last_len = 0;
+    }
+    return !s->dec_staged;
+}
+
 int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
                               unsigned flags, const b64x_session *carry_from,
                               b64x_done_fn done, void *arg)
@@ -3612,10 +3649,16 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
     if (carry_from && carry_from->device != s->device) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    const uint8_t *src = s->d_in;
+    if (carry_from && hipStreamQuery(carry_from->stream) == hipSuccess &&
+        (carry_from->h_res->tail_n == 0 || carry_from->h_res->tail_n >= 4))
+        carry_from = nullptr;  // finished, and nothing to carry (k_spell_carry's rule)
+    const bool in_place = decode_in_place(s) && !carry_from;
+    uint8_t *in = in_place ? s->h_in : s->d_in;
+    uint8_t *out = in_place ? s->h_out : s->d_out;
+    const uint8_t *src = in;
     uint64_t len = n;
-    if (n && (err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice,
-                                           s->stream))))
+    if (n && !in_place &&
+        (err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream))))
         return err;
     if (carry_from) {
         // The carry is spelled on carry_from's stream, right after the decode
@@ -3624,12 +3667,13 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
         // waits for the spelling.  (Spelled on this stream instead, behind an
         // event, the read could lose the race against carry_from's next
         // decode when many streams share the hardware queues.)  The prefix
-        // it writes lies in front of d_in, so it overlaps the H2D above.
+        // it writes lies in front of the input (device or pinned host
+        // headroom), so it overlaps the H2D above.
         const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
         const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
         if ((err = hip_err(hipSetDevice(carry_from->device)))) return err;
         hipLaunchKernelGGL(k_spell_carry, dim3(1), dim3(64), 0, carry_from->stream,
-                           carry_from->d_res, s->d_in - kCarryHead, p62, p63, skip_char(abc));
+                           carry_from->d_res, in - kCarryHead, p62, p63, skip_char(abc));
         if ((err = launch_status())) return err;
         if ((err = hip_err(hipEventRecord(carry_from->decoded, carry_from->stream)))) return err;
         if ((err = hip_err(hipSetDevice(s->device)))) return err;
@@ -3637,15 +3681,17 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
         src -= kCarryHead;
         len += kCarryHead;
     }
-    if ((err = b64x_decode_dev(src, len, s->d_out, s->d_res, abc, flags, s->d_ws, s->stream)))
+    if ((err = b64x_decode_dev(src, len, out, s->d_res, abc, flags, s->d_ws, s->stream)))
         return err;
     if ((err = hip_err(hipEventRecord(s->decoded, s->stream)))) return err;
     if ((err = hip_err(hipMemcpyAsync(s->h_res, s->d_res, sizeof(b64x_dec_result),
                                       hipMemcpyDeviceToHost, s->stream))))
         return err;
+    s->last_len = len;
     // The output length is device-determined: copy the capacity bound.
-    if (len && (err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(len),
-                                             hipMemcpyDeviceToHost, s->stream))))
+    if (len && !in_place &&
+        (err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(len),
+                                      hipMemcpyDeviceToHost, s->stream))))
         return err;
     if (done) return hip_err(hipLaunchHostFunc(s->stream, done, arg));
     return 0;

@@ -59,6 +59,8 @@ def run_resident(src: np.ndarray, block: int, k: int, op: str, total: int):
             n = min(step, total - i * step)
             if op == "encode":
                 s.encode_async(n)
+            elif op == "decode_blocks":  # whole groups, clean: blocks need no carry
+                s.decode_async(n, None, 0)
             else:
                 s.decode_async(n, None, HOLD_TAIL if i + 1 < nblk else 0, carry_from=prev)
             prev = s
@@ -260,6 +262,12 @@ def main():
                           "pcie_GB_s": (total + len(ref_chars)) / dt / 1e9}), flush=True)
         dt = run_resident(ref_chars, block, kk, "decode", len(ref_chars))
         print(json.dumps({"measure": "resident_decode", "bytes": total, "block": block,
+                          "k": kk, "seconds": dt, "GiB_s": total / dt / 2**30,
+                          "pcie_GB_s": (total + len(ref_chars)) / dt / 1e9}), flush=True)
+        # the same blocks decoded without carries (each holds whole groups):
+        # clean input with no carry head reads and writes in place
+        dt = run_resident(ref_chars, block, kk, "decode_blocks", len(ref_chars))
+        print(json.dumps({"measure": "resident_decode_blocks", "bytes": total, "block": block,
                           "k": kk, "seconds": dt, "GiB_s": total / dt / 2**30,
                           "pcie_GB_s": (total + len(ref_chars)) / dt / 1e9}), flush=True)
 

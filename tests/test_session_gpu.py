@@ -19,9 +19,10 @@ def _dirty(rng, n, pad=True, abc=(-1, -1)):
     return sep.join(chars[i:i + 76] for i in range(0, len(chars), 76))
 
 
-def _chained_decode(blocks, abc=(-1, -1), cap=None):
+def _chained_decode(blocks, abc=(-1, -1), cap=None, drain=False):
     """Decode `blocks` through two alternating sessions, queueing each block
-    before the previous one's result is back on the host."""
+    before the previous one's result is back on the host (drain=True: after
+    it, so the library sees the carry on the host)."""
     cap = cap or max(64, max((len(b) for b in blocks), default=0))
     out = []
     with Session(cap) as a, Session(cap) as b:
@@ -36,6 +37,8 @@ def _chained_decode(blocks, abc=(-1, -1), cap=None):
                 pending.pop(0)
             s.host_in[:len(blk)] = np.frombuffer(blk, np.uint8)
             last = i == len(blocks)
+            if drain and prev is not None:
+                prev.wait()
             s.decode_async(len(blk), abc + (True, -1), 0 if last else HOLD_TAIL,
                            carry_from=prev)
             pending.append(s)
@@ -136,3 +139,26 @@ def test_reference_topology_small_slots(monkeypatch):
     enc, dec = res
     assert enc == orc.encode(util.counting(100003).tobytes(), ".", "_", True, "-")
     assert dec == util.counting(100003).tobytes()
+
+
+def test_chained_decode_in_place_and_staged_blocks():
+    """Clean blocks decode in place over PCIe; a session whose last block
+    held junk throughout stages its next one (b64x_session_decode_async).
+    Clean and MIME blocks alternate in one chain, so both forms, and carries
+    spelled into host or device headroom, meet at the seams."""
+    rng = np.random.default_rng(21)
+    chars = orc.encode(rng.integers(0, 256, 300000, dtype=np.uint8).tobytes(), pad=False)
+    blocks = []
+    for i, p in enumerate(range(0, len(chars), 19999)):
+        blk = chars[p:p + 19999]
+        if i % 3 == 1:
+            blk = b"\r\n".join(blk[j:j + 76] for j in range(0, len(blk), 76))
+        blocks.append(blk)
+    stream = b"".join(blocks)
+    assert _chained_decode(blocks) == orc.decode(stream)
+    # Drained chains: empty carries read in place with no carry head, the
+    # rest stage behind a spelled head; ragged cuts give every tail_n.
+    assert _chained_decode(blocks, drain=True) == orc.decode(stream)
+    cuts = np.sort(rng.integers(0, len(stream) + 1, 30))
+    ragged = [stream[i:j] for i, j in zip([0, *cuts], [*cuts, len(stream)])]
+    assert _chained_decode(ragged, drain=True) == orc.decode(stream)
