@@ -3437,6 +3437,21 @@ static uint64_t session_out_cap(uint64_t cap)
     return e > dcap ? e : dcap;
 }
 
+// A session's pinned buffers are fine-grained (hipHostMallocCoherent).
+// host_in/host_out are read and written in place by the kernels (zero-copy),
+// and host_res is the target of the last small D2H copy before the
+// completion callback once the output copy is gone: coarse-grained lines
+// written through an XCD's L2 (a kernel, or a blit copy, whose release is
+// agent-scoped) could still be there when the host callback ran, and the
+// host read a pooled session's previous result -- a block's output length
+// gone stale, so a block went missing from a stream or a stream never
+// finished (600-stream decoder ingress: 1 bad stream + 1 hang in ~84
+// repetitions coarse-grained, 0 in 120 fine-grained,
+// tests/tools/stress_ingress.py).  Fine-grained memory is not held in L2;
+// the host-pipeline rates are unchanged (resident decode blocks 28.1 ->
+// 27.8, encode 31.0 -> 30.9 GiB/s).
+constexpr unsigned kSessionHostFlags = hipHostMallocCoherent;
+
 b64x_session *b64x_session_open(uint64_t capacity)
 {
     if (capacity == 0) {
@@ -3456,9 +3471,9 @@ b64x_session *b64x_session_open(uint64_t capacity)
     const uint64_t wsz = b64x_decode_workspace_size(capacity + kCarryHead);
     bool ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
               hipHostMalloc((void **) &s->h_base, kSessionHead + capacity + kSessionTail,
-                            hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void **) &s->h_out, ocap, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void **) &s->h_res, sizeof(b64x_dec_result), hipHostMallocDefault) == hipSuccess &&
+                            kSessionHostFlags) == hipSuccess &&
+              hipHostMalloc((void **) &s->h_out, ocap, kSessionHostFlags) == hipSuccess &&
+              hipHostMalloc((void **) &s->h_res, sizeof(b64x_dec_result), kSessionHostFlags) == hipSuccess &&
               hipEventCreateWithFlags(&s->decoded, hipEventDisableTiming) == hipSuccess &&
               hipMalloc((void **) &s->d_base, kSessionHead + capacity) == hipSuccess &&
               hipMalloc((void **) &s->d_out, ocap) == hipSuccess &&

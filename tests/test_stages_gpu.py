@@ -96,5 +96,15 @@ def test_many_long_decoder_streams_on_one_loop(monkeypatch):
     msgs[7] = b"\r\n".join(msgs[7][i:i + 76] for i in range(0, len(msgs[7]), 76))
     got, err = util.ingress_stacks(msgs, 4096)
     assert err == 0
+    bad = []
     for i, m in enumerate(msgs):
-        assert got[i] == orc.decode(m), i
+        want = orc.decode(m)
+        if got[i] != want:
+            g = got[i] or b""
+            first = next((j for j in range(min(len(g), len(want))) if g[j] != want[j]),
+                         min(len(g), len(want)))
+            last = max((j for j in range(min(len(g), len(want))) if g[j] != want[j]),
+                       default=-1)
+            bad.append((i, len(m), len(g), len(want), first, last))
+    # (stream, chars, got bytes, want bytes, first/last differing byte)
+    assert not bad, bad
