@@ -3440,16 +3440,12 @@ static uint64_t session_out_cap(uint64_t cap)
 // A session's pinned buffers are fine-grained (hipHostMallocCoherent).
 // host_in/host_out are read and written in place by the kernels (zero-copy),
 // and host_res is the target of the last small D2H copy before the
-// completion callback once the output copy is gone: coarse-grained lines
-// written through an XCD's L2 (a kernel, or a blit copy, whose release is
-// agent-scoped) could still be there when the host callback ran, and the
-// host read a pooled session's previous result -- a block's output length
-// gone stale, so a block went missing from a stream or a stream never
-// finished (600-stream decoder ingress: 1 bad stream + 1 hang in ~84
-// repetitions coarse-grained, 0 in 120 fine-grained,
-// tests/tools/stress_ingress.py).  Fine-grained memory is not held in L2;
-// the host-pipeline rates are unchanged (resident decode blocks 28.1 ->
-// 27.8, encode 31.0 -> 30.9 GiB/s).
+// completion callback once the output copy is gone; fine-grained memory is
+// never held in an XCD's L2, so no fence scope can leave the host a stale
+// line.  Defensive: the rates are unchanged (resident decode blocks 28.1 ->
+// 27.8, encode 31.0 -> 30.9 GiB/s).  It did NOT cure the intermittent
+// missing-block bug of the 600-stream decoder ingress (known
+// issues; tests/tools/stress_ingress.py).
 constexpr unsigned kSessionHostFlags = hipHostMallocCoherent;
 
 b64x_session *b64x_session_open(uint64_t capacity)
@@ -3729,7 +3725,10 @@ void *b64x_host_alloc(uint64_t bytes)
 {
     void *p = nullptr;
     if (!device_info()) return nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    // Fine-grained, like a session's buffers: a lane's decode batch ends on a
+    // small D2H copy of the output lengths right before its host callback
+    // (see kSessionHostFlags).
+    if (hipHostMalloc(&p, bytes ? bytes : 1, kSessionHostFlags) != hipSuccess) return nullptr;
     return p;
 }
 
