@@ -18,7 +18,7 @@ ARCH     ?= gfx950
 # -Wno-pass-failed: k_encode_flat's `#pragma unroll` loops (compile-time trip
 # counts) are reported "not unrolled" after they have already been fully
 # unrolled by an earlier pass; the ISA is the unrolled one.
-HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC \
+HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -Iasync_amd/csrc \
             -Wall -Wno-pass-failed -Iinclude
 CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
 
@@ -37,12 +37,17 @@ HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
 
-all: $(LIB) $(CORE) $(ORACLE) $(HARNESS)
+# The same harness over the product's host C with a CPU stand-in for the GPU
+# side (tests/csrc/fake_b64x.c): deterministic, adversarially ordered tests
+# of the stages' slot accounting, no GPU needed (test infrastructure only).
+FAKE     = tests/csrc/libstage_fake.so
+
+all: $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
 
-$(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) | $(OBJDIR)
+$(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h | $(OBJDIR)
@@ -62,7 +67,13 @@ $(HARNESS): tests/csrc/stage_harness.c $(LIB) $(HEADERS)
 	    -Lasync_amd -lasync_b64 -Wl,-rpath,'$$ORIGIN/../../async_amd' \
 	    -L/opt/rocm/lib -lamdhip64 -lpthread
 
+$(FAKE): tests/csrc/stage_harness.c tests/csrc/fake_b64x.c oracle/b64_oracle.c $(HOST_SRC) $(HEADERS) \
+         async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h async_amd/csrc/b64x_result_check.h
+	$(CC) $(CFLAGS) -Ioracle -Iasync_amd/csrc -shared -o $@ tests/csrc/stage_harness.c \
+	    tests/csrc/fake_b64x.c oracle/b64_oracle.c $(HOST_SRC) -lpthread
+
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS)
+	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE)
 
 .PHONY: all clean
+

@@ -86,6 +86,7 @@ SIGNATURES = {
     "b64x_session_encode_async": (_int, [_vp, _u64, _ap, _vp, _vp]),
     "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp, _vp]),
     "b64x_session_result": (ctypes.POINTER(DecResult), [_vp]),
+    "b64x_session_decode_result": (_int, [_vp, ctypes.POINTER(DecResult)]),
     "b64x_session_wait": (_int, [_vp]),
     "b64x_host_alloc": (_vp, [_u64]),
     "b64x_host_free": (None, [_vp]),
@@ -94,8 +95,11 @@ SIGNATURES = {
     "b64x_lane_acquire": (_vp, []),
     "b64x_lane_release": (None, [_vp]),
     "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp, _vp]),
-    "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _ap, _vp, _vp]),
+    "b64x_lane_encode_check": (_int, [_vp]),
+    "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _ap, _vp, _vp]),
+    "b64x_lane_decode_check": (_int, [_vp, _vp, _vp, _vp, _u32]),
     "b64x_lane_wait": (_int, [_vp]),
+    "b64x_diag_counters": (None, [ctypes.POINTER(_u64)]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),
     "b64x_build_info": (ctypes.c_char_p, []),

@@ -31,6 +31,8 @@ enum {
                                      stages are made to wait */
     POOL_MAX = 16,          /* idle arenas kept process-wide for reuse */
     HUB_JOBS = 1 << 16,     /* jobs per arena */
+    HUB_DEPTH = 8,          /* reservations open at once (stages reading
+                               through stages, see b64_hub_reserve) */
 };
 
 typedef enum { B_FREE, B_FILLING, B_READY, B_INFLIGHT, B_DONE } batch_state;
@@ -40,7 +42,8 @@ struct b64_batch {
     b64_batch *next;             /* ready / free list */
     uint8_t *h_in, *h_out;       /* pinned arenas */
     uint64_t *h_in_off, *h_out_off; /* pinned, HUB_JOBS + 1 each */
-    uint64_t *h_outlen;          /* pinned, HUB_JOBS: decode byte counts */
+    uint8_t *h_flags;            /* pinned, HUB_JOBS: decode jobs' flags */
+    b64x_dec_result *h_res;      /* pinned, HUB_JOBS: decode jobs' records */
     b64_hub_kind kind;
     b64_ticket **jobs;
     size_t in_cap, out_cap;
@@ -60,7 +63,8 @@ struct b64_hub {
     int efd;
     b64x_lane *lanes[HUB_LANES];
     b64_batch *running[HUB_LANES];
-    b64_batch *filling;
+    b64_batch *filling[HUB_DEPTH]; /* the open arena of each nesting level */
+    unsigned depth;              /* reservations open (gathers in progress) */
     b64_batch *ready, *ready_tail;
     unsigned inflight;
     unsigned live;               /* arenas taken from the pool */
@@ -72,11 +76,6 @@ struct b64_hub {
     size_t nwaiters, waiters_cap;
     action_1 *kicking;           /* the list hub_kick() is working through */
     size_t nkicking;
-    pthread_mutex_t post_lock;   /* guards posted: HIP callback threads push */
-    action_1 *posted;
-    size_t nposted, posted_cap;
-    action_1 *draining;          /* the posted list hub_wake() is running */
-    size_t ndraining;
     struct {                     /* ASYNC_B64_HUB_TRACE=1: printed at teardown */
         bool on;
         unsigned long batches, jobs, allocs, wake_calls, max_ready;
@@ -119,7 +118,8 @@ static void batch_free(b64_batch *b)
     b64x_host_free(b->h_out);
     b64x_host_free(b->h_in_off);
     b64x_host_free(b->h_out_off);
-    b64x_host_free(b->h_outlen);
+    b64x_host_free(b->h_flags);
+    b64x_host_free(b->h_res);
     free(b->jobs);
     free(b);
 }
@@ -137,9 +137,11 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     b->h_out = b64x_host_alloc(b->out_cap);
     b->h_in_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
     b->h_out_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
-    b->h_outlen = b64x_host_alloc(HUB_JOBS * sizeof(uint64_t));
+    b->h_flags = b64x_host_alloc(HUB_JOBS);
+    b->h_res = b64x_host_alloc(HUB_JOBS * sizeof(b64x_dec_result));
     b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
-    if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_outlen || !b->jobs) {
+    if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_flags || !b->h_res ||
+        !b->jobs) {
         batch_free(b);
         errno = ENOMEM;
         return NULL;
@@ -214,12 +216,12 @@ static void batch_done(void *arg)
 
 /* ------------------------------------------------------------ scheduling */
 
-static void seal(b64_hub *h)
+static void seal(b64_hub *h, unsigned level)
 {
-    b64_batch *b = h->filling;
+    b64_batch *b = h->filling[level];
     if (!b)
         return;
-    h->filling = NULL;
+    h->filling[level] = NULL;
     b->state = B_READY;
     b->next = NULL;
     if (h->ready_tail)
@@ -255,8 +257,8 @@ static void launch_ready(b64_hub *h)
         if (!rc)
             rc = b->kind == B64_HUB_DECODE
                      ? b64x_lane_decode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
-                                              b->h_out, b->h_out_off, b->h_outlen, &b->abc,
-                                              batch_done, b)
+                                              b->h_out, b->h_out_off, b->h_flags, b->h_res,
+                                              &b->abc, batch_done, b)
                      : b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
                                               b->h_out, b->h_out_off, &b->abc, batch_done, b);
         if (rc) { /* report through the normal completion path */
@@ -292,8 +294,9 @@ static void hub_flush(b64_hub *h)
             hub_destroy(h);
         return;
     }
-    if (h->filling && h->filling->njobs)
-        seal(h);
+    for (unsigned l = 0; l < HUB_DEPTH; l++)
+        if (h->filling[l] && h->filling[l]->njobs && l >= h->depth)
+            seal(h, l);
     launch_ready(h);
 }
 
@@ -380,8 +383,10 @@ static void complete(b64_hub *h, b64_batch *b, bool collect)
         if (!t)
             continue;
         t->out = b->h_out + b->h_out_off[j];
-        if (b->kind == B64_HUB_DECODE)
-            t->out_len = b->err ? 0 : (size_t) b->h_outlen[j];
+        if (b->kind == B64_HUB_DECODE && !b->err) {
+            t->res = b->h_res[j];
+            t->out_len = (size_t) t->res.out_len;
+        }
         t->err = b->err;
         atomic_store_explicit(&t->done, 1, memory_order_release);
         if (collect)
@@ -405,6 +410,14 @@ static void hub_wake(b64_hub *h)
         if (b && atomic_load_explicit(&b->done, memory_order_acquire)) {
             h->running[i] = NULL;
             h->inflight--;
+            /* the batch's records or completion stamp, checked (and
+             * waited for, should the callback have come early) before
+             * anything of it is read */
+            if (!b->err)
+                b->err = b->kind == B64_HUB_DECODE
+                             ? b64x_lane_decode_check(h->lanes[i], b->h_in_off, b->h_flags,
+                                                      b->h_res, b->njobs)
+                             : b64x_lane_encode_check(h->lanes[i]);
             complete(h, b, true);
         }
     }
@@ -415,21 +428,6 @@ static void hub_wake(b64_hub *h)
     size_t n = h->nwakes;
     for (size_t i = 0; i < n; i++)
         action_1_perf(h->wakes[i]);
-    /* actions posted from other threads (session completions) */
-    pthread_mutex_lock(&h->post_lock);
-    action_1 *p = h->posted;
-    size_t np = h->nposted;
-    h->posted = NULL;
-    h->nposted = h->posted_cap = 0;
-    pthread_mutex_unlock(&h->post_lock);
-    h->draining = p;
-    h->ndraining = np;
-    for (size_t i = 0; i < np && !h->doomed; i++)
-        if (p[i].act) /* NULL: forgotten, its stage closed meanwhile */
-            action_1_perf(p[i]);
-    h->draining = NULL;
-    h->ndraining = 0;
-    free(p);
     h->in_wake = false;
     if (h->tr.on) {
         h->tr.wake_calls++;
@@ -472,7 +470,6 @@ b64_hub *b64_hub_acquire(async_t *async)
         errno = e;
         return NULL;
     }
-    pthread_mutex_init(&h->post_lock, NULL);
     h->users = 1;
     h->next_hub = registry;
     registry = h;
@@ -506,8 +503,9 @@ static void hub_destroy(b64_hub *h)
         }
         b64x_lane_release(h->lanes[i]);
     }
-    if (h->filling)
-        batch_put(h->filling);
+    for (unsigned l = 0; l < HUB_DEPTH; l++)
+        if (h->filling[l])
+            batch_put(h->filling[l]);
     while (h->ready) {
         b64_batch *b = h->ready;
         h->ready = b->next;
@@ -517,8 +515,6 @@ static void hub_destroy(b64_hub *h)
     close(h->efd);
     free(h->wakes);
     free(h->waiters);
-    free(h->posted);
-    pthread_mutex_destroy(&h->post_lock);
     free(h);
 }
 
@@ -533,34 +529,8 @@ void b64_hub_release(b64_hub *h)
         hub_destroy(h);
 }
 
-void b64_hub_post(b64_hub *h, action_1 a)
-{
-    pthread_mutex_lock(&h->post_lock);
-    if (h->nposted == h->posted_cap) {
-        size_t cap = h->posted_cap ? 2 * h->posted_cap : 64;
-        action_1 *p = realloc(h->posted, cap * sizeof *p);
-        if (!p)
-            abort();
-        h->posted = p;
-        h->posted_cap = cap;
-    }
-    h->posted[h->nposted++] = a;
-    pthread_mutex_unlock(&h->post_lock);
-    uint64_t one = 1;
-    ssize_t rc = write(h->efd, &one, sizeof one);
-    (void) rc; /* EAGAIN only when the counter is saturated: still readable */
-}
-
 void b64_hub_forget(b64_hub *h, void *obj, bool waiting)
 {
-    pthread_mutex_lock(&h->post_lock);
-    for (size_t i = 0; i < h->nposted; i++)
-        if (h->posted[i].obj == obj)
-            h->posted[i].act = NULL;
-    pthread_mutex_unlock(&h->post_lock);
-    for (size_t i = 0; i < h->ndraining; i++)
-        if (h->draining[i].obj == obj)
-            h->draining[i].act = NULL;
     if (!waiting)
         return;
     for (size_t i = 0; i < h->nkicking; i++)
@@ -575,21 +545,34 @@ void b64_hub_forget(b64_hub *h, void *obj, bool waiting)
 
 /* -------------------------------------------------------------- the API */
 
+/*
+ * Reservations nest: a stage gathers its block from upstream while holding
+ * its reservation, and that upstream may itself be a base64 stage on the
+ * same loop reserving its own block (the reference test's decoder reads
+ * through nice(91) from the encoder, test/asynctest-base64encoder.c:
+ * 123-151).  Each open reservation has its own arena (filling[depth]), so
+ * an inner reservation never moves, seals or recycles an outer one.
+ */
 uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
                          size_t room, size_t min_room, size_t *granted, action_1 waiter)
 {
+    if (h->depth == HUB_DEPTH) {
+        errno = ELOOP; /* stages nested deeper than HUB_DEPTH */
+        return NULL;
+    }
+    const unsigned lv = h->depth;
     if (min_room > room)
         min_room = room;
-    b64_batch *b = h->filling;
+    b64_batch *b = h->filling[lv];
     if (b && (b->kind != kind || memcmp(&b->abc, abc, sizeof *abc) || b->njobs == HUB_JOBS ||
               b->in_cap - b->in_used < (min_room ? min_room : 1))) {
         if (b->njobs) {
-            seal(h);
+            seal(h, lv);
             launch_ready(h);
         }
-        b = h->filling; /* NULL after seal; kept if it was empty */
+        b = h->filling[lv]; /* NULL after seal; kept if it was empty */
         if (b && (b->in_cap < room || b->kind != kind || memcmp(&b->abc, abc, sizeof *abc))) {
-            h->filling = NULL;
+            h->filling[lv] = NULL;
             batch_put(b);
             h->live--;
             b = NULL;
@@ -615,18 +598,20 @@ uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc
         b->state = B_FILLING;
         b->abc = *abc;
         b->kind = kind;
-        h->filling = b;
+        h->filling[lv] = b;
     }
     size_t avail = b->in_cap - b->in_used;
     *granted = room < avail ? room : avail;
+    h->depth++;
     return b->h_in + b->in_used;
 }
 
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
-                    action_1 wake)
+                    unsigned flags, action_1 wake)
 {
-    b64_batch *b = h->filling;
+    b64_batch *b = h->filling[--h->depth];
     uint32_t j = b->njobs++;
+    b->h_flags[j] = (uint8_t) flags;
     b->h_in_off[j] = b->in_used;
     b->in_used += n;
     b->h_in_off[j + 1] = b->in_used;
@@ -647,7 +632,7 @@ void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
 
 void b64_hub_cancel(b64_hub *h)
 {
-    (void) h; /* nothing was recorded */
+    h->depth--; /* nothing was recorded */
 }
 
 void b64_ticket_release(b64_ticket *t)

@@ -1,18 +1,20 @@
 /*
- * b64_hub.h -- internal: cross-stream batching of encoder blocks, and of
- * short decoder streams, for one event loop.
+ * b64_hub.h -- internal: cross-stream batching of encoder and decoder
+ * blocks for one event loop.
  *
- * Every base64 encoder stage on an async_t shares one hub.  A stage
- * reserves room in the hub's open pinned arena, reads its upstream
- * straight into it, and commits the block as a job; the hub launches the
- * arena as one ragged batch (b64x_lane_encode_async: H2D, one kernel, D2H)
- * when the arena fills or at the end of the current loop turn, on up to
- * B64_HUB_LANES concurrent HIP streams.  Completion comes back through one
- * eventfd registered with async_register(); the hub marks each job's
- * ticket done and calls the stage's wake action.
+ * Every base64 stage on an async_t shares one hub.  A stage reserves room
+ * in the hub's open pinned arena, reads its upstream straight into it, and
+ * commits the block as a job; the hub launches the arena as one ragged
+ * batch (b64x_lane_encode_async / _decode_async: one H2D, the kernels
+ * writing their outputs straight into the pinned arena) when the arena
+ * fills or at the end of the current loop turn, on up to 4 concurrent HIP
+ * streams ("lanes").  Completion comes back through one eventfd registered
+ * with async_register(); the hub checks the batch (b64x_lane_*_check),
+ * marks each job's ticket done and calls the stage's wake action.
  *
  * Many small messages (config 5: Zipf 64 B - 1 MiB) thus cost one launch
- * and two copies per arena instead of per message.
+ * and one copy per arena instead of per message, and a loop's thousands of
+ * streams hold no HIP stream of their own.
  */
 #ifndef ASYNC_AMD_B64_HUB_H
 #define ASYNC_AMD_B64_HUB_H
@@ -37,6 +39,7 @@ typedef struct {
     int err;               /* negative errno if the batch failed */
     const uint8_t *out;    /* the block's output, valid once done */
     size_t out_len;        /* decode jobs: the bytes decoded (device count) */
+    b64x_dec_result res;   /* decode jobs: the job's checked result record */
     action_1 wake;         /* performed on the loop when done */
 } b64_ticket;
 
@@ -52,7 +55,10 @@ void b64_hub_release(b64_hub *h);
 /* Room for one block of at most `room` bytes, at least `min_room`, encoded
  * with `abc`; returns where to write it, or NULL + errno.  *granted gets
  * the room actually given.  Must be followed by commit or cancel before
- * control returns to the loop.  Backpressure: when the hub already holds
+ * control returns to the loop.  Reservations nest (the caller may read
+ * upstream through other stages of the same hub while holding one, up to 8
+ * deep, ELOOP beyond): each open reservation has its own arena.
+ * Backpressure: when the hub already holds
  * its share of arenas and a new one is needed, a caller passing a
  * `waiter` (a stage with nothing staged or in flight) gets NULL/EAGAIN and
  * the waiter is performed once an arena is recycled; NULL_ACTION_1-like
@@ -60,20 +66,18 @@ void b64_hub_release(b64_hub *h);
  * are always served. */
 uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
                          size_t room, size_t min_room, size_t *granted, action_1 waiter);
-/* Drop any posted action -- and, when `waiting` (it may be on the waiter
- * list), any waiter -- whose object is `obj` (its stage is closing).  The
- * waiter lists can hold thousands of stages: scanning them on every close
- * would be quadratic. */
+/* When `waiting` (the stage may be on the waiter list): drop any waiter
+ * whose object is `obj` (its stage is closing).  The waiter lists can hold
+ * thousands of stages: scanning them on every close would be quadratic. */
 void b64_hub_forget(b64_hub *h, void *obj, bool waiting);
-/* Any thread (a HIP host callback): perform `a` on the loop at the hub's
- * next wake-up.  The poster must not outlive its b64_hub_forget(). */
-void b64_hub_post(b64_hub *h, action_1 a);
 /* Turn the reservation into a job of n bytes -> out_len characters
- * (encode) or of n characters -> at most out_len bytes (decode: a whole
- * stream, its final partial group emitted; the count lands in
- * ticket->out_len). */
+ * (encode) or of n characters -> at most out_len bytes (decode; `flags`
+ * B64X_DEC_HOLD_TAIL when more of the stream follows: whole groups only,
+ * the last V mod 4 sextets reported; 0 ends the stream: its final partial
+ * group emitted).  A decode job's record lands in ticket->res, its byte
+ * count in ticket->out_len. */
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
-                    action_1 wake);
+                    unsigned flags, action_1 wake);
 void b64_hub_cancel(b64_hub *h);
 /* The stage is done with the ticket (consumed, or closing before the
  * batch finished: its output is then discarded). */

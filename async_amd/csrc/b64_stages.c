@@ -6,34 +6,35 @@
  * Reference: src/base64encoder.c and src/base64decoder.c.  The reference
  * transforms in place inside the caller's buffer, one byte per loop trip
  * (encoder :101-142, decoder :52-80), synchronously inside read().  Here a
- * stage is a small pipeline of two slots, each a b64x session (pinned host
- * staging + device buffers + a HIP stream):
+ * stage is a small pipeline of up to NSLOTS blocks, each a job of a batch
+ * of the loop's hub (b64_hub.h), which packs the blocks of every stage on
+ * the loop into one ragged GPU launch:
  *
- *   read() --> serve the oldest finished slot
- *          --> top up: pull upstream into an idle slot's pinned buffer and
- *              queue H2D + kernels + D2H on its stream (read-ahead: both
- *              slots can be in flight while the consumer drains a third
- *              block's worth of output)
+ *   read() --> serve the oldest finished block
+ *          --> top up: pull upstream straight into the hub's pinned arena
+ *              and commit the block as a job
  *          --> nothing finished yet: -1 / EAGAIN.
  *
- *   GPU completion: a HIP host function marks the slot finished and posts
- *   the stage on the loop's hub, whose one eventfd is registered with
- *   async_register(), so the loop calls the stage, which calls the
- *   consumer's registered
+ *   GPU completion: a HIP host function writes the hub's eventfd, which is
+ *   registered with async_register(); the loop checks the batch, marks its
+ *   jobs done and calls each stage, which calls the consumer's registered
  *   callback -- the same "EAGAIN now, callback later" contract every
- *   bytestream_1 in the reference follows.
+ *   bytestream_1 in the reference follows.  A
+ *   stage holds no HIP stream, event or session of its own.
  *
  * Group carries:
  *  - encoder: whole 3-byte groups are encoded; the 0-2 leftover bytes are
  *    carried on the host into the next block, and encoded with the final
  *    padding once upstream reports EOF (the reference's finalize(),
  *    :61-99);
- *  - decoder: blocks are decoded with B64X_DEC_HOLD_TAIL; the 0-3 sextets
- *    a block leaves over are device-determined, so the next block is
- *    chained on the device (b64x_session_decode_async(carry_from)) instead
- *    of waiting for the result on the host; at EOF the last block (or an
- *    empty flush) is decoded without HOLD_TAIL, giving the reference's
- *    floor(6V/8) bytes overall.
+ *  - decoder: blocks are decoded with B64X_DEC_HOLD_TAIL; the device
+ *    reports the 0-3 sextets a block leaves over (its result record), and
+ *    the stage spells them as alphabet characters in a 4-byte head in
+ *    front of the stream's next block (the reference keeps those bits in
+ *    decoder->bits across reads, :64-76).  So a decoder stream has one
+ *    block on the GPU at a time; finished blocks still queue up for the
+ *    consumer.  At EOF the last block (or a head alone) is decoded without
+ *    HOLD_TAIL, giving the reference's floor(6V/8) bytes overall.
  *
  * The byte stream each stage produces is the reference's, byte for byte,
  * and the encoder's per-read counts are too whenever upstream keeps up
@@ -45,11 +46,19 @@
  * 4) has no counterpart.  With no usable GPU the first read fails with
  * ENODEV: there is no CPU path.
  *
+ * Round 1 ran decoder blocks past the first on per-stage chained sessions
+ * (a HIP stream, pinned buffers and a device carry chain each); under load
+ * (600 streams on one loop) a block's result record copied back from the
+ * device was read before it held the launch's values, and the block was
+ * served as empty.  Every block now goes through the hub,
+ * whose kernels write outputs and records into host memory themselves and
+ * whose batches are checked before they are read.
+ *
  * Tuning (environment, read when a stage is created):
- *   ASYNC_B64_STAGE_CAPACITY  staging bytes per slot (default 1 MiB; the
- *                             encoder grows it to hold its first read's
- *                             count, up to ASYNC_B64_STAGE_MAX_CAPACITY,
- *                             default 64 MiB)
+ *   ASYNC_B64_STAGE_CAPACITY  bytes per block (default 1 MiB; the encoder
+ *                             grows it to hold its first read's count, up
+ *                             to ASYNC_B64_STAGE_MAX_CAPACITY, default
+ *                             64 MiB)
  *   ASYNC_B64_MIN_PULL        gather at least this much from upstream
  *                             before launching, unless it runs dry
  *                             (default 64 KiB)
@@ -69,21 +78,21 @@
 #include "base64decoder.h"
 #include "base64encoder.h"
 
-enum { NSLOTS = 4 }; /* blocks in flight or staged per stage (read-ahead) */
+enum {
+    NSLOTS = 4,   /* blocks in flight or staged per stage (read-ahead) */
+    DEC_HEAD = 4, /* decoder: characters in front of a block for the carry */
+};
 
 typedef struct stage stage;
 
 typedef struct {
     stage *owner;
-    b64x_session *sess; /* decoder: this slot's session */
-    b64_ticket ticket;  /* encoder, and a short decoder stream: this slot's
-                           job in a hub batch */
-    bool hubbed;        /* decoder: the slot's block went through the hub */
-    atomic_int done;    /* decoder: set by the HIP host function */
-    bool resolved;    /* out_len/body_end valid (decoder: after done) */
+    b64_ticket ticket;  /* this slot's job in a hub batch */
+    bool hold;          /* decoder: more of the stream follows this block */
+    bool resolved;      /* out_len/body_end valid (decoder: after done) */
     size_t out_pos;
-    size_t body_end;  /* encoder: end of the full sextets; the finalize
-                         characters after it are served on their own */
+    size_t body_end;    /* encoder: end of the full sextets; the finalize
+                           characters after it are served on their own */
     size_t out_len;
 } slot;
 
@@ -97,22 +106,19 @@ struct stage {
     b64x_alphabet abc;
     size_t cap, min_pull, max_cap;
     b64_hub *hub;       /* the loop's batching hub */
-    bool hub_first;     /* decoder: the first block may go through the hub
-                           (a stream that ends inside it is one job) */
-    atomic_bool wake_posted; /* decoder: a session completion is queued
-                                on the hub for this stage */
     unsigned hub_waits; /* entries on the hub's waiter list (room for a block) */
-    bool started;       /* the hub (and any sessions) are held */
+    bool started;       /* the hub is held */
     int err;            /* sticky failure errno, 0 while healthy */
     slot slots[NSLOTS];
     unsigned head;      /* oldest busy slot */
     unsigned nbusy;     /* launched, output not fully served */
     bool final_queued;  /* the last block (or nothing) has been launched */
-    bool launched_any;
     bool short_seen;    /* an upstream read came up short (not EAGAIN)
                            since the staged output last ran out */
-    uint8_t carry[2];   /* encoder: bytes of the incomplete group */
+    uint8_t carry[3];   /* encoder: bytes of the incomplete group;
+                           decoder: sextets the last block held back */
     size_t ncarry;
+    uint8_t skip;       /* decoder: a character its alphabet skips */
     bool lend_want;     /* this read may lend instead of copy (b64_lend.h) */
     uint8_t *spill;     /* lent copy of reads that span blocks (no fallback) */
     size_t spill_cap;
@@ -131,6 +137,42 @@ static size_t env_size(const char *name, size_t dflt, size_t lo)
     return (size_t) x;
 }
 
+/* The decoder alphabet's effective positions 62/63 ((char) -1 = the
+ * reference's defaults, base64decoder.c:31-32). */
+static char dec_pos62(const b64x_alphabet *abc)
+{
+    return abc->pos62 == (char) -1 ? '+' : abc->pos62;
+}
+
+static char dec_pos63(const b64x_alphabet *abc)
+{
+    return abc->pos63 == (char) -1 ? '/' : abc->pos63;
+}
+
+/* A byte the decoder skips (ref map(), base64decoder.c:38-48: not
+ * alphanumeric and not pos62/pos63). */
+static uint8_t skip_char(const b64x_alphabet *abc)
+{
+    const char cand[3] = { '\n', '\r', ' ' };
+    for (int i = 0; i < 3; i++)
+        if (cand[i] != dec_pos62(abc) && cand[i] != dec_pos63(abc))
+            return (uint8_t) cand[i];
+    return '\n'; /* unreachable: two characters cannot shadow three */
+}
+
+/* A sextet as a character that decodes back to it.  62 and 63 only reach
+ * a carry when the decoder recognised them, i.e. through pos62/pos63. */
+static uint8_t spell_sextet(const b64x_alphabet *abc, uint8_t v)
+{
+    if (v < 26)
+        return (uint8_t) ('A' + v);
+    if (v < 52)
+        return (uint8_t) ('a' + (v - 26));
+    if (v < 62)
+        return (uint8_t) ('0' + (v - 52));
+    return (uint8_t) (v == 62 ? dec_pos62(abc) : dec_pos63(abc));
+}
+
 static void stage_init(stage *st, async_t *async, bytestream_1 up,
                        direction dir, b64x_alphabet abc)
 {
@@ -143,6 +185,7 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
     st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
     st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
+    st->skip = skip_char(&abc);
     for (int i = 0; i < NSLOTS; i++)
         st->slots[i].owner = st;
 }
@@ -162,25 +205,6 @@ static void stage_kicked(stage *st)
     action_1_perf(st->cb);
 }
 
-/* Loop side of a session completion (posted through the loop's hub: one
- * eventfd per loop, not one per stage -- thousands of decoder streams
- * would otherwise hold a descriptor each). */
-static void stage_posted(stage *st)
-{
-    atomic_store_explicit(&st->wake_posted, false, memory_order_relaxed);
-    action_1_perf(st->cb);
-}
-
-/* HIP runtime thread: publish, then signal (once until the loop runs it). */
-static void slot_done(void *arg)
-{
-    slot *sl = arg;
-    stage *st = sl->owner;
-    atomic_store_explicit(&sl->done, 1, memory_order_release);
-    if (!atomic_exchange_explicit(&st->wake_posted, true, memory_order_acq_rel))
-        b64_hub_post(st->hub, (action_1) { st, (act_1) stage_posted });
-}
-
 /* Hub completion of one of this stage's blocks (on the loop). */
 static void stage_notify(stage *st)
 {
@@ -193,48 +217,25 @@ static int stage_start(stage *st, size_t count)
         return 0;
     if (st->dir == DIR_ENCODE) {
         /* A fresh block must be able to hold a full read (see
-         * stage_read()); blocks go to the loop's hub. */
+         * stage_read()). */
         size_t need = (count + 3) / 4 * 3 + 3;
         if (need > st->max_cap)
             need = st->max_cap;
         if (need > st->cap)
             st->cap = need;
-        int rc = b64x_device_check(); /* fail loudly: no CPU path */
-        if (rc)
-            return rc;
-        st->hub = b64_hub_acquire(st->async);
-        if (!st->hub)
-            return -(errno ? errno : ENODEV);
-        st->started = true;
-        return 0;
     }
-    /* A stream that ends inside its first block is decoded as one job of
-     * a hub batch (many short streams, one launch); longer streams take
-     * sessions, from the process-wide pool as slots are first used, whose
-     * completions come back through the hub's eventfd too (a descriptor
-     * per stage would cap a loop at ~1,000 decoder streams and cost
-     * fd-table expansions). */
     int rc = b64x_device_check(); /* fail loudly: no CPU path */
     if (rc)
         return rc;
     st->hub = b64_hub_acquire(st->async);
     if (!st->hub)
         return -(errno ? errno : ENODEV);
-    st->hub_first = true;
     st->started = true;
     return 0;
 }
 
 static void stage_stop(stage *st)
 {
-    /* sessions first: a release waits for the session's work, so no
-     * completion can be posted for this stage after the forget below */
-    for (int i = 0; i < NSLOTS; i++) {
-        if (st->slots[i].sess) {
-            b64x_session_release(st->slots[i].sess); /* waits, then pools */
-            st->slots[i].sess = NULL;
-        }
-    }
     if (st->hub) {
         b64_hub_forget(st->hub, st, st->hub_waits > 0);
         for (int i = 0; i < NSLOTS; i++)
@@ -285,8 +286,8 @@ static slot *next_launch_slot(stage *st)
 
 static void slot_arm(stage *st, slot *sl)
 {
-    atomic_store_explicit(&sl->done, 0, memory_order_relaxed);
     sl->resolved = false;
+    sl->hold = false;
     sl->out_pos = sl->body_end = sl->out_len = 0;
     st->nbusy++;
 }
@@ -305,6 +306,28 @@ static size_t finalize_len(size_t n, bool pad)
     }
 }
 
+/* Backpressure: a stage may be made to wait for an arena unless it holds
+ * finished output that cannot be served without more input (it must make
+ * progress, or arenas could stay pinned by partially read jobs forever). */
+static action_1 hub_waiter(stage *st)
+{
+    bool must_progress = st->nbusy > 0;
+    for (unsigned i = 0; i < st->nbusy && must_progress; i++)
+        if (!atomic_load_explicit(&st->slots[(st->head + i) % NSLOTS].ticket.done,
+                                  memory_order_acquire))
+            must_progress = false; /* a completion will wake us */
+    if (must_progress)
+        return (action_1) { NULL, NULL };
+    return (action_1) { st, (act_1) stage_kicked };
+}
+
+static int reserve_failed(stage *st, action_1 waiter)
+{
+    if (errno == EAGAIN && waiter.act)
+        st->hub_waits++;
+    return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
+}
+
 /* Launch as many blocks as slots and upstream allow.  Returns 0, or a
  * positive errno from upstream (EAGAIN included) that stopped it, or a
  * negative errno from the GPU side. */
@@ -316,25 +339,11 @@ static int top_up_encoder(stage *st)
          * will do (the next block gets a fresh arena and a full slot, so
          * two slots always cover a full read). */
         size_t room;
-        /* Backpressure: a stage may be made to wait for an arena unless
-         * it holds finished output that cannot be served without more
-         * input (it must make progress, or arenas could stay pinned by
-         * partially read jobs forever). */
-        bool must_progress = st->nbusy > 0;
-        for (unsigned i = 0; i < st->nbusy && must_progress; i++)
-            if (!atomic_load_explicit(&st->slots[(st->head + i) % NSLOTS].ticket.done,
-                                      memory_order_acquire))
-                must_progress = false; /* a completion will wake us */
-        action_1 waiter = { NULL, NULL };
-        if (!must_progress)
-            waiter = (action_1) { st, (act_1) stage_kicked };
+        action_1 waiter = hub_waiter(st);
         uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_ENCODE, &st->abc, st->cap,
                                       st->ncarry + 4096, &room, waiter);
-        if (!in) {
-            if (errno == EAGAIN && waiter.act)
-                st->hub_waits++;
-            return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
-        }
+        if (!in)
+            return reserve_failed(st, waiter);
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;
@@ -365,7 +374,7 @@ static int top_up_encoder(stage *st)
         }
         slot_arm(st, sl);
         sl->out_len = (size_t) b64x_encoded_len(total, st->abc.pad);
-        b64_hub_commit(st->hub, &sl->ticket, total, sl->out_len,
+        b64_hub_commit(st->hub, &sl->ticket, total, sl->out_len, 0,
                        (action_1) { st, (act_1) stage_notify });
         sl->out_pos = skip;
         sl->body_end = total * 8 / 6;
@@ -380,100 +389,47 @@ static int top_up_encoder(stage *st)
     return 0;
 }
 
-/* The first block of a decoder stream through the hub: a stream that
- * ends inside it is one job (its final partial group emitted, like the
- * reference at EOF); one that does not moves what was gathered into a
- * session and continues on sessions.  Returns as top_up does, or 1 when
- * the caller should launch `*moved` bytes already in sl's session. */
-static int decoder_first_via_hub(stage *st, slot *sl, size_t *moved)
-{
-    *moved = 0;
-    action_1 waiter = { st, (act_1) stage_kicked };
-    size_t room;
-    uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_DECODE, &st->abc, st->cap, 4096, &room,
-                                  waiter);
-    if (!in) {
-        if (errno == EAGAIN)
-            st->hub_waits++;
-        return errno == EAGAIN ? EAGAIN : -(errno ? errno : ENOMEM);
-    }
-    bool eof;
-    int uerr;
-    size_t got = gather(st, in, room, &eof, &uerr);
-    if (eof) {
-        st->final_queued = true;
-        st->hub_first = false;
-        if (got == 0) {
-            b64_hub_cancel(st->hub);
-            return 0;
-        }
-        slot_arm(st, sl);
-        sl->hubbed = true;
-        b64_hub_commit(st->hub, &sl->ticket, got, (got + 3) / 4 * 3,
-                       (action_1) { st, (act_1) stage_notify });
-        st->launched_any = true;
-        return 0;
-    }
-    if (got == 0) {
-        b64_hub_cancel(st->hub);
-        return uerr ? uerr : EAGAIN;
-    }
-    /* more than a block, or upstream paused: the session path from here */
-    st->hub_first = false;
-    if (!sl->sess && !(sl->sess = b64x_session_acquire(st->cap))) {
-        b64_hub_cancel(st->hub);
-        return -(errno ? errno : ENOMEM);
-    }
-    memcpy(b64x_session_host_in(sl->sess), in, got);
-    b64_hub_cancel(st->hub);
-    *moved = got;
-    return 1;
-}
+static bool slot_ready(slot *sl);
 
+/* Decoder blocks: each one a hub job of DEC_HEAD + n characters, the head
+ * spelling the sextets the previous block held back (skip characters when
+ * none), so a block is launched once the one before it has finished. */
 static int top_up_decoder(stage *st)
 {
     slot *sl;
     while ((sl = next_launch_slot(st))) {
-        size_t moved = 0;
-        if (st->hub_first && !st->launched_any) {
-            int rc = decoder_first_via_hub(st, sl, &moved);
-            if (rc != 1) {
-                if (rc)
-                    return rc;
-                continue;
-            }
-        }
-        slot *prev = st->launched_any
-                         ? &st->slots[(st->head + st->nbusy + NSLOTS - 1) %
-                                      NSLOTS]
-                         : NULL;
-        if (!sl->sess) {
-            sl->sess = b64x_session_acquire(st->cap);
-            if (!sl->sess)
-                return -(errno ? errno : ENOMEM);
-        }
-        bool eof = false;
-        int uerr = 0;
-        size_t got = moved;
-        if (!moved)
-            got = gather(st, b64x_session_host_in(sl->sess), st->cap, &eof, &uerr);
-        unsigned flags = B64X_DEC_HOLD_TAIL;
+        if (st->nbusy && !slot_ready(&st->slots[(st->head + st->nbusy - 1) % NSLOTS]))
+            return 0; /* its completion brings us back */
+        size_t room;
+        action_1 waiter = hub_waiter(st);
+        size_t want = DEC_HEAD + st->cap;
+        uint8_t *in = b64_hub_reserve(st->hub, B64_HUB_DECODE, &st->abc, want,
+                                      DEC_HEAD + (st->cap < 4096 ? st->cap : 4096), &room,
+                                      waiter);
+        if (!in)
+            return reserve_failed(st, waiter);
+        bool eof;
+        int uerr;
+        size_t got = gather(st, in + DEC_HEAD, room - DEC_HEAD, &eof, &uerr);
         if (eof) {
             st->final_queued = true;
-            if (!st->launched_any && got == 0)
+            if (got == 0 && st->ncarry == 0) { /* nothing held back: done */
+                b64_hub_cancel(st->hub);
                 return 0;
-            flags = 0; /* last block, or a flush of the carried sextets */
+            }
         } else if (got == 0) {
+            b64_hub_cancel(st->hub);
             return uerr ? uerr : EAGAIN;
         }
+        memset(in, st->skip, DEC_HEAD);
+        for (size_t k = 0; k < st->ncarry; k++)
+            in[DEC_HEAD - st->ncarry + k] = spell_sextet(&st->abc, st->carry[k]);
+        st->ncarry = 0;
         slot_arm(st, sl);
-        sl->hubbed = false;
-        int rc = b64x_session_decode_async(sl->sess, got, &st->abc, flags,
-                                           prev ? prev->sess : NULL, slot_done,
-                                           sl);
-        if (rc)
-            return rc;
-        st->launched_any = true;
+        sl->hold = !eof;
+        b64_hub_commit(st->hub, &sl->ticket, DEC_HEAD + got,
+                       (size_t) b64x_decoded_cap(DEC_HEAD + got),
+                       eof ? 0u : B64X_DEC_HOLD_TAIL, (action_1) { st, (act_1) stage_notify });
         if (uerr)
             return uerr;
     }
@@ -485,35 +441,33 @@ static int top_up(stage *st)
     return st->dir == DIR_ENCODE ? top_up_encoder(st) : top_up_decoder(st);
 }
 
-/* A finished slot's lengths (the decoder's are device-determined). */
+/* A finished slot's lengths (the decoder's come from its checked record,
+ * whose held-back sextets become the next block's carry). */
 static bool slot_ready(slot *sl)
 {
-    if (sl->owner->dir == DIR_ENCODE)
-        return atomic_load_explicit(&sl->ticket.done, memory_order_acquire);
-    if (sl->hubbed) {
-        if (!atomic_load_explicit(&sl->ticket.done, memory_order_acquire))
-            return false;
-        if (!sl->resolved) {
-            sl->out_len = sl->ticket.out_len;
-            sl->body_end = sl->out_len;
-            sl->resolved = true;
-        }
-        return true;
-    }
-    if (!atomic_load_explicit(&sl->done, memory_order_acquire))
+    if (!atomic_load_explicit(&sl->ticket.done, memory_order_acquire))
         return false;
-    if (!sl->resolved) {
-        sl->out_len = (size_t) b64x_session_result(sl->sess)->out_len;
+    if (!sl->resolved) { /* decoder */
+        stage *st = sl->owner;
+        sl->out_len = sl->ticket.err ? 0 : sl->ticket.out_len;
         sl->body_end = sl->out_len;
         sl->resolved = true;
+        if (sl->hold && !sl->ticket.err) {
+            st->ncarry = sl->ticket.res.tail_n < 4 ? sl->ticket.res.tail_n : 0;
+            memcpy(st->carry, sl->ticket.res.tail, st->ncarry);
+        }
     }
     return true;
 }
 
+static int slot_err(slot *sl)
+{
+    return sl->ticket.err;
+}
+
 static const uint8_t *slot_out(slot *sl)
 {
-    return sl->owner->dir == DIR_ENCODE || sl->hubbed ? sl->ticket.out
-                                                      : b64x_session_host_out(sl->sess);
+    return sl->ticket.out;
 }
 
 static void retire_head(stage *st)
@@ -623,8 +577,8 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
         return stage_fail(st, rc);
     for (;;) {
         slot *h = &st->slots[st->head];
-        if (st->nbusy && slot_ready(h) && h->ticket.err)
-            return stage_fail(st, h->ticket.err);
+        if (st->nbusy && slot_ready(h) && slot_err(h))
+            return stage_fail(st, slot_err(h));
         if (st->nbusy && slot_ready(h) && h->out_pos == h->body_end &&
             h->out_pos < h->out_len) {
             /* finalize(): partial sextet and pads, `count` at a time */

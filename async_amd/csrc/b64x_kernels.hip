@@ -42,11 +42,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <utility>
 
 #include "b64x.h"
+#include "b64x_result_check.h"
 
 #define DEV __device__ __forceinline__
 
@@ -1234,7 +1236,7 @@ void k_decode_pass1(
 // The stream's last V mod 4 alphabet characters (as sextets) into
 // res->tail, scanning backwards from the end; one wave.
 DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, uint64_t V,
-                           b64x_dec_result *res)
+                           b64x_dec_result *res, b64x_dec_result *hres)
 {
     const uint32_t lane = lane_id();
     int need = (int) (V & 3);
@@ -1252,15 +1254,31 @@ DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, ui
         }
         end = beg;
     }
-    if (lane == 0)
+    if (lane == 0) {
         for (int j = 0; j < 4; j++) res->tail[j] = got[j];
+        if (hres) {
+            for (int j = 0; j < 4; j++) hres->tail[j] = got[j];
+            hres->tail_n = (uint32_t) (V & 3);
+        }
+    }
 }
 
-DEV void write_result(b64x_dec_result *res, uint64_t V, uint32_t hold)
+// The result record: `res` in device memory (read by the next chained
+// decode's k_spell_carry), and, when `hres` is set, the same record in
+// fine-grained host memory, written by this kernel instead of a D2H copy
+// queued behind it (see b64x_session_decode_async); the host checks every
+// field of it against the poison it wrote before the launch, so the order
+// of these stores does not matter.
+DEV void write_result(b64x_dec_result *res, b64x_dec_result *hres, uint64_t V, uint32_t hold)
 {
+    const uint64_t out_len = hold ? V / 4 * 3 : V * 6 / 8;
     res->valid = V;
     res->tail_n = (uint32_t) (V & 3);
-    res->out_len = hold ? V / 4 * 3 : V * 6 / 8;
+    res->out_len = out_len;
+    if (hres) {
+        hres->valid = V;
+        hres->out_len = out_len;
+    }
 }
 
 // Block-wide exclusive scan of one u64 per thread (256 threads); returns
@@ -1321,7 +1339,7 @@ DEV uint64_t st_load(uint64_t *p)
 template <int PRICE, int TK>
 __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
-    DecAlpha a, void *ws, b64x_dec_result *res, uint32_t hold)
+    DecAlpha a, void *ws, b64x_dec_result *res, b64x_dec_result *hres, uint32_t hold)
 {
     __shared__ uint8_t tab[256];
     __shared__ uint64_t wtot[kWavesPerBlock];
@@ -1336,9 +1354,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
         const uint64_t V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
         if (threadIdx.x == 0) {
             *w.fd_cur = 0;
-            write_result(res, V, hold);
+            write_result(res, hres, V, hold);
         }
-        if (threadIdx.x < 64) find_tail_sextets(tab, in, n, V, res);
+        if (threadIdx.x < 64) find_tail_sextets(tab, in, n, V, res, hres);
         return;
     }
     const uint32_t r0 = (uint32_t) (~packed >> 32);
@@ -1400,8 +1418,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     }
     if (t == ntiles - 1 && threadIdx.x < 64) {
         const uint64_t V = s_excl + agg;
-        if (lane == 0) write_result(res, V, hold);
-        find_tail_sextets(tab, in, n, V, res);
+        if (lane == 0) write_result(res, hres, V, hold);
+        find_tail_sextets(tab, in, n, V, res, hres);
         if (PRICE == 0) {
             // every tile inclusive -> every look-back is over
             for (;;) {
@@ -1869,7 +1887,7 @@ template <bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold,
-    b64x_dec_result *res, uint32_t price = 0)
+    b64x_dec_result *res, b64x_dec_result *hres, uint32_t price = 0)
 {
     DecodeWs w = ws_view(ws, nranges);
     uint32_t r0 = 0xFFFFFFFFu, off0 = 0;  // fused: no range resumes mid-way
@@ -2081,8 +2099,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
         }
         if (t == ntiles - 1 && wv == 0) {
             const uint64_t V = s_excl + s_agg;
-            if (lane == 0) write_result(res, V, hold);
-            find_tail_sextets(sm.tab, in, n, V, res);
+            if (lane == 0) write_result(res, hres, V, hold);
+            find_tail_sextets(sm.tab, in, n, V, res, hres);
             for (;;) {  // every tile inclusive -> every look-back is over
                 bool all = true;
                 for (uint32_t i = lane; i < ntiles; i += 64)
@@ -2182,7 +2200,9 @@ DEV uint4 load_lane(const uint8_t *src, uint64_t p, uint64_t len, bool aligned, 
 // this buffer, or the first pair of the next one -- are issued before the
 // current pair is decoded, so small buffers do not each pay a full memory
 // latency.  A buffer any of whose chunks needs the exact path is marked in
-// outlen[] for the fix-up.
+// outlen[] for the fix-up.  RV: outlen[] receives the alphabet count V
+// instead of floor(6V/8) bytes (the hub's jobs, k_batch_finish).
+template <bool RV>
 __global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
     uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
@@ -2242,7 +2262,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
         if (more_here && ok) {
             pos = npos;
         } else {
-            if (lane == 0) outlen[b] = ok ? V * 6 / 8 : kNeedsExact;
+            if (lane == 0) outlen[b] = ok ? (RV ? V : V * 6 / 8) : kNeedsExact;
             if (bn >= nbuf) break;
             bool fresh_aligned = naligned;
             if (more_here) {
@@ -2722,6 +2742,7 @@ DEV uint64_t decode_buf_bits(const P2dSmem &sm, uint4 *bq, const uint8_t *src, u
     return V;
 }
 
+template <bool RV>
 __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
     uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
@@ -2745,9 +2766,63 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
             uint4 c[2];
             buf_first_chunks(in + beg, len, c);
             const uint64_t V = decode_buf_bits(sm, sm.bits[wv], in + beg, len, out + obeg, c);
-            if (lane == 0) outlen[b] = V * 6 / 8;
+            if (lane == 0) outlen[b] = RV ? V : V * 6 / 8;
         }
     }
+}
+
+// The hub's decode jobs, after k_decode_batch_fast/fix2<true> left each
+// job's alphabet count V in vcount[]: one wave per job writes the job's
+// result record straight into host memory (hres[j]; no D2H copy to trust).
+// A job with flags[j] & 1 (HOLD: more of its stream follows) emits only
+// whole groups, V/4*3 bytes, and reports its last V mod 4 sextets, which
+// the stage spells in front of the stream's next job (the reference keeps
+// those bits in decoder->bits across reads, base64decoder.c:64-76); a final
+// job emits floor(6V/8) (the trailing partial bits dropped, :71-76).
+__global__ __launch_bounds__(kThreads) void k_batch_finish(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+    const uint8_t *__restrict__ flags, const uint64_t *__restrict__ vcount, uint32_t njobs,
+    DecAlpha a, b64x_dec_result *__restrict__ hres)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t j = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+         j < njobs; j += nw) {
+        const uint64_t beg = in_off[j], n = in_off[j + 1] - beg, V = vcount[j];
+        const bool hold = flags[j] & 1;
+        int need = hold ? (int) (V & 3) : 0;
+        uint8_t got[4] = {0, 0, 0, 0};
+        uint64_t end = n;
+        while (need > 0 && end > 0) {  // the last V mod 4 alphabet characters
+            const uint64_t b0 = end >= 64 ? end - 64 : 0;
+            const uint64_t p = b0 + lane;
+            const uint32_t t = p < end ? tab[in[beg + p]] : 0xFFu;
+            uint64_t bm = __ballot(t < 64u);
+            while (need > 0 && bm) {
+                const int hi = 63 - __clzll(bm);
+                got[--need] = (uint8_t) __shfl(t, hi, 64);
+                bm &= ~(1ull << hi);
+            }
+            end = b0;
+        }
+        if (lane == 0) {
+            b64x_dec_result *r = hres + j;
+            for (int k = 0; k < 4; k++) r->tail[k] = got[k];
+            r->valid = V;
+            r->out_len = hold ? V / 4 * 3 : V * 6 / 8;
+            r->tail_n = (uint32_t) (V & 3);
+        }
+    }
+}
+
+// Completion stamp of a lane's encode batch: written into host memory by a
+// kernel queued behind the batch's encode (b64x_lane_encode_check).
+__global__ void __launch_bounds__(64) k_stamp(uint64_t *h_stamp, uint64_t v)
+{
+    if (threadIdx.x == 0) *(volatile uint64_t *) h_stamp = v;
 }
 
 // ------------------------------------------------------------ utilities --
@@ -2795,7 +2870,7 @@ DeviceInfo query_device()
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_encode, kThreads, 0) == hipSuccess && nb > 0)
         d.enc_blocks_per_cu = nb;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_batch_fast, kThreads, 0) == hipSuccess && nb > 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_batch_fast<false>, kThreads, 0) == hipSuccess && nb > 0)
         d.dec_blocks_per_cu = nb;
     d.ok = true;
     return d;
@@ -3169,9 +3244,19 @@ static void *library_workspace(void *stream, int *err)
     return ws;
 }
 
-int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
-                    b64x_dec_result *d_res, const b64x_alphabet *abc,
-                    unsigned flags, void *d_workspace, void *stream)
+__global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres)
+{
+    if (threadIdx.x != 0) return;
+    *res = b64x_dec_result{};
+    if (hres) *hres = b64x_dec_result{};
+}
+
+// b64x_decode_dev, plus an optional host mirror of the result record that
+// the kernels write themselves (sessions; see write_result).
+static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
+                           b64x_dec_result *d_res, b64x_dec_result *h_res,
+                           const b64x_alphabet *abc, unsigned flags, void *d_workspace,
+                           void *stream)
 {
     if (!d_res) return -EINVAL;
     if (flags & ~(unsigned) (B64X_DEC_HOLD_TAIL | B64X_DEC_EXPECT_JUNK)) return -EINVAL;
@@ -3179,8 +3264,10 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
     hipStream_t s = (hipStream_t) stream;
-    if (nchars == 0)
-        return hip_err(hipMemsetAsync(d_res, 0, sizeof(b64x_dec_result), s));
+    if (nchars == 0) {
+        hipLaunchKernelGGL(k_result_zero, dim3(1), dim3(64), 0, s, d_res, h_res);
+        return launch_status();
+    }
     int err = 0;
     void *ws = d_workspace ? d_workspace : library_workspace(stream, &err);
     if (!ws) return err;
@@ -3194,7 +3281,7 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
         const uint32_t tiles = (p.nranges + kFuseTile - 1) / kFuseTile;
         hipLaunchKernelGGL(k_decode_fused, dim3(tiles), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                           a, ws, hold, d_res, (uint32_t) g_tune[9]);
+                           a, ws, hold, d_res, h_res, (uint32_t) g_tune[9]);
         return launch_status();
     }
     p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
@@ -3206,7 +3293,7 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
         hipLaunchKernelGGL(ks,
                            dim3((p.nranges + kScanTile - 1) / kScanTile),
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges,
-                           a, ws, d_res, hold);
+                           a, ws, d_res, h_res, hold);
     }
     if ((err = launch_status())) return err;
     // grid-stride over the ranges with exactly the resident blocks (a second
@@ -3224,31 +3311,42 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
     const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2d);
     hipLaunchKernelGGL(k_decode_pass2d, dim3(b2), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                       a, ws, hold, (b64x_dec_result *) nullptr, 0u);
+                       a, ws, hold, (b64x_dec_result *) nullptr, (b64x_dec_result *) nullptr, 0u);
     return launch_status();
 }
 
+int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
+                    b64x_dec_result *d_res, const b64x_alphabet *abc,
+                    unsigned flags, void *d_workspace, void *stream)
+{
+    return decode_dev_impl(d_in, nchars, d_out, d_res, nullptr, abc, flags, d_workspace,
+                           stream);
+}
+
+// rv: d_outlen receives alphabet counts V (the hub's jobs) instead of bytes.
 static int launch_batch_decode(const void *d_in, const BatchLayout &L, uint32_t nbuf,
                                void *d_out, uint64_t *d_outlen,
-                               const b64x_alphabet *abc, void *stream)
+                               const b64x_alphabet *abc, void *stream, bool rv = false)
 {
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
     hipStream_t s = (hipStream_t) stream;
     const DecAlpha a = dec_alpha(abc);
-    static const int occ = occupancy_of(k_decode_batch_fast);
+    static const int occ = occupancy_of(k_decode_batch_fast<false>);
     uint32_t grid = cap_grid((nbuf + kWavesPerBlock - 1) / kWavesPerBlock,
                              (uint64_t) d->cus * occ);
-    hipLaunchKernelGGL(k_decode_batch_fast, dim3(grid), dim3(kThreads), 0, s,
-                       (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
+    hipLaunchKernelGGL(rv ? k_decode_batch_fast<true> : k_decode_batch_fast<false>, dim3(grid),
+                       dim3(kThreads), 0, s, (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf,
+                       d_outlen, a);
     int err = launch_status();
     if (err) return err;
     // The fix-up scans outlen[] 64 words per wave; on clean input that is
     // all it does.
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
-                       (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
+    hipLaunchKernelGGL(rv ? k_decode_batch_fix2<true> : k_decode_batch_fix2<false>, dim3(fgrid),
+                       dim3(kThreads), 0, s, (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf,
+                       d_outlen, a);
     return launch_status();
 }
 
@@ -3356,7 +3454,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     }
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
                               (uint64_t) d->cus * 8);
-    hipLaunchKernelGGL(k_decode_batch_fix2, dim3(fgrid), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(k_decode_batch_fix2<false>, dim3(fgrid), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a);
     return launch_status();
 }
@@ -3396,10 +3494,28 @@ struct b64x_session {
     uint8_t *d_base;     // d_in - kSessionHead
     uint64_t last_len;   // characters of the last decode (0: none yet)
     bool dec_staged;     // the last decode found junk throughout: stage the next
+    uint64_t res_len;    // characters and flags of the last decode, for the
+    unsigned res_flags;  // result check (b64x_session_decode_result)
     uint8_t *d_in, *d_out;
     void *d_ws;
     b64x_dec_result *d_res, *h_res;
 };
+
+// ---- completion results: written by the kernels, checked by the host ----
+//
+// A session decode's result record is written by the kernel that computes
+// it straight into the fine-grained host mirror (no D2H copy behind the
+// kernels), the host poisons the mirror before every launch, and
+// b64x_session_decode_result() checks every field: a record that is still
+// poisoned or inconsistent is counted, the session's stream is waited for,
+// and the record is checked again (-EIO if it is still wrong: loud, never a
+// silently short stream).  The hub's lanes do the same for their batches
+// (b64x_lane_*_check).  Round 1 read records that D2H copies had filled, and
+// under load (600 decoder streams on one loop on per-stage sessions) a block
+// was now and then served as empty from a well-formed "nothing decoded"
+// record (profiles/r02_diag_notes.md).  The check itself is
+// b64x_result_check.h, shared with the CPU stage tests.
+static std::atomic<uint64_t> g_early_session{0}, g_early_lane{0};
 
 // Device headroom in front of d_in: a chained decode writes the carried
 // sextets (re-spelled as characters, right-aligned, padded on the left with
@@ -3574,8 +3690,7 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
     int err;
     if ((err = b64x_session_decode_async(s, n, abc, flags, nullptr, nullptr, nullptr))) return err;
     if ((err = b64x_session_wait(s))) return err;
-    *res = *s->h_res;
-    return 0;
+    return b64x_session_decode_result(s, res);
 }
 
 // A session's encode reads and writes its pinned host buffers in place over
@@ -3643,9 +3758,10 @@ constexpr uint64_t kZeroCopyJunk = 64;  // skipped characters beyond the carry h
 static bool decode_in_place(b64x_session *s)
 {
     if (!zero_copy_sessions()) return false;
-    if (s->last_len && hipStreamQuery(s->stream) == hipSuccess) {
-        const uint64_t junk = s->last_len - (s->h_res->valid < s->last_len ? s->h_res->valid
-                                                                            : s->last_len);
+    b64x_dec_result r;
+    if (s->last_len && hipStreamQuery(s->stream) == hipSuccess &&
+        b64x_result_ok(s->h_res, s->res_len, s->res_flags, &r)) {
+        const uint64_t junk = s->last_len - (r.valid < s->last_len ? r.valid : s->last_len);
         s->dec_staged = junk > kCarryHead + kZeroCopyJunk;
         s->last_len = 0;
     }
@@ -3660,9 +3776,11 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
     if (carry_from && carry_from->device != s->device) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(s->device)))) return err;
+    b64x_dec_result cr;
     if (carry_from && hipStreamQuery(carry_from->stream) == hipSuccess &&
-        (carry_from->h_res->tail_n == 0 || carry_from->h_res->tail_n >= 4))
-        carry_from = nullptr;  // finished, and nothing to carry (k_spell_carry's rule)
+        b64x_result_ok(carry_from->h_res, carry_from->res_len, carry_from->res_flags, &cr) &&
+        cr.tail_n == 0)
+        carry_from = nullptr;  // finished, and nothing to carry
     const bool in_place = decode_in_place(s) && !carry_from;
     uint8_t *in = in_place ? s->h_in : s->d_in;
     uint8_t *out = in_place ? s->h_out : s->d_out;
@@ -3692,12 +3810,13 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
         src -= kCarryHead;
         len += kCarryHead;
     }
-    if ((err = b64x_decode_dev(src, len, out, s->d_res, abc, flags, s->d_ws, s->stream)))
+    b64x_poison_result(s->h_res);
+    s->res_len = len;
+    s->res_flags = flags;
+    if ((err = decode_dev_impl(src, len, out, s->d_res, s->h_res, abc, flags, s->d_ws,
+                               s->stream)))
         return err;
     if ((err = hip_err(hipEventRecord(s->decoded, s->stream)))) return err;
-    if ((err = hip_err(hipMemcpyAsync(s->h_res, s->d_res, sizeof(b64x_dec_result),
-                                      hipMemcpyDeviceToHost, s->stream))))
-        return err;
     s->last_len = len;
     // The output length is device-determined: copy the capacity bound.
     if (len && !in_place &&
@@ -3711,6 +3830,23 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
 const b64x_dec_result *b64x_session_result(const b64x_session *s)
 {
     return s ? s->h_res : nullptr;
+}
+
+int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res)
+{
+    if (!s || !res) return -EINVAL;
+    if (b64x_result_ok(s->h_res, s->res_len, s->res_flags, res)) return 0;
+    g_early_session.fetch_add(1, std::memory_order_relaxed);
+    int err = b64x_session_wait(s);
+    if (err) return err;
+    const bool ok = b64x_result_ok(s->h_res, s->res_len, s->res_flags, res);
+    return ok ? 0 : -EIO;
+}
+
+void b64x_diag_counters(uint64_t out[2])
+{
+    out[0] = g_early_session.load(std::memory_order_relaxed);
+    out[1] = g_early_lane.load(std::memory_order_relaxed);
 }
 
 int b64x_session_wait(b64x_session *s)
@@ -3737,12 +3873,23 @@ void b64x_host_free(void *p)
     if (p) (void) hipHostFree(p);
 }
 
+// A lane's batches read their input from device memory (one H2D copy of the
+// arena) and write their outputs -- characters, bytes and the decode jobs'
+// result records -- straight into the pinned host arena: no D2H copy.  The
+// host checks every batch once its completion callback has run: decode
+// records were poisoned before the launch (b64x_lane_decode_check), and an
+// encode batch ends with a kernel that stamps the lane's sequence number
+// into host memory (b64x_lane_encode_check).  Round 1's D2H copies of
+// results are what lost blocks under load.
 struct b64x_lane {
     int device;
     hipStream_t stream;
-    uint8_t *d_in, *d_out;
-    uint64_t *d_offs;
-    uint64_t in_cap, out_cap, offs_cap;  // bytes / words allocated
+    uint8_t *d_in;
+    uint64_t *d_offs;     // in_off | out_off | vcount (decode) words
+    uint8_t *d_flags;
+    uint64_t *h_stamp;    // fine-grained pinned: the last finished encode batch
+    uint64_t seq;         // the last encode batch queued
+    uint64_t in_cap, offs_cap, flags_cap;  // bytes allocated
 };
 
 b64x_lane *b64x_lane_open(void)
@@ -3759,6 +3906,13 @@ b64x_lane *b64x_lane_open(void)
         errno = EIO;
         return nullptr;
     }
+    if (hipHostMalloc((void **) &l->h_stamp, sizeof(uint64_t), kSessionHostFlags) != hipSuccess) {
+        (void) hipStreamDestroy(l->stream);
+        free(l);
+        errno = ENOMEM;
+        return nullptr;
+    }
+    *l->h_stamp = 0;
     return l;
 }
 
@@ -3768,8 +3922,9 @@ void b64x_lane_close(b64x_lane *l)
     (void) hipSetDevice(l->device);
     (void) hipStreamSynchronize(l->stream);
     if (l->d_in) (void) hipFree(l->d_in);
-    if (l->d_out) (void) hipFree(l->d_out);
     if (l->d_offs) (void) hipFree(l->d_offs);
+    if (l->d_flags) (void) hipFree(l->d_flags);
+    if (l->h_stamp) (void) hipHostFree(l->h_stamp);
     (void) hipStreamDestroy(l->stream);
     free(l);
 }
@@ -3821,6 +3976,27 @@ static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need)
     return 0;
 }
 
+// Offsets (and, for decode, the per-job counts) and the input on the device.
+static int lane_stage_in(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
+                         const uint64_t *h_in_off, const uint64_t *h_out_off, uint64_t words_extra)
+{
+    const uint64_t in_bytes = h_in_off[njobs];
+    const uint64_t words = (uint64_t) njobs + 1;
+    int err;
+    if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
+    if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, (2 * words + words_extra) * 8)))
+        return err;
+    if ((err = hip_err(hipMemcpyAsync(l->d_offs, h_in_off, words * 8, hipMemcpyHostToDevice,
+                                      l->stream))) ||
+        (err = hip_err(hipMemcpyAsync(l->d_offs + words, h_out_off, words * 8,
+                                      hipMemcpyHostToDevice, l->stream))))
+        return err;
+    if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
+                                                  hipMemcpyHostToDevice, l->stream))))
+        return err;
+    return 0;
+}
+
 int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const b64x_alphabet *abc,
@@ -3829,65 +4005,60 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off))) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(l->device)))) return err;
-    if (njobs) {  // staged: the ragged kernel's block-per-job form is PCIe-latency-bound in place
-        const uint64_t in_bytes = h_in_off[njobs], out_bytes = h_out_off[njobs];
+    if (njobs) {
         const uint64_t words = (uint64_t) njobs + 1;
-        if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
-        if ((err = lane_grow(l, (void **) &l->d_out, &l->out_cap, out_bytes + 64))) return err;
-        if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, 2 * words * 8))) return err;
-        if ((err = hip_err(hipMemcpyAsync(l->d_offs, h_in_off, words * 8, hipMemcpyHostToDevice,
-                                          l->stream))) ||
-            (err = hip_err(hipMemcpyAsync(l->d_offs + words, h_out_off, words * 8,
-                                          hipMemcpyHostToDevice, l->stream))))
-            return err;
-        if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
-                                                      hipMemcpyHostToDevice, l->stream))))
-            return err;
-        if ((err = b64x_encode_batch(l->d_in, l->d_offs, njobs, l->d_out, l->d_offs + words,
-                                     abc, l->stream)))
-            return err;
-        if (out_bytes && (err = hip_err(hipMemcpyAsync(h_out, l->d_out, out_bytes,
-                                                       hipMemcpyDeviceToHost, l->stream))))
+        if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, 0))) return err;
+        if ((err = b64x_encode_batch(l->d_in, l->d_offs, njobs, h_out, l->d_offs + words, abc,
+                                     l->stream)))
             return err;
     }
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, l->stream, l->h_stamp, ++l->seq);
+    if ((err = launch_status())) return err;
     if (done) return hip_err(hipLaunchHostFunc(l->stream, done, arg));
     return 0;
 }
 
+int b64x_lane_encode_check(b64x_lane *l)
+{
+    if (!l) return -EINVAL;
+    if (*(volatile uint64_t *) l->h_stamp == l->seq) return 0;
+    g_early_lane.fetch_add(1, std::memory_order_relaxed);
+    int err = b64x_lane_wait(l);
+    if (err) return err;
+    return *(volatile uint64_t *) l->h_stamp == l->seq ? 0 : -EIO;
+}
+
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
-                           const uint64_t *h_out_off, uint64_t *h_outlen,
-                           const b64x_alphabet *abc, b64x_done_fn done, void *arg)
+                           const uint64_t *h_out_off, const uint8_t *h_flags,
+                           b64x_dec_result *h_res, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg)
 {
-    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off || !h_outlen)))
+    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off || !h_flags || !h_res)))
         return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(l->device)))) return err;
     if (njobs) {
-        const uint64_t in_bytes = h_in_off[njobs], out_bytes = h_out_off[njobs];
         const uint64_t words = (uint64_t) njobs + 1;
-        if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
-        if ((err = lane_grow(l, (void **) &l->d_out, &l->out_cap, out_bytes + 64))) return err;
-        if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, 3 * words * 8))) return err;
+        for (uint32_t j = 0; j < njobs; j++) b64x_poison_result(h_res + j);
+        if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, words))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_flags, &l->flags_cap, njobs))) return err;
+        if ((err = hip_err(hipMemcpyAsync(l->d_flags, h_flags, njobs, hipMemcpyHostToDevice,
+                                          l->stream))))
+            return err;
         uint64_t *d_in_off = l->d_offs, *d_out_off = l->d_offs + words,
-                 *d_outlen = l->d_offs + 2 * words;
-        if ((err = hip_err(hipMemcpyAsync(d_in_off, h_in_off, words * 8, hipMemcpyHostToDevice,
-                                          l->stream))) ||
-            (err = hip_err(hipMemcpyAsync(d_out_off, h_out_off, words * 8,
-                                          hipMemcpyHostToDevice, l->stream))))
+                 *d_vcount = l->d_offs + 2 * words;
+        const BatchLayout L{d_in_off, d_out_off, 0, 0, 0};
+        const uint8_t *src = h_in_off[njobs] ? l->d_in : (const uint8_t *) l->d_offs;
+        if ((err = launch_batch_decode(src, L, njobs, h_out, d_vcount, abc, l->stream, true)))
             return err;
-        if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
-                                                      hipMemcpyHostToDevice, l->stream))))
-            return err;
-        if ((err = b64x_decode_batch(in_bytes ? l->d_in : l->d_out, d_in_off, njobs, l->d_out,
-                                     d_out_off, d_outlen, abc, l->stream)))
-            return err;
-        if (out_bytes && (err = hip_err(hipMemcpyAsync(h_out, l->d_out, out_bytes,
-                                                       hipMemcpyDeviceToHost, l->stream))))
-            return err;
-        if ((err = hip_err(hipMemcpyAsync(h_outlen, d_outlen, (uint64_t) njobs * 8,
-                                          hipMemcpyDeviceToHost, l->stream))))
-            return err;
+        const DeviceInfo *d = device_info();
+        const uint32_t grid = cap_grid((njobs + kWavesPerBlock - 1) / kWavesPerBlock,
+                                       (uint64_t) d->cus * 8);
+        hipLaunchKernelGGL(k_batch_finish, dim3(grid), dim3(kThreads), 0, l->stream, src, d_in_off,
+                           (const uint8_t *) l->d_flags, (const uint64_t *) d_vcount, njobs,
+                           dec_alpha(abc), h_res);
+        if ((err = launch_status())) return err;
     }
     if (done) return hip_err(hipLaunchHostFunc(l->stream, done, arg));
     return 0;
@@ -3897,6 +4068,26 @@ int b64x_lane_wait(b64x_lane *l)
 {
     if (!l) return -EINVAL;
     return hip_err(hipStreamSynchronize(l->stream));
+}
+
+static bool jobs_ok(const uint64_t *h_in_off, const uint8_t *h_flags,
+                    const b64x_dec_result *h_res, uint32_t njobs)
+{
+    for (uint32_t j = 0; j < njobs; j++)
+        if (!b64x_result_ok(h_res + j, h_in_off[j + 1] - h_in_off[j], h_flags[j] & 1, nullptr))
+            return false;
+    return true;
+}
+
+int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t *h_flags,
+                           const b64x_dec_result *h_res, uint32_t njobs)
+{
+    if (!l || (njobs && (!h_in_off || !h_flags || !h_res))) return -EINVAL;
+    if (jobs_ok(h_in_off, h_flags, h_res, njobs)) return 0;
+    g_early_lane.fetch_add(1, std::memory_order_relaxed);
+    int err = b64x_lane_wait(l);
+    if (err) return err;
+    return jobs_ok(h_in_off, h_flags, h_res, njobs) ? 0 : -EIO;
 }
 
 // Tuning and calibration hooks for scripts/bench_variants.py (exported,

@@ -1,0 +1,55 @@
+/*
+ * b64x_result_check.h -- internal: the host-side check of completion
+ * records, shared by the library (b64x_kernels.hip) and the CPU test
+ * backend (tests/csrc/fake_b64x.c), so the deterministic stage tests run the
+ * product's own check.
+ *
+ * A decode's result record (b64x_dec_result: a session's, or each job's of
+ * a lane batch) is poisoned on the host before the launch; the kernels
+ * overwrite it in host memory.  When the completion callback has run, a
+ * record that still holds poison, or whose fields contradict each other,
+ * was read too early: the caller waits for the stream and checks again
+ * (b64x.h, b64x_session_decode_result / b64x_lane_decode_check).
+ */
+#ifndef ASYNC_AMD_B64X_RESULT_CHECK_H
+#define ASYNC_AMD_B64X_RESULT_CHECK_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#include "b64x.h"
+
+#define B64X_RES_POISON (~(uint64_t) 0)
+#define B64X_TAIL_POISON (~(uint32_t) 0)
+
+static inline void b64x_poison_result(b64x_dec_result *r)
+{
+    volatile b64x_dec_result *v = r;
+    v->out_len = B64X_RES_POISON;
+    v->valid = B64X_RES_POISON;
+    v->tail_n = B64X_TAIL_POISON;
+}
+
+/* A landed, self-consistent record of a decode of `len` characters with
+ * `flags`; *copy receives what was read (each field once). */
+static inline bool b64x_result_ok(const b64x_dec_result *r, uint64_t len, unsigned flags,
+                                  b64x_dec_result *copy)
+{
+    const volatile b64x_dec_result *v = r;
+    b64x_dec_result c;
+    c.out_len = v->out_len;
+    c.valid = v->valid;
+    c.tail_n = v->tail_n;
+    for (int j = 0; j < 4; j++)
+        c.tail[j] = v->tail[j];
+    if (copy)
+        *copy = c;
+    if (c.valid == B64X_RES_POISON || c.out_len == B64X_RES_POISON ||
+        c.tail_n == B64X_TAIL_POISON)
+        return false;
+    const bool hold = (flags & B64X_DEC_HOLD_TAIL) != 0;
+    return c.valid <= len && c.tail_n == (uint32_t) (c.valid & 3) &&
+           c.out_len == (hold ? c.valid / 4 * 3 : c.valid * 6 / 8);
+}
+
+#endif /* ASYNC_AMD_B64X_RESULT_CHECK_H */

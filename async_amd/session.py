@@ -103,6 +103,17 @@ class Session:
         _lib.check("b64x_session_wait", self._L.b64x_session_wait(self._h))
 
     def result(self) -> DecResult:
-        """Copy of the last completed decode's result (call after wait())."""
-        p = self._L.b64x_session_result(self._h)
-        return DecResult.from_buffer_copy(ctypes.string_at(p, ctypes.sizeof(DecResult)))
+        """Checked copy of the last completed decode's result (call after
+        wait()); raises if the record is not a finished, consistent one."""
+        res = DecResult()
+        _lib.check("b64x_session_decode_result",
+                   self._L.b64x_session_decode_result(self._h, ctypes.byref(res)))
+        return res
+
+
+def diag_counters() -> tuple[int, int]:
+    """(session records, lane batches) found unfinished when their
+    completion callback had already run (see b64x_diag_counters)."""
+    out = (ctypes.c_uint64 * 2)()
+    _lib.load().b64x_diag_counters(out)
+    return int(out[0]), int(out[1])

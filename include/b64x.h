@@ -174,8 +174,9 @@ typedef void (*b64x_done_fn)(void *arg);
 
 /* Asynchronous forms of b64x_session_encode/_decode: enqueue H2D, kernels
  * and D2H on the session's stream and return at once.  `done(arg)` (may be
- * NULL) runs once host_out -- and, for decode, b64x_session_result() -- hold
- * the results.  One call in flight per session. */
+ * NULL) runs once the call's work has finished; for decode, read the
+ * result with b64x_session_decode_result().  One call in flight per
+ * session. */
 int b64x_session_encode_async(b64x_session *s, uint64_t n,
                               const b64x_alphabet *abc, b64x_done_fn done,
                               void *arg);
@@ -192,22 +193,35 @@ int b64x_session_decode_async(b64x_session *s, uint64_t n,
                               const b64x_alphabet *abc, unsigned flags,
                               const b64x_session *carry_from,
                               b64x_done_fn done, void *arg);
-/* The decode result of the last completed call (host memory). */
+/* The decode result of the last completed call (host memory; the kernels
+ * write it there themselves).  Raw view: prefer the checked form below. */
 const b64x_dec_result *b64x_session_result(const b64x_session *s);
+/* Checked copy of the last decode's result, to be called once its `done`
+ * has run (or after b64x_session_wait).  The record is poisoned before each
+ * launch; one that is still poisoned or inconsistent (valid > characters,
+ * tail_n != valid mod 4, out_len not the flags' function of valid) is
+ * counted (b64x_diag_counters), the session's stream is waited for and the
+ * record is checked again.  0, or -EIO if it is still wrong. */
+int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res);
 /* Wait for everything queued on the session. */
 int b64x_session_wait(b64x_session *s);
 
 /* ---- batch lanes (cross-stream batching of host blocks) --------------- */
 
-/* Pinned host memory for batch arenas (hipHostMalloc); NULL on failure. */
+/* Pinned host memory for batch arenas (hipHostMalloc, fine-grained); NULL
+ * on failure. */
 void *b64x_host_alloc(uint64_t bytes);
 void b64x_host_free(void *p);
 
 /* A lane: one HIP stream plus device buffers that grow on demand.  It
- * runs one ragged batch at a time out of caller-owned pinned arenas; the
- * bytestream_1 stages pack many streams' blocks into one batch so that a
- * launch (and its two copies) is amortised over them (SURVEY.md §8(f)
- * row f3, ref src/queuestream.c:150-191 being the per-message feed). */
+ * runs ragged batches out of caller-owned pinned arenas; the bytestream_1
+ * stages pack many streams' blocks into one batch so that a launch (and
+ * its one H2D copy) is amortised over them (ref
+ * src/queuestream.c:150-191 being the per-message feed).  The kernels
+ * write every output -- characters, bytes, result records -- straight into
+ * the pinned host buffers: there is no D2H copy to trust.  After a batch's
+ * `done(arg)` has run, the caller checks it with b64x_lane_encode_check /
+ * b64x_lane_decode_check before reading anything. */
 typedef struct b64x_lane b64x_lane;
 
 b64x_lane *b64x_lane_open(void);
@@ -220,26 +234,44 @@ void b64x_lane_release(b64x_lane *l);
 /* Encode njobs buffers: buffer i is h_in[h_in_off[i] .. h_in_off[i+1])
  * and its b64x_encoded_len(len, abc->pad) characters go to
  * h_out + h_out_off[i] (both offset arrays hold njobs+1 monotone entries
- * starting at 0; the last = bytes copied each way).  All four host
- * buffers must be pinned (b64x_host_alloc) and stay untouched until
- * `done(arg)` has run.  Asynchronous; the lane's device buffers are grown
- * (synchronously) when a batch needs more. */
+ * starting at 0).  All four host buffers must be pinned (b64x_host_alloc)
+ * and stay untouched until `done(arg)` has run.  Asynchronous; the lane's
+ * device buffers are grown (synchronously) when a batch needs more.  One
+ * batch in flight per lane. */
 int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const b64x_alphabet *abc,
                            b64x_done_fn done, void *arg);
-/* Decode njobs independent, complete character buffers (each one whole
- * stream: its final partial group is emitted): buffer i is
- * h_in[h_in_off[i] .. h_in_off[i+1]) and decodes to h_out + h_out_off[i]
- * (capacity h_out_off[i+1] - h_out_off[i] >= b64x_decoded_cap(len));
- * h_outlen[i] receives its byte count.  Pinned host buffers, as for
- * b64x_lane_encode_async. */
+/* The encode batch whose `done` has run really finished: its completion
+ * stamp (written by a kernel queued behind the encode) is there; if not,
+ * counted (b64x_diag_counters), waited for and checked again.  0 or -EIO. */
+int b64x_lane_encode_check(b64x_lane *l);
+/* Decode njobs character buffers: job i is h_in[h_in_off[i] ..
+ * h_in_off[i+1]), its bytes go to h_out + h_out_off[i] (capacity
+ * >= b64x_decoded_cap(len)) and its result record to h_res[i].  h_flags[i]
+ * & B64X_DEC_HOLD_TAIL: more of the job's stream follows, so only whole
+ * groups are emitted and the last V mod 4 sextets are reported in the
+ * record (b64x_decode_dev's HOLD_TAIL); otherwise the job ends its stream
+ * and its final partial group is emitted.  Pinned host buffers, as for
+ * b64x_lane_encode_async; the records are poisoned here. */
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
-                           const uint64_t *h_out_off, uint64_t *h_outlen,
-                           const b64x_alphabet *abc, b64x_done_fn done, void *arg);
+                           const uint64_t *h_out_off, const uint8_t *h_flags,
+                           b64x_dec_result *h_res, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg);
+/* Checks a finished decode batch's records (see b64x_session_decode_result
+ * for what is checked): one still poisoned or inconsistent is counted, the
+ * lane is waited for and the records are checked again.  0 or -EIO. */
+int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off,
+                           const uint8_t *h_flags, const b64x_dec_result *h_res,
+                           uint32_t njobs);
 /* Wait for everything queued on the lane. */
 int b64x_lane_wait(b64x_lane *l);
+
+/* Completion results found unfinished when their `done` had already run:
+ * out[0] session decode records, out[1] lane batches (process-wide totals,
+ * for tests and diagnostics). */
+void b64x_diag_counters(uint64_t out[2]);
 
 /* ---- utilities ----------------------------------------------------------- */
 

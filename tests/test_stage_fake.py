@@ -1,0 +1,186 @@
+"""The bytestream_1 stages' slot accounting and completion handling, on CPU.
+
+tests/csrc/libstage_fake.so links the product's host C (event loop,
+streams, framing, batching hub and the encoder/decoder stages of
+async_amd/csrc/) with a CPU stand-in for the GPU side of the b64x ABI
+(tests/csrc/fake_b64x.c).  Its "device" completes queued work in an order a
+seeded generator picks (sessions and lanes each in their own order, different
+ones interleaved at random), and can run a job's completion callback *before*
+publishing its result record and output ("early" jobs) -- the failure that
+lost a whole 768-byte block of one decoder stream now and then in round 1
+(profiles/r01_v15_stress_ingress.log).  Every stream is compared with the
+oracle (the reference's decoder_read, src/base64decoder.c:52-80: no byte is
+ever lost).
+
+`raw` mode stands for the round-1 stage, which read the record without
+checking it: the same interleavings then lose blocks, which shows the test
+has the power to catch the bug.  The product's check
+(async_amd/csrc/b64x_result_check.h) is what the non-raw runs exercise.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as orc
+from tests import util
+
+
+def fake():
+    return util.fake_harness()
+
+
+def counters(L):
+    out = (ctypes.c_uint64 * 2)()
+    L.b64x_diag_counters(out)
+    return int(out[0]), int(out[1])
+
+
+def stats(L):
+    out = (ctypes.c_uint64 * 2)()
+    L.fake_stats(out)
+    return int(out[0]), int(out[1])
+
+
+def long_msgs(seed, n=200, junk_every=7):
+    rng = np.random.default_rng(seed)
+    msgs = [orc.encode(rng.integers(0, 256, int(k), dtype=np.uint8).tobytes())
+            for k in rng.integers(1500, 5000, n)]
+    for i in range(0, n, junk_every):  # MIME lines: carries at block edges
+        msgs[i] = b"\r\n".join(msgs[i][j:j + 76] for j in range(0, len(msgs[i]), 76))
+    return msgs
+
+
+def bad_streams(msgs, got):
+    bad = []
+    for i, m in enumerate(msgs):
+        want = orc.decode(m)
+        if got is None or got[i] != want:
+            bad.append(i)
+    return bad
+
+
+@pytest.fixture
+def small_blocks(monkeypatch):
+    # 1 KiB staging: every stream outgrows its first block and continues on
+    # chained sessions, 2-7 blocks each (the round-1 stress shape)
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", "1024")
+
+
+@pytest.mark.parametrize("seed,pct", [(1, 30), (2, 60), (3, 100)])
+def test_long_decoder_streams_adversarial_orders(small_blocks, seed, pct):
+    """Many long decoder streams on one loop (every block a job of a shared
+    batch), batches completing in random orders, `pct` % of them calling
+    back before their records are published: every stream is the
+    oracle's, and the early ones were caught by the check."""
+    L = fake()
+    L.fake_configure(seed, pct, 0)
+    e0 = counters(L)
+    j0 = stats(L)
+    msgs = long_msgs(seed)
+    got, err = util.ingress_stacks(msgs, 4096, lib=L)
+    assert err == 0
+    assert bad_streams(msgs, got) == []
+    batches, early = (a - b for a, b in zip(stats(L), j0))
+    assert batches >= 4  # 2-7 blocks a stream, one on the GPU at a time
+    if pct == 100:
+        assert early == batches and counters(L)[1] - e0[1] == batches
+
+
+def test_round1_raw_read_loses_blocks(small_blocks):
+    """The same interleavings with the records read unchecked (round 1):
+    blocks are lost -- the test above would have failed before the fix."""
+    L = fake()
+    L.fake_configure(7, 100, 1)
+    try:
+        msgs = long_msgs(7)
+        got, err = util.ingress_stacks(msgs, 4096, lib=L)
+        assert err != 0 or bad_streams(msgs, got)
+    finally:
+        L.fake_configure(1, 0, 0)
+
+
+@pytest.mark.parametrize("read_size", [1, 200, 4096])
+def test_decoder_stage_every_order(small_blocks, read_size):
+    """One stream at a time, many read sizes and carries (junk at block
+    edges, '=' mid-stream, ragged tails), completions reordered and early."""
+    L = fake()
+    L.fake_configure(11 + read_size, 30, 0)
+    rng = np.random.default_rng(read_size)
+    for n in (0, 1, 2, 700, 766, 767, 768, 769, 3000, 10001):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        chars = orc.encode(data, pad=bool(n % 2))
+        dirty = b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76))
+        for text in (chars, dirty, b"QQ==" + chars + b"=QU", chars[:max(len(chars) - 1, 0)]):
+            got, err = util.stage_decode(text, 0, read_size, lib=L)
+            assert err == 0
+            assert got == orc.decode(text), (n, len(text))
+
+
+@pytest.mark.parametrize("seed,pct", [(5, 30), (6, 100)])
+def test_short_decoder_streams_through_hub(seed, pct):
+    """Short streams are jobs of shared decode batches (lanes): early batch
+    callbacks are caught by the lane check (b64x_lane_decode_check)."""
+    L = fake()
+    L.fake_configure(seed, pct, 0)
+    e0 = counters(L)
+    rng = np.random.default_rng(seed)
+    msgs = []
+    for i in range(400):
+        data = rng.integers(0, 256, int(rng.integers(0, 2000)), dtype=np.uint8).tobytes()
+        c = orc.encode(data)
+        if i % 3 == 1:
+            c = b"\r\n".join(c[j:j + 76] for j in range(0, len(c), 76))
+        msgs.append(c)
+    got, err = util.ingress_stacks(msgs, 200, lib=L)
+    assert err == 0
+    assert bad_streams(msgs, got) == []
+    if pct == 100:  # every batch called back early: each one was caught
+        assert counters(L)[1] > e0[1]
+
+
+def test_egress_stacks_reordered():
+    """Encoder stages and the chunkencoder over hub batches completing in
+    random orders: framed bytes equal the oracle stack's."""
+    L = fake()
+    L.fake_configure(9, 0, 0)
+    lens = [int(x) for x in util.zipf_lengths(300, seed=0x31, rmax=512)]
+    payload = util.splitmix64(0x5EED, sum(lens))
+    got, err = util.egress_stacks(payload, lens, 1 << 20, 4096, lib=L)
+    assert err == 0
+    off = 0
+    for i, n in enumerate(lens):
+        want = orc.chunked_encode(payload[off:off + n].tobytes(), max_chunk=1 << 20,
+                                  read_size=4096)
+        off += n
+        assert got[i] == want, i
+
+
+def test_reference_topology_on_fake_device():
+    """The reference test's own topology (test/asynctest-base64encoder.c:
+    123-151) through the stages with reordered, early completions."""
+    L = fake()
+    L.fake_configure(3, 20, 0)
+    d = util.golden("digests.json")["G1"]
+    res, err, eagains = util.stage_reftest(200001, lib=L)
+    assert err == 0 and res is not None
+    enc, dec = res
+    assert dec == util.counting(200001).tobytes()
+    assert enc == orc.encode(util.counting(200001).tobytes(), ".", "_", True, "-")
+    assert d["out_len"] == 1333336  # the full-size digest stays a GPU test
+
+
+@pytest.mark.parametrize("cap", ["4096", "100"])
+def test_reference_topology_small_blocks(monkeypatch, cap):
+    """The decoder gathers its blocks through nice(91) from the encoder, so
+    the encoder reserves hub room while the decoder's reservation is open:
+    nested reservations must not share or recycle an arena."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", cap)
+    monkeypatch.setenv("ASYNC_B64_MIN_PULL", "1")
+    L = fake()
+    L.fake_configure(4, 30, 0)
+    res, err, eagains = util.stage_reftest(100003, lib=L)
+    assert err == 0 and res is not None
+    enc, dec = res
+    assert enc == orc.encode(util.counting(100003).tobytes(), ".", "_", True, "-")
+    assert dec == util.counting(100003).tobytes()

@@ -33,7 +33,10 @@ def counting(n: int) -> np.ndarray:
     return (np.arange(n, dtype=np.uint64) & 0xFF).astype(np.uint8)
 
 
+FAKE_HARNESS = os.path.join(ROOT, "tests", "csrc", "libstage_fake.so")
+
 _harness = None
+_fake = None
 
 
 def harness() -> ctypes.CDLL:
@@ -44,40 +47,65 @@ def harness() -> ctypes.CDLL:
             import torch  # noqa: F401  (one HIP runtime: see async_amd/_lib.py)
         except ImportError:
             pass
-        L = ctypes.CDLL(HARNESS)
-        sz, ssz, vp, ch, ip = (ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p,
-                               ctypes.c_char, ctypes.POINTER(ctypes.c_int))
-        L.h_reftest.argtypes = [sz, vp, sz, ctypes.POINTER(sz), vp, sz, ip,
-                                ctypes.POINTER(sz)]
-        L.h_reftest.restype = ssz
-        L.h_encode_stream.argtypes = [vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
-        L.h_encode_stream.restype = ssz
-        L.h_decode_stream.argtypes = [vp, sz, sz, sz, ch, ch, vp, sz, ip]
-        L.h_decode_stream.restype = ssz
-        L.h_copy_stream.argtypes = [vp, sz, sz, sz, vp, sz, ip, ctypes.POINTER(sz)]
-        L.h_copy_stream.restype = ssz
-        L.h_encode_counts.argtypes = [vp, sz, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
-        L.h_encode_counts.restype = ssz
-        L.h_chunk_stream.argtypes = [vp, sz, sz, sz, ctypes.c_int, sz, vp, sz, ip]
-        L.h_chunk_stream.restype = ssz
-        L.h_queue_stream.argtypes = [vp, vp, sz, ctypes.c_int, sz, sz, vp, sz, ip,
-                                     ctypes.POINTER(sz)]
-        L.h_queue_stream.restype = ssz
-        L.h_egress_stacks.argtypes = [vp, vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, vp,
-                                      vp, ip, vp]
-        L.h_egress_stacks.restype = ctypes.c_int
-        L.h_egress_stacks_mt.argtypes = L.h_egress_stacks.argtypes + [sz]
-        L.h_egress_stacks_mt.restype = ctypes.c_int
-        L.h_egress_stacks_mt_dev.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
-        L.h_egress_stacks_mt_dev.restype = ctypes.c_int
-        L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
-        L.h_ingress_stacks.restype = ctypes.c_int
-        L.h_prof_start.argtypes = [ctypes.c_int]
-        L.h_prof_stop.argtypes = [ctypes.c_char_p]
-        L.h_device_count.argtypes = []
-        L.h_device_count.restype = ctypes.c_int
-        _harness = L
+        _harness = _bind(ctypes.CDLL(HARNESS))
     return _harness
+
+
+def fake_harness() -> ctypes.CDLL:
+    """tests/csrc/libstage_fake.so: the same harness and the product's host
+    C (loop, streams, framing, hub, stages) over the CPU stand-in for the
+    GPU side (tests/csrc/fake_b64x.c).  No GPU, no HIP runtime."""
+    global _fake
+    if _fake is None:
+        L = _bind(ctypes.CDLL(FAKE_HARNESS))
+        L.fake_configure.argtypes = [ctypes.c_uint64, ctypes.c_uint, ctypes.c_int]
+        L.fake_configure.restype = None
+        L.fake_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+        L.fake_stats.restype = None
+        L.b64x_diag_counters.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+        L.b64x_diag_counters.restype = None
+        _fake = L
+    return _fake
+
+
+def _lib_or_default(lib):
+    return lib if lib is not None else harness()
+
+
+def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
+    """Argument types of the harness entry points (both builds)."""
+    sz, ssz, vp, ch, ip = (ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p,
+                           ctypes.c_char, ctypes.POINTER(ctypes.c_int))
+    L.h_reftest.argtypes = [sz, vp, sz, ctypes.POINTER(sz), vp, sz, ip,
+                            ctypes.POINTER(sz)]
+    L.h_reftest.restype = ssz
+    L.h_encode_stream.argtypes = [vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
+    L.h_encode_stream.restype = ssz
+    L.h_decode_stream.argtypes = [vp, sz, sz, sz, ch, ch, vp, sz, ip]
+    L.h_decode_stream.restype = ssz
+    L.h_copy_stream.argtypes = [vp, sz, sz, sz, vp, sz, ip, ctypes.POINTER(sz)]
+    L.h_copy_stream.restype = ssz
+    L.h_encode_counts.argtypes = [vp, sz, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
+    L.h_encode_counts.restype = ssz
+    L.h_chunk_stream.argtypes = [vp, sz, sz, sz, ctypes.c_int, sz, vp, sz, ip]
+    L.h_chunk_stream.restype = ssz
+    L.h_queue_stream.argtypes = [vp, vp, sz, ctypes.c_int, sz, sz, vp, sz, ip,
+                                 ctypes.POINTER(sz)]
+    L.h_queue_stream.restype = ssz
+    L.h_egress_stacks.argtypes = [vp, vp, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, vp,
+                                  vp, ip, vp]
+    L.h_egress_stacks.restype = ctypes.c_int
+    L.h_egress_stacks_mt.argtypes = L.h_egress_stacks.argtypes + [sz]
+    L.h_egress_stacks_mt.restype = ctypes.c_int
+    L.h_egress_stacks_mt_dev.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
+    L.h_egress_stacks_mt_dev.restype = ctypes.c_int
+    L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
+    L.h_ingress_stacks.restype = ctypes.c_int
+    L.h_prof_start.argtypes = [ctypes.c_int]
+    L.h_prof_stop.argtypes = [ctypes.c_char_p]
+    L.h_device_count.argtypes = []
+    L.h_device_count.restype = ctypes.c_int
+    return L
 
 
 def cch(v) -> bytes:
@@ -94,36 +122,36 @@ def _buf(data: bytes):
 
 
 def stage_encode(data: bytes, burst=0, read_size=200, pos62=-1, pos63=-1, pad=True,
-                 padchar=-1):
+                 padchar=-1, lib=None):
     """Product encoder stage on the product loop; returns (bytes|None, errno)."""
     a, p = _buf(data)
     cap = (len(data) + 2) // 3 * 4 + 16
     out = np.empty(cap, np.uint8)
     err = ctypes.c_int(0)
-    n = harness().h_encode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
+    n = _lib_or_default(lib).h_encode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
                                   int(bool(pad)), cch(padchar), out.ctypes.data, cap,
                                   ctypes.byref(err))
     return (None if n < 0 else out[:n].tobytes()), err.value
 
 
-def stage_decode(data: bytes, burst=0, read_size=200, pos62=-1, pos63=-1):
+def stage_decode(data: bytes, burst=0, read_size=200, pos62=-1, pos63=-1, lib=None):
     a, p = _buf(data)
     cap = (len(data) + 3) // 4 * 3 + 16
     out = np.empty(cap, np.uint8)
     err = ctypes.c_int(0)
-    n = harness().h_decode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
+    n = _lib_or_default(lib).h_decode_stream(p, len(data), burst, read_size, cch(pos62), cch(pos63),
                                   out.ctypes.data, cap, ctypes.byref(err))
     return (None if n < 0 else out[:n].tobytes()), err.value
 
 
-def stage_reftest(length=1000001):
+def stage_reftest(length=1000001, lib=None):
     ecap = (length + 2) // 3 * 4 + 16
     enc = np.empty(ecap, np.uint8)
     dec = np.empty(length + 16, np.uint8)
     elen = ctypes.c_size_t(0)
     err = ctypes.c_int(0)
     eag = ctypes.c_size_t(0)
-    n = harness().h_reftest(length, enc.ctypes.data, ecap, ctypes.byref(elen),
+    n = _lib_or_default(lib).h_reftest(length, enc.ctypes.data, ecap, ctypes.byref(elen),
                             dec.ctypes.data, dec.size, ctypes.byref(err), ctypes.byref(eag))
     return (None if n < 0 else (enc[: elen.value].tobytes(), dec[:n].tobytes())), \
         err.value, eag.value
@@ -142,36 +170,36 @@ def zipf_lengths(n_msgs=16384, seed=0x2F, rmax=16384, s=1.1) -> np.ndarray:
 
 
 def encode_counts(data: bytes, read_size: int, burst=0, pos62=-1, pos63=-1, pad=True,
-                  padchar=-1):
+                  padchar=-1, lib=None):
     """The GPU encoder stage's positive read returns; (list|None, errno)."""
     a, p = _buf(data)
     cap = len(data) // 2 + 64
     counts = np.empty(cap, dtype=np.intp)
     err = ctypes.c_int(0)
-    n = harness().h_encode_counts(p, len(data), 0, burst, read_size, cch(pos62), cch(pos63),
+    n = _lib_or_default(lib).h_encode_counts(p, len(data), 0, burst, read_size, cch(pos62), cch(pos63),
                                   int(bool(pad)), cch(padchar), counts.ctypes.data, cap,
                                   ctypes.byref(err))
     return (None if n < 0 else counts[:min(n, cap)].tolist()), err.value
 
 
-def chunk_stream(data: bytes, max_chunk: int, termination=0, read_size=100, burst=0):
+def chunk_stream(data: bytes, max_chunk: int, termination=0, read_size=100, burst=0, lib=None):
     a, p = _buf(data)
     cap = len(data) + (len(data) // max(max_chunk, 2) + 2) * 16 + 16
     out = np.empty(cap, np.uint8)
     err = ctypes.c_int(0)
-    n = harness().h_chunk_stream(p, len(data), burst, max_chunk, termination, read_size,
+    n = _lib_or_default(lib).h_chunk_stream(p, len(data), burst, max_chunk, termination, read_size,
                                  out.ctypes.data, cap, ctypes.byref(err))
     return (None if n < 0 else out[:n].tobytes()), err.value
 
 
-def queue_stream(pieces, push=False, burst=0, read_size=100):
+def queue_stream(pieces, push=False, burst=0, read_size=100, lib=None):
     data = b"".join(pieces)
     a, p = _buf(data)
     lens = np.asarray([len(x) for x in pieces] or [0], dtype=np.uintp)
     out = np.empty(len(data) + 16, np.uint8)
     err = ctypes.c_int(0)
     eag = ctypes.c_size_t(0)
-    n = harness().h_queue_stream(p, lens.ctypes.data, len(pieces), int(push), burst,
+    n = _lib_or_default(lib).h_queue_stream(p, lens.ctypes.data, len(pieces), int(push), burst,
                                  read_size, out.ctypes.data, out.size, ctypes.byref(err),
                                  ctypes.byref(eag))
     return (None if n < 0 else out[:n].tobytes()), err.value, eag.value
@@ -188,7 +216,7 @@ def device_count() -> int:
 
 def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos62=-1,
                   pos63=-1, pad=True, padchar=-1, times=None, raw=False, threads=1,
-                  devices=1):
+                  devices=1, lib=None):
     """Run len(lens) GPU egress stacks on `threads` loops (loop t on GPU
     t mod `devices` when devices > 1); returns
     (list of framed bytes | None, errno).  `times` (a float64[2] array)
@@ -210,11 +238,11 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
             cch(pos63), int(bool(pad)), cch(padchar), out.ctypes.data, out_off.ctypes.data,
             out_len.ctypes.data, ctypes.byref(err), tp)
     if devices > 1:
-        rc = harness().h_egress_stacks_mt_dev(*args, max(threads, 1), devices)
+        rc = _lib_or_default(lib).h_egress_stacks_mt_dev(*args, max(threads, 1), devices)
     elif threads > 1:
-        rc = harness().h_egress_stacks_mt(*args, threads)
+        rc = _lib_or_default(lib).h_egress_stacks_mt(*args, threads)
     else:
-        rc = harness().h_egress_stacks(*args)
+        rc = _lib_or_default(lib).h_egress_stacks(*args)
     if rc != 0:
         return None, err.value
     if raw:
@@ -223,7 +251,7 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
             for i in range(lens.size)], 0
 
 
-def ingress_stacks(msgs, read_size: int, pos62=-1, pos63=-1, times=None):
+def ingress_stacks(msgs, read_size: int, pos62=-1, pos63=-1, times=None, lib=None):
     """Run len(msgs) GPU decoder stacks (queuestream -> base64_decode) on one
     loop; returns (list of decoded bytes | None, errno)."""
     lens = np.array([len(m) for m in msgs], np.uint64)
@@ -237,7 +265,7 @@ def ingress_stacks(msgs, read_size: int, pos62=-1, pos63=-1, times=None):
     out_len = np.zeros(max(lens.size, 1), np.uint64)
     err = ctypes.c_int(0)
     tp = times.ctypes.data if times is not None else None
-    rc = harness().h_ingress_stacks(src.ctypes.data, in_off.ctypes.data, lens.size, read_size,
+    rc = _lib_or_default(lib).h_ingress_stacks(src.ctypes.data, in_off.ctypes.data, lens.size, read_size,
                                     cch(pos62), cch(pos63), out.ctypes.data,
                                     out_off.ctypes.data, out_len.ctypes.data,
                                     ctypes.byref(err), tp)
