@@ -3,7 +3,8 @@
 #   make            -> async_amd/libasync_b64.so  (product: HIP kernels + C ABI
 #                      + bytestream_1 stages + minimal loop/streams)
 #                      oracle/liboracle.so          (test infrastructure only)
-#                      tests/csrc/libstage_harness.so (test infrastructure only)
+#                      tests/csrc/libstage_harness.so, libstage_fake.so,
+#                      libb64x_hooks.so     (test infrastructure only)
 #   make clean
 #
 # Everything is compiled for gfx950 only (no other offload targets, no
@@ -41,8 +42,11 @@ HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
 # side (tests/csrc/fake_b64x.c): deterministic, adversarially ordered tests
 # of the stages' slot accounting, no GPU needed (test infrastructure only).
 FAKE     = tests/csrc/libstage_fake.so
+# The kernels again with the test-only hooks compiled in (B64X_TEST_HOOKS:
+# forced decode range lengths); never linked into the product libraries.
+HOOKS    = tests/csrc/libb64x_hooks.so
 
-all: $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE)
+all: $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE) $(HOOKS)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -52,6 +56,12 @@ $(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_ch
 
 $(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h | $(OBJDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OBJDIR)/b64x_kernels_hooks.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DB64X_TEST_HOOKS -c $< -o $@
+
+$(HOOKS): $(OBJDIR)/b64x_kernels_hooks.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libb64x_hooks.so
 
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
@@ -73,7 +83,7 @@ $(FAKE): tests/csrc/stage_harness.c tests/csrc/fake_b64x.c oracle/b64_oracle.c $
 	    tests/csrc/fake_b64x.c oracle/b64_oracle.c $(HOST_SRC) -lpthread
 
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE)
+	rm -rf $(OBJDIR) $(LIB) $(CORE) $(ORACLE) $(HARNESS) $(FAKE) $(HOOKS)
 
 .PHONY: all clean
 

@@ -371,32 +371,6 @@ __global__ __launch_bounds__(kThreads) void k_encode(
     }
 }
 
-// Runtime tuning knobs (scripts/bench_variants.py; not part of the public
-// ABI).  Index: 0 = encode variant, 1 = decode pass-1 variant, 2 = range
-// chunks, 3 = plain-store pricing, 4 = batch kernel layout (bit 0 grouped,
-// bit 1 cached loads, any bit: not the tight/row kernels), 5 = pass 2 of
-// the exact decode (0: bit-stream pass2d, 4: pass2c, the per-character
-// scatter), 6 = 1: the first-form tight/row batch kernels, 7 = lanes'
-// slots per batch-kernel tile (2 or 4), 8 = decode scan (2: look-back
-// priced out, 3: tiles by block index), 9 = single-pass decode pricing
-// (bit 0: no look-back, bit 1: no decode phase; wrong results, A/B only).
-int g_tune[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-
-// ASYNC_B64_TUNE="i=v,i=v": kernel-variant knobs for A/B runs of the whole
-// test suite or bench (the same knobs b64x__tune sets).
-__attribute__((constructor)) void tune_from_env()
-{
-    const char *v = getenv("ASYNC_B64_TUNE");
-    while (v && *v) {
-        char *end;
-        const long i = strtol(v, &end, 10);
-        if (*end != '=') break;
-        const long x = strtol(end + 1, &end, 10);
-        if (i >= 0 && i < 10) g_tune[i] = (int) x;
-        v = *end == ',' ? end + 1 : nullptr;
-    }
-}
-
 template <bool NT>
 DEV void store16(uint8_t *p, uint4 o)
 {
@@ -407,16 +381,6 @@ DEV void store16(uint8_t *p, uint4 o)
     }
 }
 
-// One dword-aligned device buffer (the BASELINE config-2 hot path).  The
-// n/12 full quads form tiles of U quads per lane (U x 768 B in per wave);
-// blocks take whole tiles grid-stride with no per-lane guards, so loads
-// and stores are never exec-masked and the compiler can wait on loads with
-// counted vmcnt instead of draining the stores (vmcnt counts both).  With
-// PIPE the next tile's loads are issued before this tile's compute; LNT/NT
-// make loads/stores non-temporal.  Launched with one block per tile (a
-// non-persistent grid streams fastest here: tests/tools/copy_sweep.hip).  The
-// last, partial tile and the final n mod 12 bytes (with padding) are done
-// by the last block.
 template <bool NT>
 DEV u32x3a4 ld12(const uint8_t *p)
 {
@@ -424,7 +388,19 @@ DEV u32x3a4 ld12(const uint8_t *p)
     return *(const u32x3a4 *) p;
 }
 
-template <int U, bool PIPE, bool LNT, bool NT>
+// One dword-aligned device buffer (the BASELINE config-2 hot path).  The
+// n/12 full quads form tiles of kFlatU quads per lane (kFlatU x 768 B in
+// per wave); a block takes whole tiles with no per-lane guards, so loads
+// and stores are never exec-masked and the compiler can wait on loads with
+// counted vmcnt instead of draining the stores (vmcnt counts both).  Loads
+// and stores are non-temporal.  Launched with one block per tile (a
+// non-persistent grid streams fastest here: tests/tools/copy_sweep.hip; the
+// loop only matters past 2^31 tiles).  The last, partial tile and the final
+// n mod 12 bytes (with padding) are done by the last block.  Round 1's A/B
+// of tile depth (1-8 quads), software pipelining and cached loads picked
+// this form (profiles/r01_v6_*).
+constexpr int kFlatU = 2;
+
 __global__ __launch_bounds__(kThreads) void k_encode_flat(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
 {
@@ -432,83 +408,26 @@ __global__ __launch_bounds__(kThreads) void k_encode_flat(
     build_enc_table(tab, a);
     __syncthreads();
     const uint64_t nq = n / 12;
-    const uint64_t tile = (uint64_t) kThreads * U;
+    const uint64_t tile = (uint64_t) kThreads * kFlatU;
     const uint64_t full = nq / tile;
     const uint32_t tid = threadIdx.x;
-    uint64_t t = blockIdx.x;
-    if (t < full) {
-        u32x3a4 cur[U];
+    for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
+        u32x3a4 cur[kFlatU];
         const uint8_t *src = in + (t * tile + tid) * 12;
 #pragma unroll
-        for (int u = 0; u < U; u++) cur[u] = ld12<LNT>(src + u * kThreads * 12);
-        for (;;) {
-            const uint64_t tn = t + gridDim.x;
-            u32x3a4 nxt[U];
-            if (PIPE) {
-                // unconditional (re-reads this tile on the last trip) so
-                // the compute below waits on exactly the older loads
-                const uint64_t tl = tn < full ? tn : t;
-                const uint8_t *nsrc = in + (tl * tile + tid) * 12;
+        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<true>(src + u * kThreads * 12);
+        uint8_t *dst = out + (t * tile + tid) * 16;
 #pragma unroll
-                for (int u = 0; u < U; u++) nxt[u] = ld12<LNT>(nsrc + u * kThreads * 12);
-            }
-            uint8_t *dst = out + (t * tile + tid) * 16;
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                store16<NT>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
-            if (tn >= full) break;
-            t = tn;
-            const uint8_t *src2 = in + (t * tile + tid) * 12;
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                cur[u] = PIPE ? nxt[u] : ld12<LNT>(src2 + u * kThreads * 12);
-        }
+        for (int u = 0; u < kFlatU; u++)
+            store16<true>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
     }
     if (blockIdx.x == gridDim.x - 1) {
-        for (uint64_t q = full * tile + tid; q < nq; q += kThreads)
-            store16<NT>(out + q * 16, enc_quad(tab, ((const u32x3a4 *) (in + q * 12))->x,
-                                                ((const u32x3a4 *) (in + q * 12))->y,
-                                                ((const u32x3a4 *) (in + q * 12))->z));
+        for (uint64_t q = full * tile + tid; q < nq; q += kThreads) {
+            const u32x3a4 v = *(const u32x3a4 *) (in + q * 12);
+            store16<true>(out + q * 16, enc_quad(tab, v.x, v.y, v.z));
+        }
         if (tid == 0 && n % 12)
             enc_bytes(tab, in + nq * 12, (uint32_t) (n % 12), out + nq * 16, true, a);
-    }
-}
-
-// Calibration probe: a pure stream with a kernel's access widths --
-// RD bytes loaded and WR bytes stored per lane per slot (12 or 16), U slots
-// per lane per tile, whole tiles grid-stride -- to measure the HBM rate the
-// same traffic shape reaches without any base64 work.
-template <int RD, int WR, bool NT>
-__global__ __launch_bounds__(kThreads) void k_copy_probe(
-    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t slots)
-{
-    constexpr int U = 4;
-    const uint64_t tile = (uint64_t) kThreads * U;
-    const uint64_t full = slots / tile;
-    for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
-        const uint64_t s0 = t * tile + threadIdx.x;
-        uint4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint8_t *p = in + (s0 + u * kThreads) * RD;
-            if (RD == 16) {
-                v[u] = *(const uint4 *) p;
-            } else {
-                u32x3a4 x = *(const u32x3a4 *) p;
-                v[u] = make_uint4(x.x, x.y, x.z, x.x ^ x.y);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            uint8_t *q = out + (s0 + u * kThreads) * WR;
-            if (WR == 16) {
-                store16<NT>(q, v[u]);
-            } else if (NT) {
-                __builtin_nontemporal_store(u32x3a4{v[u].x, v[u].y, v[u].z ^ v[u].w}, (u32x3a4 *) q);
-            } else {
-                *(u32x3a4 *) q = u32x3a4{v[u].x, v[u].y, v[u].z ^ v[u].w};
-            }
-        }
     }
 }
 
@@ -557,144 +476,6 @@ __global__ __launch_bounds__(kThreads) void k_encode_strided(
             else
                 enc_bytes(tab, srcs[u], r, dsts[u], avails[u] <= 12, a);
         }
-    }
-}
-
-// Uniform-stride batch encode, grouped: block g owns buffers
-// [g*bpb, (g+1)*bpb) -- a run whose input and output spans start on 128-B
-// lines (bpb is chosen so), so no line is shared between blocks, which the
-// GPU spreads over XCDs with separate L2s (a shared line is fetched once
-// per XCD: the 22 % over-fetch of k_encode_strided on config 4).  Lanes
-// walk the block's bpb*qpb (buffer, quad) slots in order; the buffer index
-// is a multiply-high by magic = ceil(2^32/qpb), exact while slots < 2^16.
-template <int U, bool NTL>
-__global__ __launch_bounds__(kThreads) void k_encode_group(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
-    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
-    uint32_t qpb, uint32_t bpb, uint32_t magic, EncAlpha a)
-{
-    __shared__ uint8_t tab[64];
-    build_enc_table(tab, a);
-    __syncthreads();
-    const uint32_t b0 = blockIdx.x * bpb;
-    const uint32_t nb = min(bpb, nbuf - b0);
-    const uint32_t slots = nb * qpb;
-    const uint8_t *gin = in + (uint64_t) b0 * in_stride;
-    uint8_t *gout = out + (uint64_t) b0 * out_stride;
-    for (uint32_t s0 = 0; s0 < slots; s0 += U * kThreads) {
-        u32x3a4 v[U];
-        const uint8_t *srcs[U];
-        uint8_t *dsts[U];
-        uint32_t avails[U];
-        bool fast[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t t = s0 + u * kThreads + threadIdx.x;
-            fast[u] = false;
-            avails[u] = 0;
-            srcs[u] = gin;
-            dsts[u] = gout;
-            if (t < slots) {
-                const uint32_t b = __umulhi(t, magic), q = t - b * qpb;
-                srcs[u] = gin + (uint64_t) b * in_stride + q * 12u;
-                dsts[u] = gout + (uint64_t) b * out_stride + q * 16u;
-                const uint64_t av = len - (uint64_t) q * 12;
-                avails[u] = av > 12 ? 13u : (uint32_t) av;
-                fast[u] = av >= 12 && ((((uintptr_t) srcs[u]) | ((uintptr_t) dsts[u])) & 3) == 0;
-                if (fast[u]) v[u] = ld12<NTL>(srcs[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (fast[u]) {
-                store16<true>(dsts[u], enc_quad(tab, v[u].x, v[u].y, v[u].z));
-            } else if (avails[u]) {
-                const uint32_t r = avails[u] < 12 ? avails[u] : 12;
-                if (avails[u] < 12 && (((uintptr_t) srcs[u]) & 3) == 0)
-                    enc_tail(tab, srcs[u], r, dsts[u], a);
-                else
-                    enc_bytes(tab, srcs[u], r, dsts[u], avails[u] <= 12, a);
-            }
-        }
-    }
-}
-
-// Encode the lane whose 16 characters cross buffer b's padded last group
-// (len % 3 = r != 0): groups before it are ordinary, the partial group has
-// r bytes and its padding, groups after it belong to buffer b+1 and start
-// 3-r bytes earlier in the (contiguous) input.  x, y, z: the 12 input bytes
-// from the lane's first group on; p: the lane's character offset in b.
-DEV uint4 enc_seam(const uint8_t *tab, uint32_t x, uint32_t y, uint32_t z, uint32_t p,
-                   uint32_t E, uint32_t r, const EncAlpha &a)
-{
-    uint32_t o[4];
-#pragma unroll
-    for (uint32_t g = 0; g < 4; g++) {
-        const uint32_t c = p + 4 * g;
-        const bool partial = c + 4 == E, after = c + 4 > E;
-        const uint32_t off = 3 * g - (after ? 3 - r : 0);
-        const uint32_t wi = off >> 2, sh = (off & 3) * 8;
-        const uint32_t lo = wi == 0 ? x : wi == 1 ? y : z;
-        const uint32_t hi = wi == 0 ? y : wi == 1 ? z : 0u;
-        const uint32_t d = (uint32_t) ((((uint64_t) hi << 32) | lo) >> sh);
-        uint32_t b0 = d & 0xFFu, b1 = (d >> 8) & 0xFFu, b2 = (d >> 16) & 0xFFu;
-        if (partial) {
-            b2 = 0;
-            if (r == 1) b1 = 0;
-        }
-        uint32_t ch = enc_group(tab, (b0 << 16) | (b1 << 8) | b2);
-        if (partial)
-            ch = r == 1 ? (ch & 0xFFFFu) | (a.padc * 0x01010000u)
-                        : (ch & 0xFFFFFFu) | (a.padc << 24);
-        o[g] = ch;
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-// Batch encode for the tight layout (in_stride = len, out_stride = E: the
-// batch is one contiguous character stream), indexed by output slot: lane
-// t writes characters [16t, 16t+16) with one aligned dwordx4 store and
-// reads the 12 bytes they come from with one dwordx4 load at the dword
-// below (realigned with v_alignbyte).  Only the lane that holds a
-// buffer's padded last group (one in E/16) takes enc_seam(); loads and
-// stores stay unmasked in full tiles (GUARD only in the remainder launch).
-// Buffer b = umulhi64(16t, ceil(2^64/E)); the last buffer is left to the
-// caller (its lanes could read past the input).
-template <int U, bool GUARD>
-__global__ __launch_bounds__(kThreads) void k_encode_tight(
-    const uint8_t *__restrict__ in, uint64_t len, uint32_t E, uint32_t r, uint64_t m64,
-    uint8_t *__restrict__ out, uint64_t slot0, uint64_t nslots, EncAlpha a)
-{
-    __shared__ uint8_t tab[64];
-    build_enc_table(tab, a);
-    __syncthreads();
-    uint32_t x[U], y[U], z[U], pp[U];
-    bool seam[U];
-    const uint64_t base = slot0 + (uint64_t) blockIdx.x * U * kThreads + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint64_t t = base + (uint64_t) u * kThreads;
-        const uint64_t o = 16 * t;
-        const uint64_t b = __umul64hi(o, m64);
-        const uint32_t p = (uint32_t) (o - b * E);
-        const uint64_t pos = b * len + 3 * (uint64_t) (p >> 2);
-        pp[u] = p;
-        seam[u] = r != 0 && p + 16 >= E;
-        x[u] = y[u] = z[u] = 0;
-        if (!GUARD || t < nslots) {
-            const u32x4a4 w = __builtin_nontemporal_load((const u32x4a4 *) (in + (pos & ~3ull)));
-            const uint32_t s = (uint32_t) (pos & 3);
-            x[u] = __builtin_amdgcn_alignbyte(w.y, w.x, s);
-            y[u] = __builtin_amdgcn_alignbyte(w.z, w.y, s);
-            z[u] = __builtin_amdgcn_alignbyte(w.w, w.z, s);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint64_t t = base + (uint64_t) u * kThreads;
-        uint4 c = enc_quad(tab, x[u], y[u], z[u]);
-        if (seam[u]) c = enc_seam(tab, x[u], y[u], z[u], pp[u], E, r, a);
-        if (!GUARD || t < nslots) store16<true>(out + 16 * t, c);
     }
 }
 
@@ -834,14 +615,6 @@ DEV void wave_lds_order()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Four sextets (bits 23..0 of a group) from dword `d` holding them as
-// bytes 0..3 in stream order.
-DEV uint32_t group_of_bytes(uint32_t d)
-{
-    return ((d & 0xFFu) << 18) | (((d >> 8) & 0xFFu) << 12) |
-           (((d >> 16) & 0xFFu) << 6) | (d >> 24);
-}
-
 // Four groups -> 12 output bytes as three little-endian dwords.
 DEV void groups_to_bytes(uint32_t G0, uint32_t G1, uint32_t G2, uint32_t G3,
                          uint32_t &o0, uint32_t &o1, uint32_t &o2)
@@ -944,19 +717,6 @@ DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
         lc.G[g] = v;
     }
     lc.vmask = m;
-}
-
-// Emit the final, incomplete group (1..3 sextets at sx[0..r)):
-// floor(6r/8) bytes, exactly what the reference's accumulator has produced
-// when its upstream reaches EOF (src/base64decoder.c:59-62,71-76).
-DEV void emit_partial(uint8_t *sx, uint8_t *dst, int r)
-{
-    if (lane_id() == 0 && r >= 2) {
-        uint32_t G = ((uint32_t) sx[0] << 18) | ((uint32_t) sx[1] << 12) |
-                     (r > 2 ? (uint32_t) sx[2] << 6 : 0u);
-        dst[0] = (uint8_t) (G >> 16);
-        if (r > 2) dst[1] = (uint8_t) (G >> 8);
-    }
 }
 
 // Fast path (a): a lane's 16 alphabet characters, as 4 groups, to 12 bytes.
@@ -1133,7 +893,7 @@ DEV void p1_chunk(const uint8_t *tab, uint4 w, uint32_t nin, uint64_t pos, uint6
 // one-chunk loop that still emits fast-path chunks until one does not fit;
 // that chunk is published (atomicMax of the complemented (range, offset))
 // and the range only counts from then on.
-template <int U, bool PIPE, bool NT>
+template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7)))
 void k_decode_pass1(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
@@ -1161,13 +921,6 @@ void k_decode_pass1(
             cur[u] = ld16<NT>(in + pos + (uint64_t) u * kChunk + 16 * lane);
         for (;;) {
             const uint64_t np = pos + (uint64_t) kChunk * U;
-            uint4 nxt[U];
-            if (PIPE) {
-                const uint64_t lp = np < hot_end ? np : pos;  // unconditional load
-#pragma unroll
-                for (int u = 0; u < U; u++)
-                    nxt[u] = ld16<NT>(in + lp + (uint64_t) u * kChunk + 16 * lane);
-            }
             int u = 0;
 #pragma unroll
             for (; u < U; u++) {
@@ -1196,7 +949,7 @@ void k_decode_pass1(
             if (pos >= hot_end) break;
 #pragma unroll
             for (int v = 0; v < U; v++)
-                cur[v] = PIPE ? nxt[v] : ld16<NT>(in + pos + (uint64_t) v * kChunk + 16 * lane);
+                cur[v] = ld16<NT>(in + pos + (uint64_t) v * kChunk + 16 * lane);
         }
     }
     for (; pos < re; pos += 2 * (uint64_t) kChunk) {
@@ -1324,19 +1077,17 @@ DEV uint64_t st_load(uint64_t *p)
 // tile of 1024 ranges.  Clean call (no first-dirty record): block 0 alone
 // computes V from the last range's count and the result record; every
 // other block returns at once.  Dirty call: a single-pass scan of
-// counts[r0 ..] with decoupled look-back.  With TK (the default) blocks
-// take tiles from a ticket in the order they start, so a tile's
-// predecessors are always running or done and the look-back cannot wait on
-// a block that is not yet dispatched, whatever else shares the GPU (+6 us
-// on 1 GiB; TK = 0, tile = block index, relies on in-order dispatch across
-// the XCDs).  Each tile publishes its aggregate, looks back over its
+// counts[r0 ..] with decoupled look-back.  Blocks take tiles from a ticket
+// in the order they start, so a tile's predecessors are always running or
+// done and the look-back cannot wait on a block that is not yet dispatched,
+// whatever else shares the GPU (6 us more on 1 GiB than tiles by block
+// index, which relies on in-order dispatch across the XCDs).  Each tile publishes its aggregate, looks back over its
 // predecessors 64 at a time (one wave) until an inclusive prefix,
 // publishes its own and writes the bases of its ranges.  The last tile
 // writes the result record and the tail sextets, waits until every tile
 // has published its inclusive prefix (so no look-back is still reading)
 // and every block has its ticket, then clears the status words and the
 // ticket and re-arms the workspace (fd -> fd_cur).
-template <int PRICE, int TK>
 __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
     DecAlpha a, void *ws, b64x_dec_result *res, b64x_dec_result *hres, uint32_t hold)
@@ -1361,12 +1112,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     }
     const uint32_t r0 = (uint32_t) (~packed >> 32);
     const uint32_t ntiles = (nranges - r0 + kScanTile - 1) / kScanTile;
-    uint32_t t = blockIdx.x;
-    if (TK) {
-        if (threadIdx.x == 0) s_tile = atomicAdd(w.ticket, 1u);
-        __syncthreads();
-        t = s_tile;
-    }
+    if (threadIdx.x == 0) s_tile = atomicAdd(w.ticket, 1u);
+    __syncthreads();
+    const uint32_t t = s_tile;
     if (t >= ntiles) return;
     build_dec_table(tab, a);
     const uint32_t base = r0 + t * kScanTile + 4 * threadIdx.x;
@@ -1382,7 +1130,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint32_t lane = lane_id();
     if (threadIdx.x < 64) {
         uint64_t excl = (uint64_t) r0 * R;
-        if (t > 0 && PRICE == 0) {
+        if (t > 0) {
             if (lane == 0) st_store(&w.status[t], kStAgg | agg);
             excl = 0;
             int64_t p = (int64_t) t - 1;
@@ -1420,24 +1168,20 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
         const uint64_t V = s_excl + agg;
         if (lane == 0) write_result(res, hres, V, hold);
         find_tail_sextets(tab, in, n, V, res, hres);
-        if (PRICE == 0) {
-            // every tile inclusive -> every look-back is over
-            for (;;) {
-                bool all = true;
-                for (uint32_t i = lane; i < ntiles; i += 64)
-                    all = all && (st_load(&w.status[i]) >> 62) == 2;
-                if (__all(all)) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
+        for (;;) {  // every tile inclusive -> every look-back is over
+            bool all = true;
+            for (uint32_t i = lane; i < ntiles; i += 64)
+                all = all && (st_load(&w.status[i]) >> 62) == 2;
+            if (__all(all)) break;
+            __builtin_amdgcn_s_sleep(1);
         }
         for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.status[i], 0);
         if (lane == 0) {
-            if (TK) {  // every block has its ticket -> re-arm the counter
-                while (__hip_atomic_load(w.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                       gridDim.x)
-                    __builtin_amdgcn_s_sleep(1);
-                __hip_atomic_store(w.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            // every block has its ticket -> re-arm the counter
+            while (__hip_atomic_load(w.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                   gridDim.x)
+                __builtin_amdgcn_s_sleep(1);
+            __hip_atomic_store(w.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *w.fd_cur = packed;
             *w.fd = 0;
         }
@@ -1446,75 +1190,10 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
 
 // ---- pass 2: shared pieces ----------------------------------------------
 //
-// Ranges of kP2Range characters; both pass-2 forms issue all of a range's
-// loads at once (its base, both chunks, 64 lookahead bytes) and, for the
-// middle ranges, the next range's before processing this one.
+// Ranges of kP2Range characters; pass 2 issues all of a range's loads at
+// once (its base, both chunks, 64 lookahead bytes) and, for the middle
+// ranges, the next range's before processing this one.
 constexpr uint32_t kP2Range = 2048;
-constexpr uint32_t kP2Sx = kP2Range + 64;        // + lookahead, 16-aligned
-constexpr uint32_t kP2Bb = kP2Range / 4 * 3 + 64;
-
-// Exclusive prefix over the wave of x < 32, and the total: one ballot per
-// bit plane, no LDS traffic.
-DEV uint32_t wave_scan_small(uint32_t x, uint32_t &total)
-{
-    uint32_t ex = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const uint64_t b = __ballot((x >> i) & 1u);
-        ex += __builtin_amdgcn_mbcnt_hi((uint32_t) (b >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t) b, 0u)) << i;
-        tot += (uint32_t) __popcll(b) << i;
-    }
-    total = tot;
-    return ex;
-}
-
-// Store bytes bb[0..nb) (in LDS) to global `dst` (any alignment): dword
-// k of the aligned span covers dst bytes 4k-s .. 4k-s+3 (s = dst & 3).
-DEV void store_realigned(const uint32_t *bb, uint32_t nb, uint8_t *dst)
-{
-    const uint32_t lane = lane_id();
-    const uint32_t s = (uint32_t) ((uintptr_t) dst & 3);
-    uint8_t *a0 = dst - s;
-    const uint32_t K = (s + nb + 3) >> 2;
-    for (uint32_t k0 = 3 * lane; k0 < K; k0 += 3 * 64) {
-        uint32_t d[3];
-        bool full = true;
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const uint32_t k = k0 + i;
-            const uint32_t cur = k * 4 < nb + s ? bb[k < (nb + 3) / 4 ? k : 0] : 0u;
-            const uint32_t prv = k ? bb[k - 1] : 0u;
-            d[i] = s == 0 ? cur : __builtin_amdgcn_alignbyte(cur, prv, 4 - s);
-            const int j0 = (int) (4 * k) - (int) s;
-            full = full && j0 >= 0 && (uint32_t) j0 + 4 <= nb;
-        }
-        if (full) {
-            *(u32x3a4 *) (a0 + 4 * k0) = u32x3a4{d[0], d[1], d[2]};
-            continue;
-        }
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const int j0 = (int) (4 * (k0 + i)) - (int) s;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int j = j0 + b;
-                if (j >= 0 && (uint32_t) j < nb) dst[j] = (uint8_t) (d[i] >> (8 * b));
-            }
-        }
-    }
-}
-
-// ---- pass 2, scatter form (the previous default; ASYNC_B64_TUNE=5=4) -----
-//
-// A lane's 16 table values are packed as bytes (the value
-// of an alphabet character *is* its sextet; 0xFF otherwise), its valid
-// count is 16 - popc(P & 0x80808080) per dword, and the scatter is
-// branch-free: every character is written, the non-alphabet ones to a
-// dummy byte.  The wave's sextet buffer starts 16 bytes in, so the 0-3
-// sextets skipped at a range start land in the head instead of needing a
-// bounds test.
-constexpr uint32_t kP2cHead = 16;
 
 // A wave-uniform 64-bit load through the scalar cache (s_load, counted by
 // lgkmcnt): a vector load of a per-range base that is then made scalar
@@ -1524,18 +1203,6 @@ DEV uint64_t scalar_load_u64(const uint64_t *p)
 {
     return *(const __attribute__((address_space(4))) uint64_t *) p;
 }
-
-constexpr uint32_t kP2cPhys = kP2cHead + kP2Sx + 16;  // bytes per wave
-
-// Identity (a 4-per-128-byte pad swizzle against the scatter's bank
-// conflicts measured slower: 997 vs 928 us on dirty 1 GiB).
-DEV uint32_t swz(uint32_t p) { return p; }
-
-struct __attribute__((aligned(16))) P2cSmem {
-    uint8_t tab[256];
-    uint8_t sx[kWavesPerBlock][kP2cPhys];
-    uint32_t bb[kWavesPerBlock][kP2Bb / 4];
-};
 
 // The 16 table values of a lane's characters, packed 4 per dword; the
 // characters at and past `nin` read as non-alphabet.
@@ -1565,167 +1232,11 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
 }
 
-// One store per character, the non-alphabet ones to a dummy byte (a
-// per-dword v_perm compaction with predicated byte stores measured a
-// little slower).
-__global__ __launch_bounds__(kThreads) void k_decode_pass2c(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
-{
-    DecodeWs w = ws_view(ws, nranges);
-    const uint64_t packed = *w.fd_cur;
-    if (packed == 0) return;
-    const uint32_t r0 = (uint32_t) (~packed >> 32);
-    const uint32_t off0 = (uint32_t) ~packed;
-    __shared__ P2cSmem sm;
-    build_dec_table(sm.tab, a);
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *sxh = sm.sx[wv];  // logical byte p at sxh[swz(p)]; skipped sextets land
-                               // in the head, the range's first owned one at kP2cHead
-    const uint32_t dummy = swz(kP2cHead + kP2Sx + 8);  // target of non-alphabet bytes
-    uint32_t *bb = sm.bb[wv];
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    // One range: chunks c[] (nin[] characters of each lane in range), the
-    // lookahead byte la (valid if la_ok), its base B.
-    auto process = [&](uint32_t r, const uint4 *c, const uint32_t *nin, uint32_t la, bool la_ok,
-                       uint64_t B) {
-        const uint64_t rb = (uint64_t) r * R;
-        const uint64_t re = rb + R < n ? rb + R : n;
-        const bool last = r + 1 == nranges, first = r == r0;
-        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
-        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            uint32_t P[4];
-            lane_values(sm.tab, c[h], nin[h], P);
-            uint32_t tot;
-            const uint32_t ex = wave_scan_small(lane_valid_count(P), tot);
-            uint32_t cur = (uint32_t) ((int) kP2cHead + T + (int) ex);
-#pragma unroll
-            for (uint32_t g = 0; g < 4; g++) {
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t b = (P[g] >> (8 * j)) & 0xFFu;
-                    const bool ok = b < 64u;
-                    sxh[ok ? swz(cur) : dummy] = (uint8_t) b;
-                    cur += ok ? 1u : 0u;
-                }
-            }
-            T += (int) tot;
-        }
-        bool at_end = last;
-        if (!last && T > 0 && (T & 3)) {
-            // complete the range's last group from the characters after it
-            bool ok = la_ok;
-            for (uint64_t q = re;;) {
-                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
-                const bool v = t < 64u;
-                const uint64_t m = __ballot(v);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                const int need = 4 - (T & 3);
-                if (v && (int) rank < need) sxh[swz(kP2cHead + T + rank)] = (uint8_t) t;
-                const int got = __popcll(m);
-                if (got >= need) {
-                    T += need;
-                    break;
-                }
-                T += got;
-                q += 64;
-                if (q >= n) {
-                    at_end = true;  // the stream's final, incomplete group
-                    break;
-                }
-                ok = q + lane < n;
-                la = ok ? in[q + lane] : 0u;
-            }
-        }
-        wave_lds_order();
-        if (T > 0) {
-            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
-            for (uint32_t L = lane; 4 * L < ng; L += 64) {
-                const uint32_t *q4 = (const uint32_t *) (sxh + swz(kP2cHead + 16 * L));
-                const uint4 sv = make_uint4(q4[0], q4[1], q4[2], q4[3]);
-                uint32_t o0, o1, o2;
-                groups_to_bytes(group_of_bytes(sv.x), group_of_bytes(sv.y),
-                                group_of_bytes(sv.z), group_of_bytes(sv.w), o0, o1, o2);
-                bb[3 * L] = o0;
-                bb[3 * L + 1] = o1;
-                bb[3 * L + 2] = o2;
-            }
-            wave_lds_order();
-            store_realigned(bb, 3 * ng, ob);
-            if (rem && at_end && !hold && lane == 0) {
-                uint8_t tl[3];
-                for (uint32_t j = 0; j < rem; j++) tl[j] = sxh[swz(kP2cHead + 4 * ng + j)];
-                emit_partial(tl, ob + 3 * ng, (int) rem);
-            }
-        }
-        wave_lds_order();  // the next range reuses sx and bb
-    };
-    auto load_generic = [&](uint32_t r) {
-        const uint64_t rb = (uint64_t) r * R;
-        const uint64_t re = rb + R < n ? rb + R : n;
-        const bool last = r + 1 == nranges, first = r == r0;
-        const uint64_t start = first ? rb + off0 : rb;
-        uint4 c[2];
-        uint32_t nin[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
-        }
-        const bool la_ok = !last && re + lane < n;
-        const uint32_t la = la_ok ? in[re + lane] : 0u;
-        process(r, c, nin, la, la_ok, w.bases[r]);
-    };
-    uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
-    if (r == r0 && r < nranges) {
-        load_generic(r);
-        r += nw;
-    }
-    // Middle ranges (whole, neither first nor last): the next range's loads
-    // -- both chunks, the lookahead bytes (address clamped into the stream)
-    // and its base -- are issued before this range is processed.
-    const uint32_t mid_end = nranges - 1;
-    if (R == 2 * kChunk && r < mid_end && (((uintptr_t) in) & 3) == 0) {
-        const uint32_t full[2] = {16u, 16u};
-        auto ld_la = [&](uint32_t rr) {
-            const uint64_t q = (uint64_t) (rr + 1) * R + lane;
-            return (uint32_t) in[q < n ? q : n - 1];
-        };
-        uint4 c[2];
-        c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
-        c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
-        uint32_t la = ld_la(r);
-        uint64_t B = scalar_load_u64(w.bases + r);
-        while (r < mid_end) {
-            const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
-            uint4 cn[2];
-            cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
-            cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
-            const uint32_t lan = ld_la(rn);
-            const uint64_t Bn = scalar_load_u64(w.bases + rn);
-            process(r, c, full, la, (uint64_t) (r + 1) * R + lane < n, B);
-            r += nw;
-            c[0] = cn[0];
-            c[1] = cn[1];
-            la = lan;
-            B = Bn;
-        }
-    }
-    for (; r < nranges; r += nw) load_generic(r);
-}
-
 // ---- pass 2, bit-stream form ----------------------------------------------
 //
-// k_decode_pass2c spends most of its ~520 VALU per range on the per-character
-// scatter of sextets into LDS, the read-back and group conversion, and the
-// realigning store (PMC).  Here the range's output is built in LDS directly
-// as the decoded BIT stream: each lane compacts every dword of its table
+// The range's output is built in LDS directly as the decoded BIT stream (a
+// per-character scatter of sextets into LDS, read back and converted group
+// by group, cost ~520 VALU per range -- round 1's pass 2c): each lane compacts every dword of its table
 // values (v_perm, selector by the dword's invalid mask), turns the 0-4
 // surviving sextets into one left-aligned 24-bit field (two v_dot4), and
 // ORs that field into the wave's zeroed LDS buffer at bit 6 x (its sextet
@@ -1887,7 +1398,7 @@ template <bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
     uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold,
-    b64x_dec_result *res, b64x_dec_result *hres, uint32_t price = 0)
+    b64x_dec_result *res, b64x_dec_result *hres)
 {
     DecodeWs w = ws_view(ws, nranges);
     uint32_t r0 = 0xFFFFFFFFu, off0 = 0;  // fused: no range resumes mid-way
@@ -1991,7 +1502,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
         wave_lds_order();
         if (T > 0) {
             const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
-            // the final partial group (emit_partial): 2 sextets -> 1 byte, 3 -> 2
+            // the final partial group: 2 sextets -> 1 byte, 3 -> 2 (floor(6r/8),
+            // src/base64decoder.c:59-62,71-76)
             const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
             const uint32_t total = 3 * ng + tail;
             if (total > done) store_bits(bits, lo, lo + (total - done), ob + done - lo);
@@ -2059,7 +1571,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
             uint64_t agg = 0;
             for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
             uint64_t excl = 0;
-            if (t > 0 && !(price & 1)) {
+            if (t > 0) {
                 if (lane == 0) st_store(&w.fstatus[t], kStAgg | agg);
                 for (int64_t p = (int64_t) t - 1;;) {
                     const int64_t q = p - lane;
@@ -2089,7 +1601,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
         __syncthreads();
         uint64_t B = s_excl;
         for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
-        for (uint32_t j = 0; j < kFusePer && rw + j < nranges && !(price & 2); j++) {
+        for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             uint4 c[2];
             uint32_t nin[2], la;
             bool la_ok;
@@ -2296,7 +1808,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
 // and publishes the buffer's length.  Any other slot marks the buffer.
 // Both go through atomicMax on outlen[] (zeroed by the launcher), so a mark
 // always wins; the fix-up then decodes marked buffers exactly.
-template <int U, bool PLAIN, bool NTL>
+template <int U>
 __global__ __launch_bounds__(kThreads) void k_decode_slots(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
     uint8_t *__restrict__ out, uint64_t out_stride,
@@ -2320,7 +1832,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
             const uint8_t *src = in + (uint64_t) b * in_stride + (uint64_t) q * 16;
             const uint64_t avail = len - (uint64_t) q * 16;
             nin[u] = avail >= 16 ? 16u : (uint32_t) avail;
-            if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<NTL>(src);
+            if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<true>(src);
             else w[u] = load_chars(src, nin[u]);
         }
     }
@@ -2351,85 +1863,10 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
             } else if (nbytes) {
                 store_bytes12(dst, o0, o1, o2, nbytes);
             }
-            if (q == S - 1) {
-                if (PLAIN) outlen[b] = (16ull * q + k) * 6 / 8;
-                else atomicMax(&outlen[b], (unsigned long long) ((16ull * q + k) * 6 / 8));
-            }
+            if (q == S - 1)
+                atomicMax(&outlen[b], (unsigned long long) ((16ull * q + k) * 6 / 8));
         } else {
-            if (PLAIN) outlen[b] = kNeedsExact;
-            else atomicMax(&outlen[b], (unsigned long long) kNeedsExact);
-        }
-    }
-}
-
-// Uniform-stride batch decode for rows with room (out_stride >= 12*S):
-// every lane loads 16
-// characters and stores 12 bytes unconditionally, so no memory operation
-// is exec-masked.  The last slot of a row over-reads into the next row's
-// characters and over-writes past out_len inside its own row (those bytes
-// are unspecified, include/b64x.h); its length follows the prefix rule.
-// A lane that is not clean marks the row for the fix-up, which
-// rewrites it exactly.  The caller excludes the last row (its last slot
-// could read past the input) and runs it through k_decode_slots.
-template <int U, bool GUARD>
-__global__ __launch_bounds__(kThreads) void k_decode_rows(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
-    uint8_t *__restrict__ out, uint64_t out_stride,
-    unsigned long long *__restrict__ outlen, uint32_t S, uint64_t m64, uint64_t slot0,
-    uint64_t nslots, DecAlpha a)
-{
-    __shared__ uint8_t tab[256];
-    build_dec_table(tab, a);
-    __syncthreads();
-    const uint64_t base = slot0 + (uint64_t) blockIdx.x * U * kThreads + threadIdx.x;
-    uint4 w[U];
-    uint64_t bb[U];
-    uint32_t qq[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint64_t t = base + (uint64_t) u * kThreads;
-        const uint64_t b = __umul64hi(t, m64);
-        bb[u] = b;
-        qq[u] = (uint32_t) (t - b * S);
-        w[u] = make_uint4(0, 0, 0, 0);
-        if (!GUARD || t < nslots)
-            w[u] = ld16<true>(in + b * in_stride + 16ull * qq[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint64_t t = base + (uint64_t) u * kThreads;
-        const uint32_t q = qq[u];
-        const bool last = q == S - 1;
-        const uint32_t nin = last ? (uint32_t) (len - 16ull * q) : 16u;
-        uint32_t G[4], bad;
-        map_fast(tab, w[u], nin, G, bad);
-        uint32_t k = 16;
-        bool ok = bad == 0;
-        if (last && !ok) {
-            LaneChunk lc;
-            map_chunk_lds(tab, w[u], nin, lc);
-            const uint32_t m = lc.vmask;
-            ok = (m & (m + 1)) == 0;  // alphabet characters form a prefix
-            k = __popc(m);
-#pragma unroll
-            for (int g = 0; g < 4; g++) G[g] = lc.G[g];
-        }
-        uint32_t o0, o1, o2;
-        groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-        // one junk mark per row and wave (as in k_decode_rows2)
-        const bool live = !GUARD || t < nslots;
-        const uint64_t junk = __ballot(live && !ok);
-        const uint32_t ln = lane_id();
-        const uint32_t rs = q < ln ? ln - (uint32_t) q : 0u;
-        const bool marker =
-            (uint32_t) __ffsll((unsigned long long) (junk & (~0ull << rs))) - 1 == ln;
-        if (live) {
-            __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
-                                        (u32x3a4 *) (out + bb[u] * out_stride + 12ull * q));
-            if (!ok) {
-                if (marker) atomicMax(&outlen[bb[u]], (unsigned long long) kNeedsExact);
-            } else if (last)
-                atomicMax(&outlen[bb[u]], (unsigned long long) ((16ull * q + k) * 6 / 8));
+            atomicMax(&outlen[b], (unsigned long long) kNeedsExact);
         }
     }
 }
@@ -2483,9 +1920,8 @@ DEV bool row_last_slot(const uint8_t *tab, uint4 w, const uint32_t A[4], uint32_
 // blocks that touch the last row ("tail", block-uniform) read page-safely
 // and store only decoded bytes, so one launch covers the batch.  Lengths
 // and marks go through atomicMax on the zeroed outlen[] as in
-// k_decode_slots.  LAST = 1: the rows' last slots take row_last_slot's
-// cheap check inline for every lane (no branch), 0: in a branch.
-template <int U, int PRICE, int LAST>
+// k_decode_slots.
+template <int U>
 __global__ __launch_bounds__(kThreads) void k_decode_rows2(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
     uint8_t *__restrict__ out, uint64_t out_stride,
@@ -2502,7 +1938,6 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows2(
     uint8_t *ob = out + b0 * out_stride;
     unsigned long long *olb = outlen + b0;
     const uint32_t nlast = len - 16 * (S - 1);  // characters in a row's last slot
-    const uint32_t d = (nlast - 1) >> 2;        // dword of the last in-range one
     uint32_t bl[U], qq[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -2547,35 +1982,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows2(
         map_fast_acc(tab, w[u], G, A);
         uint32_t k = 16;
         bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
-        if (PRICE & 2) {
-            ok = true;
-        } else if (LAST) {
-            // the common last-slot shape for every lane, selected by `last`
-            bool pre = true;
-#pragma unroll
-            for (uint32_t g = 0; g < 3; g++)
-                if (g < d) pre = pre && A[g] < 64u;
-            const uint32_t wd = d == 0 ? w[u].x : d == 1 ? w[u].y : d == 2 ? w[u].z : w[u].w;
-            uint32_t v = 0, Gd = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                const uint32_t t = tab[(wd >> (8 * j)) & 0xFFu];
-                const bool okj = 4 * d + j < nlast && t < 64u;
-                v |= (okj ? 1u : 0u) << j;
-                Gd |= (okj ? t : 0u) << (18 - 6 * j);
-            }
-            const bool fast_last = pre && (v & (v + 1)) == 0;
-            if (last) {
-                ok = fast_last;
-                k = 4 * d + __popc(v);
-            }
-#pragma unroll
-            for (uint32_t g = 0; g < 4; g++)
-                if (g == d && last) G[g] = Gd;
-            if (last && !fast_last) ok = row_last_slot(tab, w[u], A, G, nlast, k);
-        } else if (last) {
-            ok = row_last_slot(tab, w[u], A, G, nlast, k);
-        }
+        if (last) ok = row_last_slot(tab, w[u], A, G, nlast, k);
         uint32_t o0, o1, o2;
         groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
         __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
@@ -2590,86 +1997,10 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows2(
         const uint32_t rs = q < ln ? ln - q : 0u;
         const uint64_t row_junk = junk & (~0ull << rs);
         const bool marker = !ok && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln;
-        if (PRICE & 1) {  // benchmark-only pricing of the atomics (racy)
-            if (!ok) *ol = kNeedsExact;
-            else if (last) *ol = (16ull * q + k) * 6 / 8;
-        } else if (!ok) {
+        if (!ok) {
             if (marker) atomicMax(ol, (unsigned long long) kNeedsExact);
         } else if (last) {
             atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
-        }
-    }
-}
-
-// Grouped twin of k_decode_slots (see k_encode_group): block g owns
-// buffers [g*bpb, (g+1)*bpb), lanes walk its bpb*S 16-character slots.
-template <int U, bool NTL>
-__global__ __launch_bounds__(kThreads) void k_decode_group(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint64_t len,
-    uint32_t nbuf, uint8_t *__restrict__ out, uint64_t out_stride,
-    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t bpb, uint32_t magic,
-    DecAlpha a)
-{
-    __shared__ uint8_t tab[256];
-    build_dec_table(tab, a);
-    __syncthreads();
-    const uint32_t b0 = blockIdx.x * bpb;
-    const uint32_t nb = min(bpb, nbuf - b0);
-    const uint32_t slots = nb * S;
-    const uint8_t *gin = in + (uint64_t) b0 * in_stride;
-    uint8_t *gout = out + (uint64_t) b0 * out_stride;
-    for (uint32_t s0 = 0; s0 < slots; s0 += U * kThreads) {
-        uint4 w[U];
-        uint32_t nin[U], bq[U][2];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t t = s0 + u * kThreads + threadIdx.x;
-            nin[u] = 0;
-            bq[u][0] = bq[u][1] = 0;
-            w[u] = make_uint4(0, 0, 0, 0);
-            if (t < slots) {
-                const uint32_t b = __umulhi(t, magic), q = t - b * S;
-                bq[u][0] = b;
-                bq[u][1] = q;
-                const uint8_t *src = gin + (uint64_t) b * in_stride + q * 16u;
-                const uint64_t avail = len - (uint64_t) q * 16;
-                nin[u] = avail >= 16 ? 16u : (uint32_t) avail;
-                if (nin[u] == 16 && (((uintptr_t) src) & 3) == 0) w[u] = ld16<NTL>(src);
-                else w[u] = load_chars(src, nin[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (!nin[u]) continue;
-            const uint32_t b = bq[u][0], q = bq[u][1];
-            uint8_t *dst = gout + (uint64_t) b * out_stride + q * 12u;
-            uint32_t G[4], bad;
-            map_fast(tab, w[u], nin[u], G, bad);
-            uint32_t nbytes = 12, k = 16;
-            bool ok = bad == 0;
-            if (!ok && q == S - 1) {
-                LaneChunk lc;
-                map_chunk(tab, w[u], nin[u], lc);
-                const uint32_t m = lc.vmask;
-                ok = (m & (m + 1)) == 0;  // alphabet characters form a prefix
-                k = __popc(m);
-                nbytes = 3 * (k >> 2) + ((6 * (k & 3)) >> 3);
-#pragma unroll
-                for (int g = 0; g < 4; g++) G[g] = lc.G[g];
-            }
-            if (ok) {
-                uint32_t o0, o1, o2;
-                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-                if (nbytes == 12 && (((uintptr_t) dst) & 3) == 0) {
-                    __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
-                } else if (nbytes) {
-                    store_bytes12(dst, o0, o1, o2, nbytes);
-                }
-                if (q == S - 1)
-                    atomicMax(&outlen[b0 + b], (unsigned long long) ((16ull * q + k) * 6 / 8));
-            } else {
-                atomicMax(&outlen[b0 + b], (unsigned long long) kNeedsExact);
-            }
         }
     }
 }
@@ -2680,7 +2011,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_group(
 // bit stream; whole dwords are flushed to the output and the partial last
 // dword moves to the window front.  A buffer of V alphabet characters
 // yields floor(6V/8) bytes -- the reference's final partial group rule
-// (emit_partial) falls out of the bit count.
+// falls out of the bit count.
 // First-step characters of a buffer (chunks 0 and 1 of lane `lane`).
 DEV void buf_first_chunks(const uint8_t *src, uint64_t len, uint4 c[2])
 {
@@ -2942,13 +2273,23 @@ struct RangePlan {
     uint32_t nranges;
 };
 
-// Ranges of kRangeChunks chunks (g_tune[2] overrides), at most kMaxRanges
-// of them: many short ranges, one wave each, launched as a non-persistent
-// grid -- the shape that streams fastest -- and enough parallelism for the
-// exact pass 2 on dirty input.
+#ifdef B64X_TEST_HOOKS
+// Test builds only (tests/csrc/libb64x_hooks.so): a decode range length in
+// chunks, so ranges longer than one pass-2 step can be tested at small
+// sizes.  The product library has no such knob.
+uint64_t g_test_range_chunks = 0;
+#endif
+
+// Ranges of kRangeChunks chunks, at most kMaxRanges of them: many short
+// ranges, one wave each, launched as a non-persistent grid -- the shape
+// that streams fastest -- and enough parallelism for the exact pass 2 on
+// dirty input.
 RangePlan plan_ranges(uint64_t n)
 {
-    uint64_t chunks = g_tune[2] > 0 ? (uint64_t) g_tune[2] : kRangeChunks;
+    uint64_t chunks = kRangeChunks;
+#ifdef B64X_TEST_HOOKS
+    if (g_test_range_chunks) chunks = g_test_range_chunks;
+#endif
     uint64_t R = chunks * kChunk;
     if ((n + R - 1) / R > kMaxRanges) {
         R = (n + kMaxRanges - 1) / kMaxRanges;
@@ -2970,69 +2311,10 @@ int occupancy_of(K kernel)
     return nb;
 }
 
-template <int U, bool P, bool LNT, bool NT>
-int launch_encode_flat(const DeviceInfo &d, const uint8_t *in, uint64_t n, uint8_t *out,
-                       EncAlpha a, hipStream_t s, bool persistent)
-{
-    static const int occ = occupancy_of(k_encode_flat<U, P, LNT, NT>);
-    const uint64_t nq = n / 12, tile = (uint64_t) kThreads * U;
-    const uint64_t cap = persistent ? (uint64_t) d.cus * occ : (uint64_t) 1 << 31;
-    uint32_t grid = cap_grid(nq / tile, cap);
-    hipLaunchKernelGGL((k_encode_flat<U, P, LNT, NT>), dim3(grid), dim3(kThreads), 0, s, in,
-                       n, out, a);
-    return launch_status();
-}
-
-// Variant 0 is the shipped configuration (fastest in the interleaved A/B of
-// scripts/bench_variants.py, profiles/r01_variants*.json); the others stay
-// selectable for re-tuning.
-int encode_flat(int variant, const DeviceInfo &d, const uint8_t *in, uint64_t n,
-                uint8_t *out, EncAlpha a, hipStream_t s)
-{
-    switch (variant) {
-    case 1: return launch_encode_flat<4, false, false, true>(d, in, n, out, a, s, false);
-    case 2: return launch_encode_flat<4, false, false, true>(d, in, n, out, a, s, true);
-    case 3: return launch_encode_flat<8, false, true, true>(d, in, n, out, a, s, false);
-    case 4: return launch_encode_flat<4, false, true, true>(d, in, n, out, a, s, false);
-    case 5: return launch_encode_flat<4, true, true, true>(d, in, n, out, a, s, true);
-    case 6: return launch_encode_flat<1, false, true, true>(d, in, n, out, a, s, false);
-    default: return launch_encode_flat<2, false, true, true>(d, in, n, out, a, s, false);
-    }
-}
-
-struct Pass1Launch {
-    int blocks_per_cu;
-    void (*launch)(dim3, hipStream_t, const uint8_t *, uint64_t, uint8_t *, uint64_t,
-                   uint32_t, DecAlpha, void *, uint32_t);
-};
-
-template <int U, bool P, bool NT>
-void pass1_launcher(dim3 g, hipStream_t s, const uint8_t *in, uint64_t n, uint8_t *out,
-                    uint64_t R, uint32_t nr, DecAlpha a, void *ws, uint32_t hold)
-{
-    hipLaunchKernelGGL((k_decode_pass1<U, P, NT>), g, dim3(kThreads), 0, s, in, n, out, R,
-                       nr, a, ws, hold);
-}
-
-template <int U, bool P, bool NT>
-Pass1Launch pass1_of()
-{
-    static const int occ = occupancy_of(k_decode_pass1<U, P, NT>);
-    return Pass1Launch{occ, pass1_launcher<U, P, NT>};
-}
-
-Pass1Launch pass1_variant(int variant)
-{
-    switch (variant) {
-    case 1: return pass1_of<4, false, false>();
-    case 2: return pass1_of<2, true, true>();
-    case 3: return pass1_of<8, false, true>();
-    case 4: return pass1_of<4, false, true>();
-    case 5: return pass1_of<4, true, true>();
-    case 6: return pass1_of<1, false, true>();
-    default: return pass1_of<2, false, true>();
-    }
-}
+// Pass 1's shipped form: two chunks per lane in flight, non-temporal loads
+// and stores (round 1's A/B of 1-8 chunks, pipelining and cached loads,
+// profiles/r01_v6_*).
+constexpr auto k_pass1 = k_decode_pass1<2, true>;
 
 }  // namespace
 
@@ -3066,10 +2348,13 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
     if (!d_in || !d_out) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-    const int variant = g_tune[0];
-    if (variant != 99 && ((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 3) == 0)
-        return encode_flat(variant, *d, (const uint8_t *) d_in, n, (uint8_t *) d_out,
-                           enc_alpha(abc), (hipStream_t) stream);
+    if (((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 3) == 0) {
+        const uint64_t tiles = n / 12 / ((uint64_t) kThreads * kFlatU);
+        hipLaunchKernelGGL(k_encode_flat, dim3(cap_grid(tiles, (uint64_t) 1 << 31)),
+                           dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in, n,
+                           (uint8_t *) d_out, enc_alpha(abc));
+        return launch_status();
+    }
     // Misaligned buffers: the generic slot kernel (bytewise where needed).
     const uint64_t slots = (n + 11) / 12;
     const uint64_t per_block = (uint64_t) kThreads * kEncUnroll;
@@ -3079,34 +2364,6 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
                        (const uint8_t *) d_in, (uint64_t) 0, n, 1u, (uint8_t *) d_out,
                        (uint64_t) 0, slots, slots, enc_alpha(abc));
     return launch_status();
-}
-
-// Buffers per block for the grouped batch kernels: enough slots per block
-// (~4 per lane) and, where a power of two up to 64 allows, input and output
-// spans that start on 128-B lines.  0 = the grouped kernels do not apply
-// (slots per block must stay below 2^16 for the multiply-high division).
-// g_tune[4] bits: 1 = grouped batch kernels, 2 = temporal (cached) loads.
-static bool batch_ntl() { return !(g_tune[4] & 2); }
-
-static uint32_t plan_group(uint64_t slots_per_buf, uint64_t in_stride, uint64_t out_stride)
-{
-    if (!(g_tune[4] & 1) || slots_per_buf == 0 || slots_per_buf >= (1u << 15)) return 0;
-    uint32_t bpb = 1;
-    while ((uint64_t) bpb * slots_per_buf < 4 * kThreads && 2 * bpb * slots_per_buf < 65536)
-        bpb *= 2;
-    uint32_t best = bpb;
-    for (uint32_t p = bpb; p <= 64 && (uint64_t) p * slots_per_buf < 65536; p *= 2) {
-        if ((p * in_stride) % 128 == 0 && (p * out_stride) % 128 == 0) {
-            best = p;
-            break;
-        }
-    }
-    return best;
-}
-
-static uint32_t magic_of(uint32_t d)  // ceil(2^32 / d), d >= 2
-{
-    return (uint32_t) ((0xFFFFFFFFull + d) / d);
 }
 
 int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
@@ -3130,75 +2387,26 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     // Tight layout, one launch (k_encode_tight2).
     const bool tight = in_stride == len && out_stride == E && len >= 16 && (ea.pad || r == 0) &&
                        (((uintptr_t) d_in) & 3) == 0 && (((uintptr_t) d_out) & 15) == 0;
-    if (g_tune[4] == 0 && g_tune[6] == 0 && tight && E < (1u << 20)) {
-        const uint32_t Uw = g_tune[7] == 4 ? 4 : 2;
+    if (tight && E < (1u << 20)) {
         const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + E) / E);
         const uint64_t e = (uint64_t) magic * E - (1ull << 32);
-        if ((E + 16ull * Uw * kThreads) * e < (1ull << 32)) {
+        if ((E + 16ull * U * kThreads) * e < (1ull << 32)) {
             const uint64_t total_out = (uint64_t) nbuf * E;
             const uint64_t nslots = (total_out + 15) / 16;
             const uint64_t tail_slot = (nbuf - 1) * E / 16 ? (nbuf - 1) * E / 16 - 1 : 0;
             const uint64_t m64 = ~0ull / E + 1;
-            const uint64_t per = (uint64_t) Uw * kThreads;
+            const uint64_t per = (uint64_t) U * kThreads;
             const dim3 g((uint32_t) ((nslots + per - 1) / per));
-            if (Uw == 4)
-                hipLaunchKernelGGL(k_encode_tight2<4>, g, dim3(kThreads), 0, (hipStream_t) stream,
-                                   (const uint8_t *) d_in, len, (uint32_t) E, r, magic, m64,
-                                   (uint8_t *) d_out, nslots, (uint64_t) nbuf * len, total_out,
-                                   tail_slot, ea);
-            else
-                hipLaunchKernelGGL(k_encode_tight2<2>, g, dim3(kThreads), 0, (hipStream_t) stream,
-                                   (const uint8_t *) d_in, len, (uint32_t) E, r, magic, m64,
-                                   (uint8_t *) d_out, nslots, (uint64_t) nbuf * len, total_out,
-                                   tail_slot, ea);
+            hipLaunchKernelGGL(k_encode_tight2<U>, g, dim3(kThreads), 0, (hipStream_t) stream,
+                               (const uint8_t *) d_in, len, (uint32_t) E, r, magic, m64,
+                               (uint8_t *) d_out, nslots, (uint64_t) nbuf * len, total_out,
+                               tail_slot, ea);
             return launch_status();
         }
     }
-    // Tight layout: one contiguous character stream (k_encode_tight).
-    if (g_tune[4] == 0 && in_stride == len && out_stride == E && nbuf >= 3 && len >= 16 &&
-        (ea.pad || r == 0) && E < (1ull << 32) && (((uintptr_t) d_in) & 3) == 0 &&
-        (((uintptr_t) d_out) & 15) == 0) {
-        const uint64_t m64 = ~0ull / E + 1;  // ceil(2^64 / E)
-        const uint64_t nslots = (nbuf - 1) * E / 16;  // lanes wholly before the last buffer
-        const uint64_t tile = (uint64_t) U * kThreads;
-        const uint64_t full = nslots / tile;
-        hipStream_t st = (hipStream_t) stream;
-        int err;
-        if (full) {
-            hipLaunchKernelGGL((k_encode_tight<U, false>), dim3((uint32_t) full), dim3(kThreads),
-                               0, st, (const uint8_t *) d_in, len, (uint32_t) E, r, m64,
-                               (uint8_t *) d_out, (uint64_t) 0, nslots, ea);
-            if ((err = launch_status())) return err;
-        }
-        if (nslots > full * tile) {
-            hipLaunchKernelGGL((k_encode_tight<U, true>), dim3(1), dim3(kThreads), 0, st,
-                               (const uint8_t *) d_in, len, (uint32_t) E, r, m64,
-                               (uint8_t *) d_out, full * tile, nslots, ea);
-            if ((err = launch_status())) return err;
-        }
-        // The last two buffers whole (the second-to-last may end inside the
-        // last slot above; rewriting it is idempotent).
-        const uint8_t *tin = (const uint8_t *) d_in + (nbuf - 2) * len;
-        uint8_t *tout = (uint8_t *) d_out + (nbuf - 2) * E;
-        auto k = k_encode_strided<U, true>;
-        hipLaunchKernelGGL(k, dim3((uint32_t) ((2 * qpb + U * kThreads - 1) / (U * kThreads))),
-                           dim3(kThreads), 0, st, tin, in_stride, len, 2u, tout, out_stride,
-                           (uint32_t) qpb, (uint32_t) (2 * qpb), ea);
-        return launch_status();
-    }
-    const uint32_t bpb = qpb >= 2 ? plan_group(qpb, in_stride, out_stride) : 0;
-    const bool ntl = batch_ntl();
-    if (bpb) {
-        auto k = ntl ? k_encode_group<U, true> : k_encode_group<U, false>;
-        hipLaunchKernelGGL(k, dim3((uint32_t) ((nbuf + bpb - 1) / bpb)),
-                           dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
-                           in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
-                           bpb, magic_of((uint32_t) qpb), enc_alpha(abc));
-        return launch_status();
-    }
+    // Any other layout: one lane per (buffer, quad).
     const uint64_t per_block = (uint64_t) kThreads * U;
-    auto k = ntl ? k_encode_strided<U, true> : k_encode_strided<U, false>;
-    hipLaunchKernelGGL(k, dim3((uint32_t) ((slots + per_block - 1) / per_block)),
+    hipLaunchKernelGGL((k_encode_strided<U, true>), dim3((uint32_t) ((slots + per_block - 1) / per_block)),
                        dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
                        in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
                        (uint32_t) slots, enc_alpha(abc));
@@ -3271,7 +2479,6 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     int err = 0;
     void *ws = d_workspace ? d_workspace : library_workspace(stream, &err);
     if (!ws) return err;
-    const Pass1Launch p1 = pass1_variant(g_tune[1]);
     const RangePlan p = plan_ranges(nchars);
     const uint32_t blocks = (p.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const DecAlpha a = dec_alpha(abc);
@@ -3281,37 +2488,23 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         const uint32_t tiles = (p.nranges + kFuseTile - 1) / kFuseTile;
         hipLaunchKernelGGL(k_decode_fused, dim3(tiles), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                           a, ws, hold, d_res, h_res, (uint32_t) g_tune[9]);
+                           a, ws, hold, d_res, h_res);
         return launch_status();
     }
-    p1.launch(dim3(blocks), s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R,
-              p.nranges, a, ws, hold);
+    hipLaunchKernelGGL(k_pass1, dim3(blocks), dim3(kThreads), 0, s, (const uint8_t *) d_in,
+                       nchars, (uint8_t *) d_out, p.R, p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
-    {
-        auto ks = g_tune[8] == 2 ? k_decode_scan2<1, 0>
-                : g_tune[8] == 3 ? k_decode_scan2<0, 0> : k_decode_scan2<0, 1>;
-        hipLaunchKernelGGL(ks,
-                           dim3((p.nranges + kScanTile - 1) / kScanTile),
-                           dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges,
-                           a, ws, d_res, h_res, hold);
-    }
+    hipLaunchKernelGGL(k_decode_scan2, dim3((p.nranges + kScanTile - 1) / kScanTile),
+                       dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges, a,
+                       ws, d_res, h_res, hold);
     if ((err = launch_status())) return err;
     // grid-stride over the ranges with exactly the resident blocks (a second
-    // partial round of blocks would trail the rest); pass 2c (ranges of at
-    // most kP2Range characters) only for A/B
-    if (g_tune[5] == 4 && p.R <= kP2Range) {
-        static const int occ2c = occupancy_of(k_decode_pass2c);
-        const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2c);
-        hipLaunchKernelGGL(k_decode_pass2c, dim3(b2), dim3(kThreads), 0, s,
-                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                           a, ws, hold);
-        return launch_status();
-    }
+    // partial round of blocks would trail the rest)
     static const int occ2d = occupancy_of(k_decode_pass2d);
     const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2d);
     hipLaunchKernelGGL(k_decode_pass2d, dim3(b2), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                       a, ws, hold, (b64x_dec_result *) nullptr, (b64x_dec_result *) nullptr, 0u);
+                       a, ws, hold, (b64x_dec_result *) nullptr, (b64x_dec_result *) nullptr);
     return launch_status();
 }
 
@@ -3368,88 +2561,37 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     const DecAlpha a = dec_alpha(abc);
     int err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s));
     if (err) return err;
-    const uint32_t bpb = S >= 2 && g_tune[3] != 1 ? plan_group(S, in_stride, out_stride) : 0;
-    const bool ntl = batch_ntl();
     const bool rows = nbuf >= 2 && S >= 2 && out_stride >= 12 * S && (in_stride & 3) == 0 &&
                       (out_stride & 3) == 0 && (((uintptr_t) d_in) & 3) == 0 &&
                       (((uintptr_t) d_out) & 3) == 0;
     bool done = false;
-    if (g_tune[4] == 0 && g_tune[6] == 0 && rows && S < (1u << 20)) {
-        const uint32_t Uw = g_tune[7] == 2 ? 2 : 4;
+    if (rows && S < (1u << 20)) {
+        // rows with room, one launch (k_decode_rows2)
+        constexpr uint32_t U = 4;
         const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
         const uint64_t e = (uint64_t) magic * S - (1ull << 32);
-        const uint64_t relmax = S + (uint64_t) Uw * kThreads;
+        const uint64_t relmax = S + (uint64_t) U * kThreads;
         if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40)) {
             const uint64_t m64 = ~0ull / S + 1;
-            const uint64_t per = (uint64_t) Uw * kThreads;
+            const uint64_t per = (uint64_t) U * kThreads;
             const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
             const dim3 g((uint32_t) ((slots + per - 1) / per));
-            auto k = Uw == 4 ? k_decode_rows2<4, 0, 0> : k_decode_rows2<2, 0, 0>;
-            if (g_tune[3] == 11) k = Uw == 4 ? k_decode_rows2<4, 0, 1> : k_decode_rows2<2, 0, 1>;
-            if (Uw == 4 && g_tune[3] == 8) k = k_decode_rows2<4, 1, 0>;  // pricing only (racy)
-            if (Uw == 4 && g_tune[3] == 9) k = k_decode_rows2<4, 2, 0>;  // pricing (wrong lengths)
-            hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s, (const uint8_t *) d_in, in_stride,
-                               (uint32_t) len, (uint8_t *) d_out, out_stride,
+            hipLaunchKernelGGL(k_decode_rows2<U>, g, dim3(kThreads), 0, s, (const uint8_t *) d_in,
+                               in_stride, (uint32_t) len, (uint8_t *) d_out, out_stride,
                                (unsigned long long *) d_outlen, (uint32_t) S, magic, m64, slots,
                                tail_slot, a);
             if ((err = launch_status())) return err;
             done = true;
         }
     }
-    // Rows with room: the uniform kernel over all rows but the last.
-    if (done) {
-    } else if (g_tune[4] == 0 && rows) {
-        constexpr int U = 2;
-        const uint64_t m64 = ~0ull / S + 1;  // ceil(2^64 / S)
-        const uint64_t nrows = (uint64_t) S * (nbuf - 1);
-        const uint64_t tile = (uint64_t) U * kThreads, full = nrows / tile;
-        if (full) {
-            hipLaunchKernelGGL((k_decode_rows<U, false>), dim3((uint32_t) full), dim3(kThreads), 0,
-                               s, (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, m64,
-                               (uint64_t) 0, nrows, a);
-            if ((err = launch_status())) return err;
-        }
-        if (nrows > full * tile) {
-            hipLaunchKernelGGL((k_decode_rows<U, true>), dim3(1), dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, m64,
-                               full * tile, nrows, a);
-            if ((err = launch_status())) return err;
-        }
-        const uint64_t lb = nbuf - 1;
-        hipLaunchKernelGGL((k_decode_slots<U, false, true>), dim3((S + U * kThreads - 1) / (U * kThreads)),
-                           dim3(kThreads), 0, s, (const uint8_t *) d_in + lb * in_stride,
-                           in_stride, len, (uint8_t *) d_out + lb * out_stride, out_stride,
-                           (unsigned long long *) d_outlen + lb, (uint32_t) S, (uint32_t) S, a);
-        if ((err = launch_status())) return err;
-    } else if (slots && bpb) {
-        constexpr int U = 2;
-        auto k = ntl ? k_decode_group<U, true> : k_decode_group<U, false>;
-        hipLaunchKernelGGL(k, dim3((nbuf + bpb - 1) / bpb), dim3(kThreads), 0, s,
-                           (const uint8_t *) d_in, in_stride, len, nbuf, (uint8_t *) d_out,
-                           out_stride, (unsigned long long *) d_outlen, (uint32_t) S, bpb,
-                           magic_of((uint32_t) S), a);
-        if ((err = launch_status())) return err;
-    } else if (slots) {
+    if (!done && slots) {
+        // any other layout: one lane per (buffer, 16-character slot)
         constexpr int U = 2;
         const uint64_t per_block = (uint64_t) kThreads * U;
         const dim3 g((uint32_t) ((slots + per_block - 1) / per_block));
-        if (g_tune[3] == 1)  // benchmark-only: racy plain stores (prices the atomics)
-            hipLaunchKernelGGL((k_decode_slots<U, true, true>), g, dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
-                               (uint32_t) slots, a);
-        else if (ntl)
-            hipLaunchKernelGGL((k_decode_slots<U, false, true>), g, dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
-                               (uint32_t) slots, a);
-        else
-            hipLaunchKernelGGL((k_decode_slots<U, false, false>), g, dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, in_stride, len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S,
-                               (uint32_t) slots, a);
+        hipLaunchKernelGGL(k_decode_slots<U>, g, dim3(kThreads), 0, s, (const uint8_t *) d_in,
+                           in_stride, len, (uint8_t *) d_out, out_stride,
+                           (unsigned long long *) d_outlen, (uint32_t) S, (uint32_t) slots, a);
         if ((err = launch_status())) return err;
     }
     uint32_t fgrid = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock),
@@ -4090,39 +3232,16 @@ int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t
     return jobs_ok(h_in_off, h_flags, h_res, njobs) ? 0 : -EIO;
 }
 
-// Tuning and calibration hooks for scripts/bench_variants.py (exported,
-// deliberately not declared in include/b64x.h).
-int b64x__tune(int idx, int value)
+#ifdef B64X_TEST_HOOKS
+// Test builds only: decode ranges of `chunks` chunks (0 = the default);
+// returns the previous setting.
+uint64_t b64x__test_range_chunks(uint64_t chunks)
 {
-    if (idx < 0 || idx >= 10) return -EINVAL;
-    int old = g_tune[idx];
-    g_tune[idx] = value;
+    const uint64_t old = g_test_range_chunks;
+    g_test_range_chunks = chunks;
     return old;
 }
-
-// kind: 0 = 16 B in / 16 B out, 1 = 12 in / 16 out (encode shape),
-// 2 = 16 in / 12 out (decode shape); +8 = non-temporal stores.  `slots`
-// lanes' worth of data are streamed.
-int b64x__probe_copy(const void *d_in, void *d_out, uint64_t slots, int kind, void *stream)
-{
-    const DeviceInfo *d = device_info();
-    if (!d) return -ENODEV;
-    if ((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 15) return -EINVAL;
-    hipStream_t s = (hipStream_t) stream;
-    uint32_t grid = cap_grid(slots / (kThreads * 4), (uint64_t) d->cus * 8);
-    const uint8_t *i = (const uint8_t *) d_in;
-    uint8_t *o = (uint8_t *) d_out;
-    switch (kind) {
-    case 0: hipLaunchKernelGGL((k_copy_probe<16, 16, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    case 1: hipLaunchKernelGGL((k_copy_probe<12, 16, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    case 2: hipLaunchKernelGGL((k_copy_probe<16, 12, false>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    case 8: hipLaunchKernelGGL((k_copy_probe<16, 16, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    case 9: hipLaunchKernelGGL((k_copy_probe<12, 16, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    case 10: hipLaunchKernelGGL((k_copy_probe<16, 12, true>), dim3(grid), dim3(kThreads), 0, s, i, o, slots); break;
-    default: return -EINVAL;
-    }
-    return launch_status();
-}
+#endif
 
 const char *b64x_build_info(void)
 {

@@ -22,10 +22,19 @@ Also reported on the same JSON line:
                 config 4's shape on up to 16 threads (the box's CPU share);
   batch_cfg4    BASELINE config 4: 1,048,576 x 1 KiB buffers split across
                 the ranks by index range, strided encode + decode, plus the
-                one exchange step (allgather of per-rank output totals).
+                one exchange step (allgather of per-rank output totals);
+                whole-job and per-rank GiB/s and roofline fractions;
+  host_inclusive  the same 1 GiB round trip starting and ending in pinned
+                host memory (rank 0): the kernels read and write the pinned
+                buffers in place over PCIe (the sessions' zero-copy path),
+                and the staged form (H2D, kernel, D2H on k streams); bit-
+                checked; never `value`.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-        (N > 1: launched by torch.distributed.run, one rank per GPU)
+        N > 1 without WORLD_SIZE in the environment: bench.py starts
+        `python -m torch.distributed.run --nproc-per-node N` itself (before
+        touching the GPU) and relays its line; every rank checks that the
+        process group has exactly N ranks, and the line reports RCCL's count.
 """
 from __future__ import annotations
 
@@ -44,7 +53,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s base64 encode+decode, device-resident, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ROUND = "r01"
+ROUND = "r01"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
 
 
 def parse():
@@ -64,6 +73,12 @@ def parse():
                     help="1 KiB buffers in the all-core CPU baseline sample")
     ap.add_argument("--no-batch", action="store_true")
     ap.add_argument("--batch-steps", type=int, default=20)
+    ap.add_argument("--no-host", action="store_true", help="skip the host_inclusive leg")
+    ap.add_argument("--host-block", type=int, default=24 << 20,
+                    help="bytes per block of the host_inclusive leg (a multiple of 3)")
+    ap.add_argument("--host-streams", type=int, default=4)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and check the process group only, no GPU work (tests)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; "
                          "gloo only to rehearse the multi-rank logic on one GPU)")
@@ -74,12 +89,23 @@ def coll_device():
     return "cpu" if dist.is_initialized() and dist.get_backend() == "gloo" else "cuda"
 
 
+
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_floats(vals, world: int):
+    """Every rank's `vals` (a short list of floats), in rank order."""
+    if world == 1:
+        return [list(vals)]
+    t = torch.tensor(vals, dtype=torch.float64, device=coll_device())
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
 
 
 def sync_all(world: int):
@@ -214,8 +240,12 @@ def bench_batch(args, world, rank, b64):
     _, tot_list = shard.exchange_totals(int(outlen.sum()), device=coll_device())
     totals.copy_(torch.tensor(tot_list, dtype=torch.int64))
     sync_all(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
+    mine = time.perf_counter() - t0
+    wall = max_over_ranks(mine, world)
     assert int(totals.sum()) == total_buf * L
+    kern_ms = ev[0].elapsed_time(ev[2]) / K
+    rank_frac = (2 * (nbuf * (L + Es))) / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
+    per_rank = gather_floats([nbuf * L * K / mine / 2**30, rank_frac], world)
     return {
         "workload": "cfg4: 1,048,576 x 1 KiB buffers split across ranks, strided "
                     "encode then decode, + allgather of per-rank output totals",
@@ -225,9 +255,112 @@ def bench_batch(args, world, rank, b64):
         "ms_per_step": wall / K * 1e3,
         "encode_kernel_ms": ev[0].elapsed_time(ev[1]) / K,
         "decode_kernel_ms": ev[1].elapsed_time(ev[2]) / K,
-        "roofline_frac": (2 * (nbuf * (L + Es))) /
-                         ((ev[0].elapsed_time(ev[2]) / K) * 1e-3) / (HBM_PEAK_GBS * 1e9),
+        "roofline_frac": rank_frac,
+        "per_rank_GiB_s": [p[0] for p in per_rank],
+        "per_rank_roofline_frac": [p[1] for p in per_rank],
     }
+
+
+def bench_host_inclusive(args, b64):
+    """BASELINE config 2 starting and ending in pinned host memory: 1 GiB of
+    bytes in pinned memory -> characters in pinned memory -> bytes back,
+    bit-checked.  Two forms, each over blocks of --host-block bytes on
+    --host-streams streams: "in_place" (the kernels read and write the
+    pinned buffers over PCIe; what b64x_session_* does for encodes and clean
+    head-free decodes) and "staged" (H2D, kernel, D2H through device
+    buffers).  Rates are payload GiB/s (N bytes per direction)."""
+    import ctypes
+
+    import numpy as np
+
+    from async_amd import _lib
+
+    L = _lib.load()
+    N, blk = args.size, args.host_block - args.host_block % 3
+    E = b64.encoded_len(N)
+    eblk = blk // 3 * 4
+    slack = 64  # decode's last vector loads may reach past its input
+
+    def pinned(nbytes):
+        p = L.b64x_host_alloc(nbytes + slack)
+        if not p:
+            raise SystemExit("b64x_host_alloc failed")
+        arr = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)),
+                                    (nbytes + slack,))
+        return p, arr
+
+    p_src, src = pinned(N)
+    p_chr, chars = pinned(E)
+    p_dst, dst = pinned(N)
+    k = args.host_streams
+    streams = [torch.cuda.Stream() for _ in range(k)]
+    dev_in = [torch.empty(eblk + slack, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    dev_out = [torch.empty(eblk + slack, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    res = [torch.zeros(24, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    ws = [torch.zeros(b64.workspace_size(eblk), dtype=torch.uint8, device="cuda")
+          for _ in range(k)]
+    a = _lib.alphabet()
+    x = torch.empty(N, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    src[:N] = x.cpu().numpy()
+    del x
+    h_src = torch.from_numpy(src[:N])
+    h_chr = torch.from_numpy(chars[:E])
+    h_dst = torch.from_numpy(dst[:N])
+
+    def run(direction, form):
+        nblocks = (N + blk - 1) // blk
+        for i in range(nblocks):
+            j = i % k
+            s = streams[j]
+            b0 = i * blk
+            n = min(blk, N - b0)
+            e0 = b0 // 3 * 4
+            m = b64.encoded_len(n)  # last block padded; others exact
+            st = s.cuda_stream
+            if direction == "encode":
+                if form == "in_place":
+                    _lib.check("b64x_encode_dev", L.b64x_encode_dev(
+                        p_src + b0, n, p_chr + e0, ctypes.byref(a), st))
+                else:
+                    with torch.cuda.stream(s):
+                        dev_in[j][:n].copy_(h_src[b0:b0 + n], non_blocking=True)
+                        b64.encode(dev_in[j][:n], out=dev_out[j], stream=s)
+                        h_chr[e0:e0 + m].copy_(dev_out[j][:m], non_blocking=True)
+            else:
+                if form == "in_place":
+                    _lib.check("b64x_decode_dev", L.b64x_decode_dev(
+                        p_chr + e0, m, p_dst + b0, res[j].data_ptr(), ctypes.byref(a), 0,
+                        ws[j].data_ptr(), st))
+                else:
+                    with torch.cuda.stream(s):
+                        dev_in[j][:m].copy_(h_chr[e0:e0 + m], non_blocking=True)
+                        b64.decode(dev_in[j][:m], out=dev_out[j], workspace=ws[j],
+                                   result=res[j], stream=s)
+                        h_dst[b0:b0 + n].copy_(dev_out[j][:n], non_blocking=True)
+        torch.cuda.synchronize()
+
+    out = {"workload": f"cfg2 from/to pinned host memory: {N >> 20} MiB, blocks of "
+                       f"{blk} B on {k} streams, payload GiB/s per direction",
+           "unit": "GiB/s"}
+    for form in ("in_place", "staged"):
+        dst[:N] = 0
+        chars[:E] = 0
+        run("encode", form)  # warm-up (code objects, page mappings)
+        run("decode", form)
+        t = {}
+        for direction in ("encode", "decode"):
+            t0 = time.perf_counter()
+            run(direction, form)
+            t[direction] = time.perf_counter() - t0
+        ok = bool(np.array_equal(dst[:N], src[:N]))
+        if not ok:
+            raise SystemExit(f"host_inclusive {form}: round trip mismatch")
+        out[form] = {"encode": N / t["encode"] / 2**30, "decode": N / t["decode"] / 2**30,
+                     "round_trip": N / (t["encode"] + t["decode"]) / 2**30, "exact": ok}
+    for p in (p_src, p_chr, p_dst):
+        L.b64x_host_free(p)
+    return out
 
 
 def cpu_model() -> str:
@@ -306,19 +439,60 @@ def cpu_baseline(args, b64):
     }
 
 
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start one rank per GPU under
+    torch.distributed.run as a child process (nothing here has touched the
+    GPU yet) and relay its output; returns its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:  # a free rendezvous port on the loopback
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if world != args.gpus:
+        # never report a line for a different GPU count than asked for
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > ndev:
+        print(f"bench.py: {world} ranks but {ndev} visible GPUs (RCCL needs one GPU per "
+              "rank)", file=sys.stderr)
+        sys.exit(2)
+    if ndev:
+        torch.cuda.set_device(local % ndev)
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.backend)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, "
+                  f"--gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+    if args.dry_run:
+        # the launch and the process group only (CPU tests, gloo): no GPU work
+        ranks = gather_floats([float(rank)], world)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world,
+                              "process_group": {"backend": dist.get_backend() if world > 1
+                                                else None, "world_size": world},
+                              "ranks_seen": [int(r[0]) for r in ranks]}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     from async_amd import b64
 
     b64.device_check()
@@ -327,6 +501,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, b64)
+    host = None
+    if rank == 0 and not args.no_host:
+        host = bench_host_inclusive(args, b64)
 
     if rank == 0:
         N, E, K = r["N"], r["E"], r["K"]
@@ -379,6 +556,9 @@ def main():
             },
             "cpu_baseline": cpu,
             "batch_cfg4": batch,
+            "host_inclusive": host,
+            "process_group": {"backend": dist.get_backend() if world > 1 else None,
+                              "world_size": dist.get_world_size() if world > 1 else 1},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -39,18 +39,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, nargs="*", default=[64, 1024])
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--tune", default="", help="idx:val,... (b64x__tune knobs, A/B only)")
     ap.add_argument("--expect-junk", action="store_true",
                     help="B64X_DEC_EXPECT_JUNK: the single-pass decode")
     args = ap.parse_args()
-    if args.tune:
-        import ctypes
-        from async_amd import _lib
-        lib = _lib.load()
-        lib.b64x__tune.argtypes = [ctypes.c_int, ctypes.c_int]
-        for kv in args.tune.split(","):
-            i, v = (int(z) for z in kv.split(":"))
-            lib.b64x__tune(i, v)
     for mib in args.mib:
         n = mib << 20
         x = torch.empty(n, dtype=torch.uint8, device="cuda")

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel medians of every counter in a directory of rocprofv3 --pmc
-passes (d1/, d2/, ... as written by scripts/pmc_dirty.sh), one line per
+passes (p1/, p2/, ... as written by scripts/pmc_passes.sh), one line per
 kernel and counter.  Usage: summarize_pmc_sets.py DIR [kernel-substring]"""
 import collections
 import csv
@@ -12,7 +12,7 @@ import sys
 src = sys.argv[1]
 filt = sys.argv[2] if len(sys.argv) > 2 else ""
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in sorted(glob.glob(os.path.join(src, "d*", "**", "*counter_collection.csv"),
+for path in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"),
                              recursive=True)):
     with open(path) as f:
         for r in csv.DictReader(f):

@@ -48,6 +48,23 @@ def test_every_declared_symbol_is_exported():
         assert name in exported, name
 
 
+def test_product_has_no_variant_knobs():
+    """The product libraries carry no kernel-variant or test hooks and read
+    no tuning variable that could select another kernel form: the only
+    knobs a user has are the documented ones, none of which
+    changes the bytes produced."""
+    core = os.path.join(ROOT, "async_amd", "libasync_b64_core.so")
+    for path in (_lib.LIB_PATH, core):
+        out = subprocess.run(["nm", "-D", "--defined-only", path],
+                             capture_output=True, text=True, check=True).stdout
+        assert "b64x__" not in out, path
+        blob = open(path, "rb").read()
+        assert b"ASYNC_B64_TUNE" not in blob, path
+    hooks = subprocess.run(["nm", "-D", "--defined-only", util.HOOKS],
+                           capture_output=True, text=True, check=True).stdout
+    assert "b64x__test_range_chunks" in hooks
+
+
 def test_binding_loads_and_sizes():
     lib = _lib.load()
     assert lib.b64x_encoded_len(0, True) == 0

@@ -547,13 +547,27 @@ def test_beyond_32bit_ragged_batch():
 @pytest.mark.parametrize("chunks", [3, 8])
 def test_decode_long_ranges_vs_oracle(chunks):
     """Ranges longer than one 2,048-character step (what inputs past 2 GiB
-    get, since the range count is capped), forced at small sizes with the
-    range-size knob: the exact pass flushes its window between steps."""
+    get, since the range count is capped), forced at small sizes through the
+    test build's range-size hook (tests/csrc/libb64x_hooks.so): the exact
+    pass flushes its window between steps."""
     import ctypes
     from async_amd import _lib
-    lib = _lib.load()
-    lib.b64x__tune.argtypes = [ctypes.c_int, ctypes.c_int]
-    old = lib.b64x__tune(2, chunks)
+    L = util.hooks()
+    old = L.b64x__test_range_chunks(chunks)
+
+    def hdec(chars: bytes, hold: bool):
+        x = dev(chars)
+        out = torch.empty(max(b64.decoded_cap(len(chars)), 1), dtype=torch.uint8, device=DEV)
+        res = torch.zeros(24, dtype=torch.uint8, device=DEV)
+        ws = torch.zeros(b64.workspace_size(len(chars)), dtype=torch.uint8, device=DEV)
+        a = _lib.alphabet()
+        _lib.check("b64x_decode_dev", L.b64x_decode_dev(
+            x.data_ptr(), len(chars), out.data_ptr(), res.data_ptr(), ctypes.byref(a),
+            b64.HOLD_TAIL if hold else 0, ws.data_ptr(),
+            torch.cuda.current_stream().cuda_stream))
+        info = b64.Decoded(out, res).info()
+        return out[:info.out_len].cpu().numpy().tobytes(), info
+
     try:
         rng = np.random.default_rng(chunks)
         for n in (1, 5000, 3 * 1024 * chunks + 7, 400_000):
@@ -563,7 +577,7 @@ def test_decode_long_ranges_vs_oracle(chunks):
                           _junk(rng, chars, 0.3),
                           _junk(rng, chars, 0, run_every=5000, run_len=3000)):
                 for hold in (False, True):
-                    got, info = gdec(dirty, hold=hold)
+                    got, info = hdec(dirty, hold)
                     want = orc.decode(dirty)
                     if hold:  # whole groups only; the rest is held back
                         assert info.out_len == 3 * (info.valid // 4)
@@ -571,7 +585,7 @@ def test_decode_long_ranges_vs_oracle(chunks):
                     else:
                         assert got == want, (n, len(dirty))
     finally:
-        lib.b64x__tune(2, old)
+        L.b64x__test_range_chunks(old)
 
 
 def gdec_j(chars, pos62=-1, pos63=-1, hold=False):

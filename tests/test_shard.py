@@ -89,3 +89,39 @@ def test_gloo_exchange(world):
 def test_single_process_exchange():
     assert shard.exchange_totals(123) == (0, [123])
     assert torch.tensor([1]).sum() == 1
+
+
+def _bench(*args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args],
+                       capture_output=True, text=True, env=env, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts
+    torch.distributed.run itself (before any GPU call), every rank joins one
+    process group of exactly --gpus ranks, and rank 0 prints one line that
+    reports the group's size (the launch and group logic only: --dry-run,
+    gloo on CPU)."""
+    rc, lines, err = _bench("--gpus", "2", "--backend", "gloo", "--dry-run")
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2
+    assert lines[0]["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert lines[0]["ranks_seen"] == [0, 1]
+
+
+def test_bench_refuses_a_mismatched_world():
+    """A rank whose world differs from --gpus exits non-zero and prints no
+    line: `--gpus 8` can never report an n_gpus=1 measurement."""
+    rc, lines, _ = _bench("--gpus", "2", "--dry-run", env_extra={"WORLD_SIZE": "1"})
+    assert rc != 0 and lines == []

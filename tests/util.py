@@ -68,6 +68,27 @@ def fake_harness() -> ctypes.CDLL:
     return _fake
 
 
+HOOKS = os.path.join(ROOT, "tests", "csrc", "libb64x_hooks.so")
+_hooks = None
+
+
+def hooks() -> ctypes.CDLL:
+    """tests/csrc/libb64x_hooks.so: the kernels built with B64X_TEST_HOOKS
+    (b64x__test_range_chunks); the product library has no such knob."""
+    global _hooks
+    if _hooks is None:
+        import torch  # noqa: F401  (one HIP runtime: see async_amd/_lib.py)
+        from async_amd import _lib
+        L = ctypes.CDLL(HOOKS)
+        for name, (res, args) in _lib.SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        L.b64x__test_range_chunks.argtypes = [ctypes.c_uint64]
+        L.b64x__test_range_chunks.restype = ctypes.c_uint64
+        _hooks = L
+    return _hooks
+
+
 def _lib_or_default(lib):
     return lib if lib is not None else harness()
 
