@@ -399,6 +399,11 @@ static void complete(b64_hub *h, b64_batch *b, bool collect)
 
 static void hub_wake(b64_hub *h)
 {
+    /* Drain to EAGAIN first: async_register() is edge-triggered (the
+     * reference's contract, include/async.h), so the next completion's
+     * write is a fresh edge; batch_done() publishes `done` before it
+     * writes, so every batch whose write this read consumed is seen done
+     * below. */
     uint64_t v;
     while (read(h->efd, &v, sizeof v) == (ssize_t) sizeof v)
         ;

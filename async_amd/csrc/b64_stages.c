@@ -74,6 +74,7 @@
 #include "async.h"
 #include "b64_hub.h"
 #include "b64_lend.h"
+#include "b64_trace.h"
 #include "b64x.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
@@ -100,6 +101,7 @@ typedef enum { DIR_ENCODE, DIR_DECODE } direction;
 
 struct stage {
     async_t *async;
+    uint64_t uid;       /* the reference's trace uid (b64_trace.h) */
     bytestream_1 up;
     action_1 cb;        /* the consumer's callback, or NULL_ACTION_1 */
     direction dir;
@@ -178,6 +180,7 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
 {
     memset(st, 0, sizeof *st);
     st->async = async;
+    st->uid = b64_trace_unique_id();
     st->up = up;
     st->cb = NULL_ACTION_1;
     st->dir = dir;
@@ -250,6 +253,8 @@ static void stage_stop(stage *st)
  * in, or EOF, EAGAIN or an error; after a short read it asks once more,
  * so the EOF of a finite upstream lands in the same block.  Returns bytes
  * gathered; *eof / *err report why it stopped. */
+FSTRACE_DECL(ASYNC_BASE64DECODER_READ_INPUT_DUMP, "UID=%64u DATA=%A");
+
 static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
                      int *err)
 {
@@ -260,6 +265,8 @@ static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
     while (got < room) {
         size_t ask = room - got;
         ssize_t n = bytestream_1_read(st->up, dst + got, ask);
+        if (st->dir == DIR_DECODE)
+            FSTRACE(ASYNC_BASE64DECODER_READ_INPUT_DUMP, st->uid, dst + got, n);
         if (n < 0) {
             *err = errno ? errno : EIO;
             break;
@@ -658,6 +665,13 @@ static void stage_unregister(stage *st)
 
 /* ================================================================ encoder */
 
+FSTRACE_DECL(ASYNC_BASE64ENCODER_CREATE, "UID=%64u PTR=%p ASYNC=%p SOURCE=%p");
+FSTRACE_DECL(ASYNC_BASE64ENCODER_READ, "UID=%64u WANT=%z GOT=%z ERRNO=%e");
+FSTRACE_DECL(ASYNC_BASE64ENCODER_READ_DUMP, "UID=%64u DATA=%A");
+FSTRACE_DECL(ASYNC_BASE64ENCODER_CLOSE, "UID=%64u");
+FSTRACE_DECL(ASYNC_BASE64ENCODER_REGISTER, "UID=%64u OBJ=%p ACT=%p");
+FSTRACE_DECL(ASYNC_BASE64ENCODER_UNREGISTER, "UID=%64u");
+
 struct base64encoder {
     stage st; /* first member: the object pointer is the stage */
 };
@@ -670,26 +684,33 @@ base64encoder_t *base64_encode(async_t *async, bytestream_1 stream, char pos62,
         abort();
     b64x_alphabet abc = { pos62, pos63, padchar, pad };
     stage_init(&e->st, async, stream, DIR_ENCODE, abc);
+    FSTRACE(ASYNC_BASE64ENCODER_CREATE, e->st.uid, e, async, stream.obj);
     return e;
 }
 
 ssize_t base64encoder_read(base64encoder_t *e, void *buf, size_t count)
 {
-    return stage_read(&e->st, buf, count);
+    ssize_t n = stage_read(&e->st, buf, count);
+    FSTRACE(ASYNC_BASE64ENCODER_READ, e->st.uid, count, n);
+    FSTRACE(ASYNC_BASE64ENCODER_READ_DUMP, e->st.uid, buf, n);
+    return n;
 }
 
 void base64encoder_close(base64encoder_t *e)
 {
+    FSTRACE(ASYNC_BASE64ENCODER_CLOSE, e->st.uid);
     stage_close(&e->st);
 }
 
 void base64encoder_register_callback(base64encoder_t *e, action_1 action)
 {
+    FSTRACE(ASYNC_BASE64ENCODER_REGISTER, e->st.uid, action.obj, action.act);
     stage_register(&e->st, action);
 }
 
 void base64encoder_unregister_callback(base64encoder_t *e)
 {
+    FSTRACE(ASYNC_BASE64ENCODER_UNREGISTER, e->st.uid);
     stage_unregister(&e->st);
 }
 
@@ -747,6 +768,13 @@ bytestream_1 base64encoder_as_bytestream_1(base64encoder_t *e)
 
 /* ================================================================ decoder */
 
+FSTRACE_DECL(ASYNC_BASE64DECODER_CREATE, "UID=%64u PTR=%p ASYNC=%p SOURCE=%p");
+FSTRACE_DECL(ASYNC_BASE64DECODER_READ, "UID=%64u WANT=%z GOT=%z ERRNO=%e");
+FSTRACE_DECL(ASYNC_BASE64DECODER_READ_DUMP, "UID=%64u DATA=%A");
+FSTRACE_DECL(ASYNC_BASE64DECODER_CLOSE, "UID=%64u");
+FSTRACE_DECL(ASYNC_BASE64DECODER_REGISTER, "UID=%64u OBJ=%p ACT=%p");
+FSTRACE_DECL(ASYNC_BASE64DECODER_UNREGISTER, "UID=%64u");
+
 struct base64decoder {
     stage st;
 };
@@ -759,26 +787,33 @@ base64decoder_t *base64_decode(async_t *async, bytestream_1 stream, char pos62,
         abort();
     b64x_alphabet abc = { pos62, pos63, (char) -1, false };
     stage_init(&d->st, async, stream, DIR_DECODE, abc);
+    FSTRACE(ASYNC_BASE64DECODER_CREATE, d->st.uid, d, async, stream.obj);
     return d;
 }
 
 ssize_t base64decoder_read(base64decoder_t *d, void *buf, size_t count)
 {
-    return stage_read(&d->st, buf, count);
+    ssize_t n = stage_read(&d->st, buf, count);
+    FSTRACE(ASYNC_BASE64DECODER_READ, d->st.uid, count, n);
+    FSTRACE(ASYNC_BASE64DECODER_READ_DUMP, d->st.uid, buf, n);
+    return n;
 }
 
 void base64decoder_close(base64decoder_t *d)
 {
+    FSTRACE(ASYNC_BASE64DECODER_CLOSE, d->st.uid);
     stage_close(&d->st);
 }
 
 void base64decoder_register_callback(base64decoder_t *d, action_1 action)
 {
+    FSTRACE(ASYNC_BASE64DECODER_REGISTER, d->st.uid, action.obj, action.act);
     stage_register(&d->st, action);
 }
 
 void base64decoder_unregister_callback(base64decoder_t *d)
 {
+    FSTRACE(ASYNC_BASE64DECODER_UNREGISTER, d->st.uid);
     stage_unregister(&d->st);
 }
 

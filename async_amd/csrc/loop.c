@@ -17,11 +17,19 @@
  *    was already scheduled (ref src/async.c:386-392);
  *  - at most kBurst due tasks run before the loop polls file descriptors
  *    (ref take_immediate_action, src/async.c:564-590, uses 20);
- *  - async_register() watches a descriptor for readability with epoll;
- *    the GPU completion eventfd of the stages goes through it.
+ *  - async_register() has the reference's contract (include/async.h,
+ *    src/async.c:733-760): the descriptor is made non-blocking and watched
+ *    edge-triggered for EPOLLIN | EPOLLOUT, so the action runs when the
+ *    descriptor's state changes and is guaranteed only after a read or
+ *    write on it has returned EAGAIN (a registration itself may bring one
+ *    spurious call).  The GPU completion eventfd of the stages goes through
+ *    it; its action drains the eventfd to EAGAIN (b64_hub.c hub_wake), as
+ *    the reference's notification probe drains its pipe
+ *    (src/notification.c:24-43).
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <fcntl.h>
 #include <stdbool.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -299,6 +307,9 @@ static struct fd_watch *find_watch(async_t *async, int fd)
 
 int async_register(async_t *async, int fd, action_1 action)
 {
+    int fl = fcntl(fd, F_GETFL, 0);
+    if (fl < 0 || (!(fl & O_NONBLOCK) && fcntl(fd, F_SETFL, fl | O_NONBLOCK) < 0))
+        return -1;
     struct fd_watch *w = find_watch(async, fd);
     if (w) {
         w->action = action;
@@ -306,7 +317,7 @@ int async_register(async_t *async, int fd, action_1 action)
     }
     struct epoll_event ev;
     memset(&ev, 0, sizeof ev);
-    ev.events = EPOLLIN;
+    ev.events = EPOLLIN | EPOLLOUT | EPOLLET;
     ev.data.fd = fd;
     if (epoll_ctl(async->epfd, EPOLL_CTL_ADD, fd, &ev) < 0)
         return -1;

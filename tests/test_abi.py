@@ -125,3 +125,72 @@ def test_loop_and_streams_copy(burst, read_size):
     assert (out[:n] == data).all()
     if burst:
         assert eag.value > 0
+
+
+def test_async_register_is_edge_triggered():
+    """async_register() keeps the reference's contract (include/async.h,
+    src/async.c:733-760): the descriptor becomes non-blocking, and the action
+    runs on a change of state -- once per write here -- not again while
+    unread input is merely pending (level-triggered delivery would call it on
+    every loop turn)."""
+    L = _lib.load()
+
+    class Action(ctypes.Structure):
+        _fields_ = [("obj", ctypes.c_void_p), ("act", ctypes.c_void_p)]
+
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    L.make_async.restype = ctypes.c_void_p
+    L.async_now.argtypes = [ctypes.c_void_p]
+    L.async_now.restype = ctypes.c_uint64
+    L.async_register.argtypes = [ctypes.c_void_p, ctypes.c_int, Action]
+    L.async_unregister.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.async_timer_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, Action]
+    L.async_timer_start.restype = ctypes.c_void_p
+    L.async_loop.argtypes = [ctypes.c_void_p]
+    L.async_quit_loop.argtypes = [ctypes.c_void_p]
+    L.destroy_async.argtypes = [ctypes.c_void_p]
+    async_ = L.make_async()
+    calls = []
+    on_fd = CB(lambda obj: calls.append(1))
+    on_quit = CB(lambda obj: L.async_quit_loop(async_))
+    quit_addr = ctypes.cast(on_quit, ctypes.c_void_p).value
+
+    def turn(ms=30):
+        before = len(calls)
+        L.async_timer_start(async_, L.async_now(async_) + ms * 1000000,
+                            Action(None, quit_addr))
+        assert L.async_loop(async_) == 0
+        return len(calls) - before
+
+    r, w = os.pipe()
+    try:
+        assert os.get_blocking(r)
+        assert L.async_register(async_, r, Action(None, ctypes.cast(on_fd, ctypes.c_void_p).value)) == 0
+        assert not os.get_blocking(r)
+        turn()                      # a registration may bring one spurious call
+        os.write(w, b"x")
+        assert turn() == 1          # one edge, one call
+        assert turn() == 0          # still unread: no further call (edge-triggered)
+        os.write(w, b"y")
+        assert turn() == 1
+        assert os.read(r, 16) == b"xy"
+        assert L.async_unregister(async_, r) == 0
+    finally:
+        os.close(r)
+        os.close(w)
+        L.destroy_async(async_)
+
+
+def test_core_library_dependencies():
+    """The stages-only library (INTEGRATION.md Option A) needs exactly the
+    documented host-library symbols besides libc/HIP."""
+    core = os.path.join(ROOT, "async_amd", "libasync_b64_core.so")
+    out = subprocess.run(["nm", "-D", "--undefined-only", core],
+                         capture_output=True, text=True, check=True).stdout
+    names = {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
+    ours = {n for n in names if n.startswith(("async_", "NULL_ACTION", "bytestream_"))}
+    assert ours == {"async_wound", "async_execute", "async_register", "async_unregister",
+                    "NULL_ACTION_1"}
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    for n in ours:
+        assert f"`{n}" in doc, n
