@@ -784,7 +784,18 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //   status  per scan tile: flag (bits 63..62: 1 aggregate, 2 inclusive
 //           prefix; 0 = not yet) | value, for the scan's decoupled
 //           look-back; zero between calls (the scan's last tile clears it)
+//   lfail   ~(first failing slot) of k_decode_lines, 0 = none (cleared by
+//           k_decode_suffix); model: the line model it used
+//   fticket, fstatus  k_decode_suffix's tile ticket and status words
+// The line model of k_decode_lines (see there): lines of L alphabet
+// characters, each followed by s separator bytes; L = 0: no separators.
+struct LineModel {
+    uint32_t L, s;
+};
+
 struct DecodeWs {
+    uint64_t *lfail;     // ~(first failing slot) of k_decode_lines, 0 = none
+    LineModel *model;    // k_decode_lines' model, for k_decode_suffix
     uint64_t *fd;
     uint64_t *fd_cur;
     uint32_t *ticket;
@@ -813,6 +824,8 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.status = w.bases + nranges;
     w.fstatus = w.status + (nranges + kScanTile - 1) / kScanTile;
     w.fticket = (uint32_t *) (p + 20);
+    w.lfail = (uint64_t *) (p + 24);
+    w.model = (LineModel *) (p + 32);
     return w;
 }
 
@@ -1385,29 +1398,461 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
     return (tot & 0xFFFFu) + (tot >> 16);
 }
 
-// FUSED = 1: the single-pass exact decode (B64X_DEC_EXPECT_JUNK), in place
-// of pass 1 + scan + pass 2.  Blocks take tiles of kFuseTile ranges from a
-// ticket (so a tile's predecessors are running or done); each wave counts
-// its kFusePer ranges, the block publishes the tile's count and looks back
-// over its predecessors' status words as k_decode_scan2 does, then each
-// wave decodes its ranges with the same range body as pass 2d, re-reading
-// them (the tile was just read: L2/MALL hits).  The last tile writes the
-// result record, waits until every tile is inclusive and every block has
-// its ticket, and clears the status words and the ticket.
-template <bool FUSED>
-__global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
+// ---- line-structured single-pass decode ------------------------------------
+//
+// MIME-formatted base64 (RFC 2045: 76-character lines and CRLF; PEM: 64 and
+// LF) is clean text with separators at fixed positions.  Under a model of
+// the stream -- lines of L alphabet characters, each followed by s bytes
+// outside the alphabet, from position 0 on; L = 0 for no separators (clean
+// input) -- sextet i sits at position pos(i) = (i / L)(L + s) + i % L, so
+// every character's output place is known in closed form and no scan is
+// needed.  k_decode_lines is output-indexed: lane slot t owns sextets
+// [16t, 16t + 16), i.e. output bytes [12t, 12t + 12), and its span of input
+// [pos(16t), pos(16t + 16)) -- 16 characters plus, when a line ends inside
+// the slot, that line's s separator bytes.  It loads the span (one
+// dword-aligned 24-byte window), drops the separator with two funnel shifts
+// and a byte select, checks that the 16 characters are alphabet and the
+// separator bytes are not, and stores 12 bytes.  Slots whose spans lie in
+// the input ("interior", t < T) partition [0, pos(16T)), so when all pass,
+// that prefix holds exactly 16T alphabet characters in model order and the
+// stored bytes are the reference's; the < 16 + s bytes left after it are
+// decoded exactly by the one wave that owns slot T, which also writes the
+// result record.  The first failing slot t_f (any other structure, junk,
+// '=' inside the stream) is published; everything before pos(16 t_f) is
+// final, and k_decode_suffix<false> decodes [pos(16 t_f), n) exactly.  The
+// model is probed from the first 256 bytes by one wave per block; the
+// decode never depends on it being right, only its speed does.
+//
+// Reference: the per-character loop of decoder_read(), src/base64decoder.c:
+// 52-80 (skip non-alphabet bytes, 8 bits out per 4 characters' 24).
+constexpr uint32_t kLinesU = 2;                     // slots per lane
+constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
+constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
+
+DEV uint64_t line_pos(const LineModel m, uint64_t i)  // position of sextet i
+{
+    if (m.L == 0) return i;
+    return i / m.L * (m.L + m.s) + i % m.L;
+}
+
+// One wave: the model from the first 256 bytes -- L = the first byte
+// outside the alphabet, s = the run of such bytes after it.  Anything that
+// does not look like lines (L < 16 or > kLinesMaxL, s > kLinesMaxS, no
+// alphabet after the first run) gives the clean model.
+DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t p = 4 * lane;
+    uint32_t alpha = 0, pres = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if (p + j < n) {
+            pres |= 1u << j;
+            if (tab[in[p + j]] < 64u) alpha |= 1u << j;
+        }
+    }
+    LineModel m{0, 0};
+    const uint32_t junk = pres & ~alpha;
+    const uint64_t bj = __ballot(junk != 0);
+    if (!bj) return m;
+    const uint32_t lj = (uint32_t) __ffsll((unsigned long long) bj) - 1;
+    const uint32_t L = 4 * lj + (uint32_t) __builtin_ctz(
+                                    (uint32_t) __builtin_amdgcn_readlane((int) junk, (int) lj));
+    // the first alphabet byte after L
+    const uint32_t gt = p > L ? 0xFu : (p + 4 <= L + 1 ? 0u : (0xFu << (L + 1 - p)) & 0xFu);
+    const uint32_t am = alpha & gt;
+    const uint64_t ba = __ballot(am != 0);
+    if (!ba) return m;
+    const uint32_t la = (uint32_t) __ffsll((unsigned long long) ba) - 1;
+    const uint32_t P = 4 * la + (uint32_t) __builtin_ctz(
+                                    (uint32_t) __builtin_amdgcn_readlane((int) am, (int) la));
+    const uint32_t s = P - L;
+    if (L < 16 || L > kLinesMaxL || s > kLinesMaxS) return m;
+    m.L = L;
+    m.s = s;
+    return m;
+}
+
+// 16 bytes from a dword-aligned p; bytes at or past `end` are unspecified
+// (never faulting: a partial window is read bytewise).
+DEV uint4 load_win16(const uint8_t *p, const uint8_t *end)
+{
+    const int64_t left = end - p;
+    if (left >= 16) return load16_a4(p);
+    if (left <= 0) return make_uint4(0, 0, 0, 0);
+    return load_chars(p, (uint32_t) left);
+}
+
+DEV uint2 load_win8(const uint8_t *p, const uint8_t *end)
+{
+    const int64_t left = end - p;
+    if (left >= 8) {
+        const u32x2a4 v = *(const u32x2a4 *) p;
+        return make_uint2(v.x, v.y);
+    }
+    uint32_t w[2] = {0, 0};
+    for (int64_t i = 0; i < left; i++) w[i >> 2] |= (uint32_t) p[i] << (8 * (i & 3));
+    return make_uint2(w[0], w[1]);
+}
+
+// byte-select: bytes of x where mask has 0xFF, else bytes of y
+DEV uint32_t bsel(uint32_t mask, uint32_t x, uint32_t y) { return (x & mask) | (y & ~mask); }
+
+// The 16 characters of a slot whose span starts at window byte o of w[0..5]
+// (24 bytes from a dword boundary), c of them before a line end followed by
+// s separator bytes (c = 16 when no line ends inside or right after the
+// slot); *sep receives the separator bytes (low s bytes).
+DEV uint4 slot_chars(const uint32_t w[6], uint32_t o, uint32_t c, uint32_t s, uint32_t *sep)
+{
+    uint32_t A[6];
+#pragma unroll
+    for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], o);
+    A[5] = __builtin_amdgcn_alignbyte(0u, w[5], o);
+    uint32_t D[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        // the bytes after the separator: A shifted by s (1..4, wave-uniform)
+        const uint32_t Bj = s >= 4 ? A[j + 1] : __builtin_amdgcn_alignbyte(A[j + 1], A[j], s);
+        const int keep = (int) c - 4 * j;  // bytes of dword j before the line end
+        const uint32_t mask = keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+        D[j] = bsel(mask, A[j], Bj);
+    }
+    // separator bytes at A[c .. c + s)
+    const uint32_t q = c >> 2, r = c & 3u;
+    const uint32_t lo = q == 0 ? A[0] : q == 1 ? A[1] : q == 2 ? A[2] : q == 3 ? A[3] : A[4];
+    const uint32_t hi = q == 0 ? A[1] : q == 1 ? A[2] : q == 2 ? A[3] : q == 3 ? A[4] : A[5];
+    *sep = __builtin_amdgcn_alignbyte(hi, lo, r);
+    return make_uint4(D[0], D[1], D[2], D[3]);
+}
+
+// One wave: the model into the workspace, for k_decode_lines (every block
+// reads it with one scalar load, instead of every block probing: 175 K
+// probes of the same 256 bytes cost 7 % of a 1 GiB decode) and
+// k_decode_suffix.
+__global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
+                                                     DecAlpha a, void *ws, uint32_t nranges)
+{
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    const LineModel m = probe_lines(tab, in, n);
+    if (threadIdx.x == 0) *ws_view(ws, nranges).model = m;
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_lines(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res)
+{
+    __shared__ uint8_t tab[256];
+    __shared__ uint8_t s_tail[64];
+    // the scalar load of the model overlaps the table build
+    const uint64_t mw = scalar_load_u64((const uint64_t *) ws_view(ws, nranges).model);
+    build_dec_table(tab, a);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t L = (uint32_t) mw;
+    const uint32_t s = (uint32_t) (mw >> 32);
+    const uint32_t P = L + s;
+    const LineModel m{L, s};
+    // n <= 2^31 (the launcher's bound), so sextet indices and positions fit
+    // in 32 bits.  T: the slots whose spans lie wholly inside the input.
+    const uint32_t n32 = (uint32_t) n;
+    uint32_t T;
+    if (L == 0) {
+        T = n32 / 16;
+    } else {
+        const uint32_t F = n32 / P * L + (n32 % P < L ? n32 % P : L);  // model alphabet positions
+        T = F / 16;
+        if (T && (16 * T) % L == 0 && (16 * T) / L * P > n32) T--;
+    }
+    const uint32_t t0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kLinesSlots;
+    if (t0 > T) return;
+    const uint32_t ns = T - t0 >= kLinesSlots ? kLinesSlots : T - t0;  // interior slots here
+    const bool full = ns == kLinesSlots;
+    uint32_t fail_u = kLinesU, fail_lane = 0;  // the wave's first failing slot
+    const bool oal = (((uintptr_t) out) & 3) == 0;
+    if (ns && L == 0 && full && oal && (((uintptr_t) in) & 3) == 0) {
+        // The hot path (clean input, a full wave, aligned buffers): lane t's
+        // 16 characters are one non-temporal dwordx4 at 16t, its 12 bytes one
+        // non-temporal dwordx3 at 12t -- pass 1's fast path, output-indexed.
+        // Kept apart from the general path below so that no load or store
+        // here is exec-masked (a masked form also lost the nt bit and waited
+        // on every load at once: 7 % slower).
+        uint4 c[kLinesU];
+#pragma unroll
+        for (uint32_t u = 0; u < kLinesU; u++) c[u] = ld16<true>(in + 16 * (t0 + u * 64 + lane));
+#pragma unroll
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            uint32_t G[4], bad;
+            map_fast(tab, c[u], 16, G, bad);
+            const uint64_t fb = __ballot(bad != 0);
+            if (fb && fail_u == kLinesU) {
+                fail_u = u;
+                fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
+            }
+            emit_full_a4<true>(G, out + 12 * (uint64_t) (t0 + u * 64));
+        }
+    } else if (ns) {
+        uint32_t G[kLinesU][4], bad[kLinesU];
+        if (L == 0 && (((uintptr_t) in) & 3) == 0) {
+            // clean model, aligned input, a partial wave
+            uint4 c[kLinesU];
+#pragma unroll
+            for (uint32_t u = 0; u < kLinesU; u++) {
+                const uint8_t *p = in + 16 * (t0 + u * 64 + lane);
+                c[u] = u * 64 + lane < ns ? load16_a4(p) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kLinesU; u++) map_fast(tab, c[u], 16, G[u], bad[u]);
+        } else {
+            // line coordinates of the wave's first sextet (scalar), then each
+            // lane's from a small offset (a 20-bit reciprocal, exact below 4,096)
+            const uint32_t i0 = 16 * t0;
+            const uint32_t line0 = L ? i0 / L : 0;
+            const uint32_t col0 = L ? i0 - line0 * L : 0;
+            const uint32_t rcp = L ? ((1u << 20) + L - 1) / L : 0;
+            const uint8_t *end = in + n;
+            // no window of this wave reaches past the input: unguarded loads
+            const uint64_t last_pos = L ? (uint64_t) ((i0 + 16 * ns) / L) * P + (i0 + 16 * ns) % L
+                                        : (uint64_t) i0 + 16 * ns;
+            const bool safe = last_pos + 40 <= n;
+            uint4 win[kLinesU];
+            uint2 wx[kLinesU];
+            uint32_t oo[kLinesU], cc[kLinesU];
+            bool hs[kLinesU];
+#pragma unroll
+            for (uint32_t u = 0; u < kLinesU; u++) {
+                const uint32_t rel = col0 + 16 * (u * 64 + lane);
+                const uint32_t dl = L ? (uint32_t) (((uint64_t) rel * rcp) >> 20) : 0;
+                const uint32_t col = rel - dl * L;
+                const uint32_t pos = L ? (line0 + dl) * P + col : i0 + 16 * (u * 64 + lane);
+                hs[u] = L && L - col <= 16;  // a line ends in (or right after) the slot
+                cc[u] = hs[u] ? L - col : 16u;
+                const uint8_t *ap = in + pos;
+                const uint8_t *ab = (const uint8_t *) ((uintptr_t) ap & ~(uintptr_t) 3);
+                oo[u] = (uint32_t) (ap - ab);
+                if (safe) {
+                    win[u] = load16_a4(ab);
+                    const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+                    wx[u] = make_uint2(v.x, v.y);
+                } else {
+                    const bool live = u * 64 + lane < ns;
+                    win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
+                    wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kLinesU; u++) {
+                const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+                uint32_t sep;
+                const uint4 d = slot_chars(w6, oo[u], cc[u], s, &sep);
+                map_fast(tab, d, 16, G[u], bad[u]);
+                if (hs[u]) {
+                    // the line's separator bytes must all be outside the alphabet
+#pragma unroll
+                    for (uint32_t k = 0; k < kLinesMaxS; k++)
+                        if (k < s && tab[(sep >> (8 * k)) & 0xFFu] < 64u) bad[u] |= 0x100u;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            const bool live = u * 64 + lane < ns;
+            const uint64_t fb = __ballot(live && bad[u] != 0);
+            if (fb && fail_u == kLinesU) {
+                fail_u = u;
+                fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
+            }
+            uint8_t *o = out + 12 * (uint64_t) (t0 + u * 64);
+            if (oal && full) {
+                emit_full_a4<true>(G[u], o);
+            } else if (live) {
+                uint32_t o0, o1, o2;
+                groups_to_bytes(G[u][0], G[u][1], G[u][2], G[u][3], o0, o1, o2);
+                store_bytes12(o + 12 * lane, o0, o1, o2, 12);
+            }
+        }
+    }
+    if (fail_u < kLinesU && lane == 0) {
+        // publish the first failing slot; only an improvement (the
+        // device-scope load sees what earlier waves published)
+        const unsigned long long key = ~(unsigned long long) (t0 + fail_u * 64 + fail_lane);
+        unsigned long long *lf = (unsigned long long *) ws_view(ws, nranges).lfail;
+        const unsigned long long cur =
+            __hip_atomic_load(lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (key > cur) atomicMax(lf, key);
+    }
+    if (T >= t0 + kLinesSlots) return;
+    // This wave owns slot T: the < 16 + s bytes after the last interior
+    // span, decoded exactly, and the result record (replaced by
+    // k_decode_suffix when a slot failed).
+    const uint64_t Q = line_pos(m, 16 * (uint64_t) T);
+    const uint32_t tl = (uint32_t) (n - Q);  // < 16 + s <= 20
+    const bool here = lane < tl;
+    const uint32_t tv = here ? tab[in[Q + lane]] : 0xFFu;
+    const bool al = tv < 64u;
+    const uint64_t mb = __ballot(al);
+    const uint32_t Vt = (uint32_t) __popcll(mb);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (mb >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t) mb, 0u));
+    if (al) s_tail[rank] = (uint8_t) tv;
+    wave_lds_order();
+    const uint32_t ng = Vt >> 2, rem = Vt & 3u;
+    uint8_t *ot = out + 12 * (uint64_t) T;
+    if (lane < ng) {
+        const uint32_t G = ((uint32_t) s_tail[4 * lane] << 18) | ((uint32_t) s_tail[4 * lane + 1] << 12) |
+                           ((uint32_t) s_tail[4 * lane + 2] << 6) | s_tail[4 * lane + 3];
+        ot[3 * lane] = (uint8_t) (G >> 16);
+        ot[3 * lane + 1] = (uint8_t) (G >> 8);
+        ot[3 * lane + 2] = (uint8_t) G;
+    } else if (lane == ng && !hold && rem >= 2) {
+        // the final partial group: floor(6r/8) bytes (src/base64decoder.c:71-76)
+        const uint32_t G = ((uint32_t) s_tail[4 * ng] << 18) | ((uint32_t) s_tail[4 * ng + 1] << 12) |
+                           (rem > 2 ? (uint32_t) s_tail[4 * ng + 2] << 6 : 0u);
+        ot[3 * ng] = (uint8_t) (G >> 16);
+        if (rem > 2) ot[3 * ng + 1] = (uint8_t) (G >> 8);
+    }
+    if (lane == 0) {
+        const uint64_t V = 16 * (uint64_t) T + Vt;
+        b64x_dec_result r;
+        r.out_len = hold ? V / 4 * 3 : V * 6 / 8;
+        r.valid = V;
+        r.tail_n = rem;
+        for (uint32_t j = 0; j < 4; j++) r.tail[j] = j < rem ? s_tail[4 * ng + j] : 0;
+        *res = r;  // provisional: k_decode_suffix mirrors it to the host or replaces it
+    }
+}
+
+// One range of the exact decode: characters [start, re) (re = the range's
+// end, the stream's when `last`), whose first 2,048 characters' chunks are
+// c[] (nin[] characters of each lane in range).  T0 = 0 when the range
+// starts on a group boundary, else minus the 0-3 sextets the previous range
+// owns (they land in the window's head); ob = the output address of the
+// range's first owned group; la (valid if la_ok) = the lookahead byte after
+// re.  A range longer than 2,048 characters (inputs past 2 GiB: the range
+// count is capped) is taken 2,048 at a time, the window's whole dwords
+// flushed between steps and its partial dword carried to the front (as
+// decode_buf_bits does); the bytes flushed early are final and never reach
+// the next range's output.
+DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ in, uint64_t n,
+                      uint64_t start, uint64_t re, int T0, uint8_t *ob, const uint4 c[2],
+                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold)
+{
+    const uint32_t lane = lane_id();
+    uint32_t *bits = (uint32_t *) bq;
+    int T = T0;
+    const uint32_t skew = (uint32_t) ((uintptr_t) ob & 3);
+    uint32_t lo = 4 + skew;       // LDS byte of output byte `done`
+    int pb0 = 8 * (int) lo;       // window bit of relative sextet 0
+    uint32_t done = 0;            // bytes flushed by earlier steps
+    static_assert(kP2dBlocks > 64 && kP2dBlocks <= 128, "two zeroing stores per lane");
+    bq[lane] = make_uint4(0, 0, 0, 0);
+    if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+    wave_lds_order();
+    for (uint64_t pos = start;; pos += 2 * kChunk) {
+        uint4 ch[2] = {c[0], c[1]};
+        uint32_t nh[2] = {nin[0], nin[1]};
+        if (pos != start) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
+                nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
+                ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
+            }
+        }
+        T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
+        if (pos + 2 * kChunk >= re) break;
+        // more of this range to come: flush the window's whole dwords
+        wave_lds_order();
+        const int bit_end = pb0 + 6 * T;
+        const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~3u : 0u;
+        if (kcut > lo) {
+            store_bits(bits, lo, kcut, ob + done - lo);
+            done += kcut - lo;
+            const uint32_t keep = bits[kcut >> 2];
+            wave_lds_order();
+            bq[lane] = make_uint4(0, 0, 0, 0);
+            if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+            wave_lds_order();
+            if (lane == 0) bits[1] = keep;
+            wave_lds_order();
+            pb0 -= 8 * (int) (kcut - 4);
+            lo = 4;
+        }
+    }
+    bool at_end = last;
+    if (!last && T > 0 && (T & 3)) {
+        // complete the range's last group from the characters after it
+        bool ok = la_ok;
+        for (uint64_t q = re;;) {
+            const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+            const bool v = t < 64u;
+            const uint64_t m = __ballot(v);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+            const int need = 4 - (T & 3);
+            if (v && (int) rank < need)
+                or_field(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
+            const int got = __popcll(m);
+            if (got >= need) {
+                T += need;
+                break;
+            }
+            T += got;
+            q += 64;
+            if (q >= n) {
+                at_end = true;  // the stream's final, incomplete group
+                break;
+            }
+            ok = q + lane < n;
+            la = ok ? in[q + lane] : 0u;
+        }
+    }
+    wave_lds_order();
+    if (T > 0) {
+        const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
+        // the final partial group: 2 sextets -> 1 byte, 3 -> 2 (floor(6r/8),
+        // src/base64decoder.c:59-62,71-76)
+        const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
+        const uint32_t total = 3 * ng + tail;
+        if (total > done) store_bits(bits, lo, lo + (total - done), ob + done - lo);
+    }
+    wave_lds_order();  // the next range re-zeroes the buffer
+}
+
+// The first step's chunks of the range [rb, re) from `start` on, and its
+// lookahead byte.
+DEV void load_range(const uint8_t *__restrict__ in, uint64_t n, uint64_t start, uint64_t re,
+                    bool last, uint4 c[2], uint32_t nin[2], uint32_t &la, bool &la_ok)
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+        nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+        c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+    }
+    la_ok = !last && re + lane < n;
+    la = la_ok ? in[re + lane] : 0u;
+}
+
+DEV int range_skip(uint64_t B) { return -(int) ((4 - (B & 3)) & 3); }
+
+// Pass 2 (exact), after pass 1 and the scan: grid-stride over the ranges
+// from the first dirty chunk on, with exactly the resident blocks.  The
+// first dirty range resumes at its dirty chunk (everything before it was
+// alphabet and is final); later ranges re-run with their true base.  For
+// the middle ranges the next range's loads (both chunks, the lookahead
+// bytes, its base) are issued before this range is processed.
+__global__ __launch_bounds__(kThreads) void k_decode_pass2d(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out,
-    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold,
-    b64x_dec_result *res, b64x_dec_result *hres)
+    uint64_t R, uint32_t nranges, DecAlpha a, void *ws, uint32_t hold)
 {
     DecodeWs w = ws_view(ws, nranges);
-    uint32_t r0 = 0xFFFFFFFFu, off0 = 0;  // fused: no range resumes mid-way
-    if (!FUSED) {
-        const uint64_t packed = *w.fd_cur;
-        if (packed == 0) return;
-        r0 = (uint32_t) (~packed >> 32);
-        off0 = (uint32_t) ~packed;
-    }
+    const uint64_t packed = *w.fd_cur;
+    if (packed == 0) return;
+    const uint32_t r0 = (uint32_t) (~packed >> 32);
+    const uint32_t off0 = (uint32_t) ~packed;
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
@@ -1415,139 +1860,135 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
-    uint32_t *bits = (uint32_t *) bq;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    // One range: the first 2,048 characters' chunks c[] (nin[] characters of
-    // each lane in range), the lookahead byte la (valid if la_ok), its base
-    // B.  A range longer than 2,048 characters (inputs past 2 GiB: the
-    // range count is capped) is taken 2,048 at a time, the window's whole
-    // dwords flushed between steps and its partial dword carried to the
-    // front (as decode_buf_bits does); the bytes flushed early are final
-    // and never reach the next range's output.
-    auto process = [&](uint32_t r, const uint4 *c, const uint32_t *nin, uint32_t la, bool la_ok,
-                       uint64_t B) {
+    auto generic = [&](uint32_t r) {
         const uint64_t rb = (uint64_t) r * R;
         const uint64_t re = rb + R < n ? rb + R : n;
         const bool last = r + 1 == nranges, first = r == r0;
-        int T = first ? 0 : -(int) ((4 - (B & 3)) & 3);  // < 0: sextets to skip
-        uint8_t *ob = out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3);
-        const uint32_t skew = (uint32_t) ((uintptr_t) ob & 3);
-        uint32_t lo = 4 + skew;       // LDS byte of output byte `done`
-        int pb0 = 8 * (int) lo;       // window bit of relative sextet 0
-        uint32_t done = 0;            // bytes flushed by earlier steps
-        static_assert(kP2dBlocks > 64 && kP2dBlocks <= 128, "two zeroing stores per lane");
-        bq[lane] = make_uint4(0, 0, 0, 0);
-        if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
-        wave_lds_order();
+        const uint64_t B = scalar_load_u64(w.bases + r);
         const uint64_t start = first ? rb + off0 : rb;
-        for (uint64_t pos = start;; pos += 2 * kChunk) {
-            uint4 ch[2] = {c[0], c[1]};
-            uint32_t nh[2] = {nin[0], nin[1]};
-            if (pos != start) {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
-                    nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
-                    ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
-                }
-            }
-            T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
-            if (pos + 2 * kChunk >= re) break;
-            // more of this range to come: flush the window's whole dwords
-            wave_lds_order();
-            const int bit_end = pb0 + 6 * T;
-            const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~3u : 0u;
-            if (kcut > lo) {
-                store_bits(bits, lo, kcut, ob + done - lo);
-                done += kcut - lo;
-                const uint32_t keep = bits[kcut >> 2];
-                wave_lds_order();
-                bq[lane] = make_uint4(0, 0, 0, 0);
-                if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
-                wave_lds_order();
-                if (lane == 0) bits[1] = keep;
-                wave_lds_order();
-                pb0 -= 8 * (int) (kcut - 4);
-                lo = 4;
-            }
-        }
-        bool at_end = last;
-        if (!last && T > 0 && (T & 3)) {
-            // complete the range's last group from the characters after it
-            bool ok = la_ok;
-            for (uint64_t q = re;;) {
-                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
-                const bool v = t < 64u;
-                const uint64_t m = __ballot(v);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                const int need = 4 - (T & 3);
-                if (v && (int) rank < need)
-                    or_field(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
-                const int got = __popcll(m);
-                if (got >= need) {
-                    T += need;
-                    break;
-                }
-                T += got;
-                q += 64;
-                if (q >= n) {
-                    at_end = true;  // the stream's final, incomplete group
-                    break;
-                }
-                ok = q + lane < n;
-                la = ok ? in[q + lane] : 0u;
-            }
-        }
-        wave_lds_order();
-        if (T > 0) {
-            const uint32_t ng = (uint32_t) T >> 2, rem = (uint32_t) T & 3u;
-            // the final partial group: 2 sextets -> 1 byte, 3 -> 2 (floor(6r/8),
-            // src/base64decoder.c:59-62,71-76)
-            const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
-            const uint32_t total = 3 * ng + tail;
-            if (total > done) store_bits(bits, lo, lo + (total - done), ob + done - lo);
-        }
-        wave_lds_order();  // the next range re-zeroes the buffer
+        uint4 c[2];
+        uint32_t nin[2], la;
+        bool la_ok;
+        load_range(in, n, start, re, last, c, nin, la, la_ok);
+        decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
+                     out + (first ? (B + off0) / 4 * 3 : (B + 3) / 4 * 3), c, nin, la, la_ok,
+                     last, hold);
     };
-    // the first step's chunks of range r (from `start`) and its lookahead
-    auto load_range = [&](uint32_t r, uint4 *c, uint32_t *nin, uint32_t &la, bool &la_ok) {
-        const uint64_t rb = (uint64_t) r * R;
-        const uint64_t re = rb + R < n ? rb + R : n;
-        const bool last = r + 1 == nranges, first = r == r0;
-        const uint64_t start = first ? rb + off0 : rb;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-            nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+    uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
+    if (r == r0 && r < nranges) {
+        generic(r);
+        r += nw;
+    }
+    const uint32_t mid_end = nranges - 1;
+    if (R == 2 * kChunk && r < mid_end && (((uintptr_t) in) & 3) == 0) {
+        const uint32_t full[2] = {16u, 16u};
+        auto ld_la = [&](uint32_t rr) {
+            const uint64_t q = (uint64_t) (rr + 1) * R + lane;
+            return (uint32_t) in[q < n ? q : n - 1];
+        };
+        uint4 c[2];
+        c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
+        c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
+        uint32_t la = ld_la(r);
+        uint64_t B = scalar_load_u64(w.bases + r);
+        while (r < mid_end) {
+            const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
+            uint4 cn[2];
+            cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
+            cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
+            const uint32_t lan = ld_la(rn);
+            const uint64_t Bn = scalar_load_u64(w.bases + rn);
+            const uint64_t rb = (uint64_t) r * R;
+            decode_range(sm, bq, in, n, rb, rb + R, range_skip(B), out + (B + 3) / 4 * 3, c, full,
+                         la, (uint64_t) (r + 1) * R + lane < n, false, hold);
+            r += nw;
+            c[0] = cn[0];
+            c[1] = cn[1];
+            la = lan;
+            B = Bn;
         }
-        la_ok = !last && re + lane < n;
-        la = la_ok ? in[re + lane] : 0u;
-    };
-    if (FUSED) {
-        __shared__ uint32_t s_tile;
-        __shared__ uint32_t s_cnt[kFuseTile];
-        __shared__ uint64_t s_excl, s_agg;
-        const uint32_t ntiles = (nranges + kFuseTile - 1) / kFuseTile;
+    }
+    for (; r < nranges; r += nw) generic(r);
+}
+
+// ---- single-pass exact decode of a suffix ---------------------------------
+//
+// Decodes characters [S, n) into out + O, S being a group boundary of the
+// whole stream (Vb = the alphabet characters before S, a multiple of 4, O =
+// 3 Vb / 4), and writes the result record for the whole stream.  WHOLE: S =
+// 0 (B64X_DEC_EXPECT_JUNK); else S, O, Vb come from the first failing slot
+// k_decode_lines published, and the kernel exits at once when there is none
+// (the common case: every block reads one word and returns).
+//
+// Ranges are the pass-1 ranges of R = 2,048 characters, aligned to the
+// stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
+// tiles of kFuseTile ranges from a ticket in the order they start (so a
+// tile's predecessors are running or done); each wave counts its kFusePer
+// ranges, the block publishes the tile's count and looks back over its
+// predecessors' status words as k_decode_scan2 does, then each wave decodes
+// its ranges with decode_range, re-reading them (the tile was just read:
+// L2/MALL hits).  The last tile writes the result record, waits until every
+// tile is inclusive and every other block has drawn its final ticket, then
+// clears the status words, the ticket and the failure word.
+template <bool WHOLE>
+__global__ __launch_bounds__(kThreads) void k_decode_suffix(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres)
+{
+    constexpr uint64_t R = 2 * kChunk;
+    DecodeWs w = ws_view(ws, nranges);
+    uint64_t S = 0, Vb = 0;
+    if (!WHOLE) {
+        const uint64_t key = scalar_load_u64(w.lfail);
+        if (key == 0) {
+            // k_decode_lines took everything: its record is final.  The host
+            // mirror is written only now, so a completion never finds a
+            // consistent but provisional record there.
+            if (hres && blockIdx.x == 0 && threadIdx.x == 0) {
+                const b64x_dec_result r = *res;
+                *hres = r;
+            }
+            return;
+        }
+        const uint64_t tf = ~key;  // the first failing slot of k_decode_lines
+        Vb = 16 * tf;
+        S = line_pos(*w.model, Vb);
+    }
+    const uint8_t *base_in = in;
+    uint8_t *base_out = out + Vb / 4 * 3;
+    const uint32_t r0 = (uint32_t) (S / R);
+    const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
+    __shared__ P2dSmem sm;
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_cnt[kFuseTile];
+    __shared__ uint64_t s_excl, s_agg;
+    build_dec_table(sm.tab, a);
+    build_compact_sel(sm.sel);
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *bq = sm.bits[wv];
+    for (;;) {
+        __syncthreads();  // s_tile / s_cnt of the previous tile are consumed
         if (threadIdx.x == 0) s_tile = atomicAdd(w.fticket, 1u);
         __syncthreads();
         const uint32_t t = s_tile;
-        const uint32_t rw = t * kFuseTile + wv * kFusePer;  // this wave's first range
-        // counts (R is one step: the caller takes this path only then); all
-        // of the wave's loads are issued before any is counted
+        if (t >= ntiles) return;
+        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
+        // counts; all of the wave's loads are issued before any is counted
         for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
             uint4 c[kFuseLoad][2];
             uint32_t nin[kFuseLoad][2];
 #pragma unroll
             for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                const uint32_t j = j0 + jj;
-                const uint64_t rb = (uint64_t) (rw + j) * R;
+                const uint32_t r = rw + j0 + jj;
+                const uint64_t rb = (uint64_t) r * R;
+                const uint64_t beg = rb > S ? rb : S;
                 const uint64_t re = rb + R < n ? rb + R : n;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const uint64_t p = rb + (uint64_t) h * kChunk + 16 * lane;
-                    nin[jj][h] = rw + j >= nranges || p >= re
+                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
+                    nin[jj][h] = r >= nranges || p >= re
                                      ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
                     c[jj][h] =
                         nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
@@ -1599,81 +2040,49 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d_t(
             }
         }
         __syncthreads();
-        uint64_t B = s_excl;
+        uint64_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
         for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
+            const uint32_t r = rw + j;
+            const uint64_t rb = (uint64_t) r * R;
+            const uint64_t re = rb + R < n ? rb + R : n;
+            const bool first = r == r0, last = r + 1 == nranges;
+            const uint64_t start = first ? S : rb;
             uint4 c[2];
             uint32_t nin[2], la;
             bool la_ok;
-            load_range(rw + j, c, nin, la, la_ok);
-            process(rw + j, c, nin, la, la_ok, B);
+            load_range(base_in, n, start, re, last, c, nin, la, la_ok);
+            decode_range(sm, bq, base_in, n, start, re, first ? 0 : range_skip(B),
+                         base_out + (B + 3) / 4 * 3, c, nin, la, la_ok, last, hold);
             B += s_cnt[wv * kFusePer + j];
         }
-        if (t == ntiles - 1 && wv == 0) {
-            const uint64_t V = s_excl + s_agg;
-            if (lane == 0) write_result(res, hres, V, hold);
-            find_tail_sextets(sm.tab, in, n, V, res, hres);
-            for (;;) {  // every tile inclusive -> every look-back is over
-                bool all = true;
-                for (uint32_t i = lane; i < ntiles; i += 64)
-                    all = all && (st_load(&w.fstatus[i]) >> 62) == 2;
-                if (__all(all)) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
-            if (lane == 0) {  // every block has its ticket -> re-arm the counter
-                while (__hip_atomic_load(w.fticket, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
+        if (t == ntiles - 1) {
+            if (wv == 0) {
+                const uint64_t V = Vb + s_excl + s_agg;
+                if (lane == 0) write_result(res, hres, V, hold);
+                find_tail_sextets(sm.tab, in, n, V, res, hres);
+                for (;;) {  // every tile inclusive -> every look-back is over
+                    bool all = true;
+                    for (uint32_t i = lane; i < ntiles; i += 64)
+                        all = all && (st_load(&w.fstatus[i]) >> 62) == 2;
+                    if (__all(all)) break;
                     __builtin_amdgcn_s_sleep(1);
-                __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+                if (lane == 0) {
+                    // every other block has drawn its final ticket -> re-arm
+                    const uint32_t want = ntiles + gridDim.x - 1;
+                    while (__hip_atomic_load(w.fticket, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) != want)
+                        __builtin_amdgcn_s_sleep(1);
+                    __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!WHOLE) *w.lfail = 0;
+                }
             }
-        }
-        return;
-    }
-    auto load_generic = [&](uint32_t r) {
-        uint4 c[2];
-        uint32_t nin[2], la;
-        bool la_ok;
-        load_range(r, c, nin, la, la_ok);
-        process(r, c, nin, la, la_ok, scalar_load_u64(w.bases + r));
-    };
-    uint32_t r = r0 + blockIdx.x * kWavesPerBlock + wv;
-    if (r == r0 && r < nranges) {
-        load_generic(r);
-        r += nw;
-    }
-    const uint32_t mid_end = nranges - 1;
-    if (R == 2 * kChunk && r < mid_end && (((uintptr_t) in) & 3) == 0) {
-        const uint32_t full[2] = {16u, 16u};
-        auto ld_la = [&](uint32_t rr) {
-            const uint64_t q = (uint64_t) (rr + 1) * R + lane;
-            return (uint32_t) in[q < n ? q : n - 1];
-        };
-        uint4 c[2];
-        c[0] = load16_a4(in + (uint64_t) r * R + 16 * lane);
-        c[1] = load16_a4(in + (uint64_t) r * R + kChunk + 16 * lane);
-        uint32_t la = ld_la(r);
-        uint64_t B = scalar_load_u64(w.bases + r);
-        while (r < mid_end) {
-            const uint32_t rn = r + nw < mid_end ? r + nw : r;  // unconditional prefetch
-            uint4 cn[2];
-            cn[0] = load16_a4(in + (uint64_t) rn * R + 16 * lane);
-            cn[1] = load16_a4(in + (uint64_t) rn * R + kChunk + 16 * lane);
-            const uint32_t lan = ld_la(rn);
-            const uint64_t Bn = scalar_load_u64(w.bases + rn);
-            process(r, c, full, la, (uint64_t) (r + 1) * R + lane < n, B);
-            r += nw;
-            c[0] = cn[0];
-            c[1] = cn[1];
-            la = lan;
-            B = Bn;
+            return;  // this block draws no further ticket
         }
     }
-    for (; r < nranges; r += nw) load_generic(r);
 }
-
-constexpr auto k_decode_pass2d = k_decode_pass2d_t<false>;
-constexpr auto k_decode_fused = k_decode_pass2d_t<true>;
 
 // Batches: buffer b is in[ioff(b) .. +len(b)) -> out + ooff(b).
 struct BatchLayout {
@@ -2483,14 +2892,35 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     const uint32_t blocks = (p.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const DecAlpha a = dec_alpha(abc);
     const uint32_t hold = flags & B64X_DEC_HOLD_TAIL;
-    if ((flags & B64X_DEC_EXPECT_JUNK) && p.R == 2 * kChunk) {
-        // one pass: a block per tile of kFuseTile ranges, in ticket order
-        const uint32_t tiles = (p.nranges + kFuseTile - 1) / kFuseTile;
-        hipLaunchKernelGGL(k_decode_fused, dim3(tiles), dim3(kThreads), 0, s,
-                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                           a, ws, hold, d_res, h_res);
+    if (p.R == 2 * kChunk) {
+        // Inputs up to 2^31 characters: the line-structured single pass
+        // (clean input is its L = 0 case), then the exact single-pass decode
+        // of whatever suffix it could not take -- nothing, on clean and
+        // MIME-formatted text: each block of that launch reads one word and
+        // returns.  EXPECT_JUNK skips the first.
+        static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
+        const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
+        if (flags & B64X_DEC_EXPECT_JUNK) {
+            hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
+                               hold, d_res, h_res);
+            return launch_status();
+        }
+        hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(64), 0, s, (const uint8_t *) d_in, nchars,
+                           a, ws, p.nranges);
+        if ((err = launch_status())) return err;
+        const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
+        hipLaunchKernelGGL(k_decode_lines, dim3((uint32_t) ((waves + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
+                           p.nranges, a, ws, hold, d_res);
+        if ((err = launch_status())) return err;
+        hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
+                           (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
+                           hold, d_res, h_res);
         return launch_status();
     }
+    // Larger inputs (ranges longer than 2,048 characters): pass 1, the scan,
+    // pass 2.
     hipLaunchKernelGGL(k_pass1, dim3(blocks), dim3(kThreads), 0, s, (const uint8_t *) d_in,
                        nchars, (uint8_t *) d_out, p.R, p.nranges, a, ws, hold);
     if ((err = launch_status())) return err;
@@ -2504,7 +2934,7 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     const uint32_t b2 = cap_grid(blocks, (uint64_t) d->cus * occ2d);
     hipLaunchKernelGGL(k_decode_pass2d, dim3(b2), dim3(kThreads), 0, s,
                        (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.R, p.nranges,
-                       a, ws, hold, (b64x_dec_result *) nullptr, (b64x_dec_result *) nullptr);
+                       a, ws, hold);
     return launch_status();
 }
 
