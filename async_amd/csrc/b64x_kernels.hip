@@ -790,8 +790,14 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 // The line model of k_decode_lines (see there): lines of L alphabet
 // characters, each followed by s separator bytes; L = 0: no separators.
 struct LineModel {
-    uint32_t L, s;
+    uint32_t L, s;  // L = 0: no separators
+    uint32_t P;     // L + s
+    uint32_t T;     // the stream's interior slots (k_decode_lines)
+    uint32_t m, k;  // i / L == (i * m) >> (31 + k) for every i < 2^31
+    uint32_t rcp;   // ceil(2^20 / L): i / L == (i * rcp) >> 20 for i < 4,096
+    uint32_t pad;
 };
+static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of model");
 
 struct DecodeWs {
     uint64_t *lfail;     // ~(first failing slot) of k_decode_lines, 0 = none
@@ -1429,10 +1435,15 @@ constexpr uint32_t kLinesU = 2;                     // slots per lane
 constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
 constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
 
-DEV uint64_t line_pos(const LineModel m, uint64_t i)  // position of sextet i
+DEV uint64_t line_pos(const LineModel &m, uint64_t i)  // position of sextet i
 {
     if (m.L == 0) return i;
-    return i / m.L * (m.L + m.s) + i % m.L;
+    return i / m.L * m.P + i % m.L;
+}
+
+DEV uint32_t line_div(const LineModel &m, uint32_t i)  // i / L, i < 2^31
+{
+    return (uint32_t) (((uint64_t) i * m.m) >> (31 + m.k));
 }
 
 // One wave: the model from the first 256 bytes -- L = the first byte
@@ -1451,7 +1462,7 @@ DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n)
             if (tab[in[p + j]] < 64u) alpha |= 1u << j;
         }
     }
-    LineModel m{0, 0};
+    LineModel m{};
     const uint32_t junk = pres & ~alpha;
     const uint64_t bj = __ballot(junk != 0);
     if (!bj) return m;
@@ -1525,18 +1536,56 @@ DEV uint4 slot_chars(const uint32_t w[6], uint32_t o, uint32_t c, uint32_t s, ui
     return make_uint4(D[0], D[1], D[2], D[3]);
 }
 
-// One wave: the model into the workspace, for k_decode_lines (every block
-// reads it with one scalar load, instead of every block probing: 175 K
-// probes of the same 256 bytes cost 7 % of a 1 GiB decode) and
-// k_decode_suffix.
+// slot_chars for L % 4 == 0 (RFC 2045's 76, PEM's 64): a line end can only
+// fall on a dword boundary of the 16 characters (c = 4 c4), so the merge is
+// a dword select and the separator the c4-th funnel-shifted dword.
+DEV uint4 slot_chars4(const uint32_t w[6], uint32_t o, uint32_t c4, uint32_t s, uint32_t *sep)
+{
+    uint32_t A[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], o);
+    uint32_t D[4];
+    D[0] = A[0];  // c4 >= 1
+#pragma unroll
+    for (int j = 1; j < 4; j++) {
+        const uint32_t Bj = s >= 4 ? A[j + 1] : __builtin_amdgcn_alignbyte(A[j + 1], A[j], s);
+        D[j] = (uint32_t) j < c4 ? A[j] : Bj;
+    }
+    *sep = c4 == 1 ? A[1] : c4 == 2 ? A[2] : c4 == 3 ? A[3] : A[4];
+    return make_uint4(D[0], D[1], D[2], D[3]);
+}
+
+// One wave: the model, the stream's interior slot count T and the division
+// constants into the workspace, for k_decode_lines (every block reads them
+// with one scalar load instead of probing -- 175 K probes of the same 256
+// bytes cost 7 % of a 1 GiB decode -- and of computing T and L's
+// reciprocals: hundreds of scalar instructions per wave) and k_decode_suffix.
+// n <= 2^31 (the launcher's bound), so sextet indices and positions fit in
+// 32 bits.
 __global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
                                                      DecAlpha a, void *ws, uint32_t nranges)
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
     __syncthreads();
-    const LineModel m = probe_lines(tab, in, n);
-    if (threadIdx.x == 0) *ws_view(ws, nranges).model = m;
+    LineModel m = probe_lines(tab, in, n);
+    if (threadIdx.x != 0) return;
+    const uint32_t n32 = (uint32_t) n;
+    if (m.L == 0) {
+        m.T = n32 / 16;
+    } else {
+        m.P = m.L + m.s;
+        // T: the slots whose spans lie wholly inside the input -- those whose
+        // 16 characters are model positions below n, less the last one if a
+        // line ends right after it and its separator is cut off
+        const uint32_t F = n32 / m.P * m.L + (n32 % m.P < m.L ? n32 % m.P : m.L);
+        m.T = F / 16;
+        if (m.T && (16 * m.T) % m.L == 0 && (16 * m.T) / m.L * m.P > n32) m.T--;
+        m.k = 32 - __builtin_clz(m.L - 1);  // ceil(log2 L)
+        m.m = (uint32_t) ((((uint64_t) 1 << (31 + m.k)) + m.L - 1) / m.L);
+        m.rcp = ((1u << 20) + m.L - 1) / m.L;
+    }
+    *ws_view(ws, nranges).model = m;
 }
 
 __global__ __launch_bounds__(kThreads) void k_decode_lines(
@@ -1545,37 +1594,42 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
 {
     __shared__ uint8_t tab[256];
     __shared__ uint8_t s_tail[64];
-    // the scalar load of the model overlaps the table build
-    const uint64_t mw = scalar_load_u64((const uint64_t *) ws_view(ws, nranges).model);
+    // the scalar loads of the model overlap the table build
+    const uint64_t *mp = (const uint64_t *) ws_view(ws, nranges).model;
+    const uint64_t mw0 = scalar_load_u64(mp), mw1 = scalar_load_u64(mp + 1),
+                   mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
     build_dec_table(tab, a);
     __syncthreads();
+    LineModel m;
+    m.L = (uint32_t) mw0;
+    m.s = (uint32_t) (mw0 >> 32);
+    m.P = (uint32_t) mw1;
+    m.T = (uint32_t) (mw1 >> 32);
+    m.m = (uint32_t) mw2;
+    m.k = (uint32_t) (mw2 >> 32);
+    m.rcp = (uint32_t) mw3;
     const uint32_t lane = lane_id();
-    const uint32_t L = (uint32_t) mw;
-    const uint32_t s = (uint32_t) (mw >> 32);
-    const uint32_t P = L + s;
-    const LineModel m{L, s};
-    // n <= 2^31 (the launcher's bound), so sextet indices and positions fit
-    // in 32 bits.  T: the slots whose spans lie wholly inside the input.
-    const uint32_t n32 = (uint32_t) n;
-    uint32_t T;
-    if (L == 0) {
-        T = n32 / 16;
-    } else {
-        const uint32_t F = n32 / P * L + (n32 % P < L ? n32 % P : L);  // model alphabet positions
-        T = F / 16;
-        if (T && (16 * T) % L == 0 && (16 * T) / L * P > n32) T--;
-    }
+    const uint32_t L = m.L, s = m.s, P = m.P, T = m.T;
     const uint32_t t0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kLinesSlots;
     if (t0 > T) return;
     const uint32_t ns = T - t0 >= kLinesSlots ? kLinesSlots : T - t0;  // interior slots here
     const bool full = ns == kLinesSlots;
-    uint32_t fail_u = kLinesU, fail_lane = 0;  // the wave's first failing slot
     const bool oal = (((uintptr_t) out) & 3) == 0;
-    if (ns && L == 0 && full && oal && (((uintptr_t) in) & 3) == 0) {
+    const bool ial = (((uintptr_t) in) & 3) == 0;
+    uint32_t fail_u = kLinesU, fail_lane = 0;  // the wave's first failing slot
+    // line coordinates of the wave's first sextet
+    const uint32_t i0 = 16 * t0;
+    const uint32_t line0 = L ? line_div(m, i0) : 0;
+    const uint32_t col0 = i0 - line0 * L;
+    // the wave's windows all end inside the input (24 bytes from a dword at
+    // or below each span's start)
+    const bool safe = (uint64_t) (L ? line_div(m, i0 + 16 * ns) * P + (i0 + 16 * ns) % L
+                                    : i0 + 16 * ns) + 24 <= n;
+    if (ns && L == 0 && full && oal && ial) {
         // The hot path (clean input, a full wave, aligned buffers): lane t's
         // 16 characters are one non-temporal dwordx4 at 16t, its 12 bytes one
         // non-temporal dwordx3 at 12t -- pass 1's fast path, output-indexed.
-        // Kept apart from the general path below so that no load or store
+        // Kept apart from the general paths below so that no load or store
         // here is exec-masked (a masked form also lost the nt bit and waited
         // on every load at once: 7 % slower).
         uint4 c[kLinesU];
@@ -1592,67 +1646,83 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
             }
             emit_full_a4<true>(G, out + 12 * (uint64_t) (t0 + u * 64));
         }
+    } else if (ns && L != 0 && full && oal && ial && safe) {
+        // The hot path of line-structured text: 32-bit offsets from the
+        // input's base, unguarded window loads, non-temporal stores.
+        const bool a4 = (L & 3) == 0;
+        uint4 win[kLinesU];
+        uint2 wx[kLinesU];
+        uint32_t oo[kLinesU], cc[kLinesU];
+        bool hs[kLinesU];
+#pragma unroll
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            const uint32_t rel = col0 + 16 * (u * 64 + lane);
+            const uint32_t dl = (rel * m.rcp) >> 20;
+            const uint32_t col = rel - dl * L;
+            const uint32_t pos = (line0 + dl) * P + col;
+            hs[u] = L - col <= 16;  // a line ends in (or right after) the slot
+            cc[u] = hs[u] ? L - col : 16u;
+            oo[u] = pos & 3u;
+            const uint8_t *ab = in + (pos & ~3u);
+            win[u] = load16_a4(ab);
+            const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+            wx[u] = make_uint2(v.x, v.y);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+            uint32_t sep, G[4], bad;
+            const uint4 d = a4 ? slot_chars4(w6, oo[u], cc[u] >> 2, s, &sep)
+                               : slot_chars(w6, oo[u], cc[u], s, &sep);
+            map_fast(tab, d, 16, G, bad);
+            // the separator bytes of a line that ends here must all be
+            // outside the alphabet (looked up by every lane, kept by those)
+            uint32_t sep_alpha = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kLinesMaxS; k++)
+                if (k < s) sep_alpha |= tab[(sep >> (8 * k)) & 0xFFu] < 64u ? 1u : 0u;
+            if (hs[u]) bad |= sep_alpha << 8;
+            const uint64_t fb = __ballot(bad != 0);
+            if (fb && fail_u == kLinesU) {
+                fail_u = u;
+                fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
+            }
+            emit_full_a4<true>(G, out + 12 * (uint64_t) (t0 + u * 64));
+        }
     } else if (ns) {
+        // Everything else (a partial wave, the input's end, misaligned
+        // buffers): guarded window loads through 64-bit addresses.
         uint32_t G[kLinesU][4], bad[kLinesU];
-        if (L == 0 && (((uintptr_t) in) & 3) == 0) {
-            // clean model, aligned input, a partial wave
-            uint4 c[kLinesU];
+        const uint8_t *end = in + n;
+        uint4 win[kLinesU];
+        uint2 wx[kLinesU];
+        uint32_t oo[kLinesU], cc[kLinesU];
+        bool hs[kLinesU];
 #pragma unroll
-            for (uint32_t u = 0; u < kLinesU; u++) {
-                const uint8_t *p = in + 16 * (t0 + u * 64 + lane);
-                c[u] = u * 64 + lane < ns ? load16_a4(p) : make_uint4(0, 0, 0, 0);
-            }
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            const uint32_t rel = col0 + 16 * (u * 64 + lane);
+            const uint32_t dl = L ? (rel * m.rcp) >> 20 : 0;
+            const uint32_t col = rel - dl * L;
+            const uint32_t pos = L ? (line0 + dl) * P + col : i0 + 16 * (u * 64 + lane);
+            hs[u] = L && L - col <= 16;
+            cc[u] = hs[u] ? L - col : 16u;
+            const uint8_t *ap = in + pos;
+            const uint8_t *ab = (const uint8_t *) ((uintptr_t) ap & ~(uintptr_t) 3);
+            oo[u] = (uint32_t) (ap - ab);
+            const bool live = u * 64 + lane < ns;
+            win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
+            wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
+        }
 #pragma unroll
-            for (uint32_t u = 0; u < kLinesU; u++) map_fast(tab, c[u], 16, G[u], bad[u]);
-        } else {
-            // line coordinates of the wave's first sextet (scalar), then each
-            // lane's from a small offset (a 20-bit reciprocal, exact below 4,096)
-            const uint32_t i0 = 16 * t0;
-            const uint32_t line0 = L ? i0 / L : 0;
-            const uint32_t col0 = L ? i0 - line0 * L : 0;
-            const uint32_t rcp = L ? ((1u << 20) + L - 1) / L : 0;
-            const uint8_t *end = in + n;
-            // no window of this wave reaches past the input: unguarded loads
-            const uint64_t last_pos = L ? (uint64_t) ((i0 + 16 * ns) / L) * P + (i0 + 16 * ns) % L
-                                        : (uint64_t) i0 + 16 * ns;
-            const bool safe = last_pos + 40 <= n;
-            uint4 win[kLinesU];
-            uint2 wx[kLinesU];
-            uint32_t oo[kLinesU], cc[kLinesU];
-            bool hs[kLinesU];
+        for (uint32_t u = 0; u < kLinesU; u++) {
+            const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+            uint32_t sep;
+            const uint4 d = slot_chars(w6, oo[u], cc[u], s, &sep);
+            map_fast(tab, d, 16, G[u], bad[u]);
+            if (hs[u]) {
 #pragma unroll
-            for (uint32_t u = 0; u < kLinesU; u++) {
-                const uint32_t rel = col0 + 16 * (u * 64 + lane);
-                const uint32_t dl = L ? (uint32_t) (((uint64_t) rel * rcp) >> 20) : 0;
-                const uint32_t col = rel - dl * L;
-                const uint32_t pos = L ? (line0 + dl) * P + col : i0 + 16 * (u * 64 + lane);
-                hs[u] = L && L - col <= 16;  // a line ends in (or right after) the slot
-                cc[u] = hs[u] ? L - col : 16u;
-                const uint8_t *ap = in + pos;
-                const uint8_t *ab = (const uint8_t *) ((uintptr_t) ap & ~(uintptr_t) 3);
-                oo[u] = (uint32_t) (ap - ab);
-                if (safe) {
-                    win[u] = load16_a4(ab);
-                    const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
-                    wx[u] = make_uint2(v.x, v.y);
-                } else {
-                    const bool live = u * 64 + lane < ns;
-                    win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
-                    wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
-                }
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kLinesU; u++) {
-                const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
-                uint32_t sep;
-                const uint4 d = slot_chars(w6, oo[u], cc[u], s, &sep);
-                map_fast(tab, d, 16, G[u], bad[u]);
-                if (hs[u]) {
-                    // the line's separator bytes must all be outside the alphabet
-#pragma unroll
-                    for (uint32_t k = 0; k < kLinesMaxS; k++)
-                        if (k < s && tab[(sep >> (8 * k)) & 0xFFu] < 64u) bad[u] |= 0x100u;
-                }
+                for (uint32_t k = 0; k < kLinesMaxS; k++)
+                    if (k < s && tab[(sep >> (8 * k)) & 0xFFu] < 64u) bad[u] |= 0x100u;
             }
         }
 #pragma unroll
@@ -1663,13 +1733,10 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
                 fail_u = u;
                 fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
             }
-            uint8_t *o = out + 12 * (uint64_t) (t0 + u * 64);
-            if (oal && full) {
-                emit_full_a4<true>(G[u], o);
-            } else if (live) {
+            if (live) {
                 uint32_t o0, o1, o2;
                 groups_to_bytes(G[u][0], G[u][1], G[u][2], G[u][3], o0, o1, o2);
-                store_bytes12(o + 12 * lane, o0, o1, o2, 12);
+                store_bytes12(out + 12 * (uint64_t) (t0 + u * 64 + lane), o0, o1, o2, 12);
             }
         }
     }
