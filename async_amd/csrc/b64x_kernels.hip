@@ -2387,26 +2387,223 @@ DEV bool row_last_slot(const uint8_t *tab, uint4 w, const uint32_t A[4], uint32_
     return (m & (m + 1)) == 0;  // alphabet characters form a prefix
 }
 
-// Uniform-stride batch decode, second form (rows with room, out_stride >=
-// 12*S, every row): the block's first slot gives its row b0 and slot q0
-// once, each lane's slot is a 32-bit offset from there split with a 32-bit
-// multiply-high (magic = ceil(2^32/S), exact in range -- the launcher
-// checks).  Blocks clear of the last row store every slot unconditionally
-// (the last slot of a row over-writes past out_len inside its own row);
-// blocks that touch the last row ("tail", block-uniform) read page-safely
-// and store only decoded bytes, so one launch covers the batch.  Lengths
-// and marks go through atomicMax on the zeroed outlen[] as in
-// k_decode_slots.
-template <int U>
-__global__ __launch_bounds__(kThreads) void k_decode_rows2(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
-    uint8_t *__restrict__ out, uint64_t out_stride,
-    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t magic, uint64_t m64,
-    uint64_t nslots, uint64_t tail_slot, DecAlpha a)
+// ---- line-structured rows ---------------------------------------------------
+//
+// Uniform-stride batch decode of rows with room (out_stride >= 12 S), with
+// k_decode_lines' line model (MIME-formatted batches:
+// every row in 76-character lines with CRLF).  The model is probed from the
+// batch's first row by k_rows_prep (which also zeroes outlen[], replacing a
+// memset) and applies to every row; a row that does not follow it fails a
+// check and is marked for the fix-up, which decodes it exactly.  Row slot q
+// owns the row's sextets [16q, 16q + 16) and their span; slots before the
+// row's last are checked strictly (16 alphabet characters, separator bytes
+// outside the alphabet), the last one by the prefix rule of a padded or
+// unaligned end (its model positions: alphabet characters, then only
+// others; any trailing separator bytes outside the alphabet).
+struct RowModel {
+    uint32_t L, s, P, rcp;  // the line model; L = 0: clean rows (k_decode_rows2's path)
+    uint32_t S;             // slots per row under the model
+    uint32_t magic;         // ceil(2^32 / S), exact for the kernel's offsets
+    uint64_t m64;           // ceil(2^64 / S)
+    uint32_t F;             // model positions per row
+    uint32_t m, k;          // i / L == (i * m) >> (31 + k)
+    uint32_t pad;
+};
+static_assert(sizeof(RowModel) == 48, "RowModel layout");
+
+// The library workspace of the stream holds the model, in the region pass 1
+// uses for its per-range counts (scratch between calls).
+DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + 64); }
+
+constexpr uint32_t kRowsU = 4;  // slots per lane of the row kernels
+
+__global__ __launch_bounds__(kThreads) void k_rows_prep(
+    uint64_t *__restrict__ outlen, uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len,
+    uint64_t in_stride, DecAlpha a, void *ws)
 {
+    for (uint64_t i = (uint64_t) blockIdx.x * kThreads + threadIdx.x; i < nbuf;
+         i += (uint64_t) gridDim.x * kThreads)
+        outlen[i] = 0;
+    if (blockIdx.x != 0) return;
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
     __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const LineModel lm = probe_lines(tab, in, len);
+    if (threadIdx.x != 0) return;
+    RowModel r{};
+    const uint32_t L = lm.L, s = lm.s, P = L + s;
+    if (L) {
+        const uint32_t F = len / P * L + (len % P < L ? len % P : L);
+        const uint32_t S = (F + 15) / 16;
+        const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
+        const uint64_t e = (uint64_t) magic * S - (1ull << 32);
+        const uint64_t relmax = S + (uint64_t) kRowsU * kThreads;
+        // (rows of at least 32 bytes: a window never reads more than 24
+        // bytes past a row start beyond the next row's)
+        if (S >= 2 && len >= 32 && relmax * e < (1ull << 32) &&
+            (relmax / S + 1) * in_stride < (1ull << 40)) {
+            r.L = L;
+            r.s = s;
+            r.P = P;
+            r.rcp = ((1u << 20) + L - 1) / L;
+            r.S = S;
+            r.magic = magic;
+            r.m64 = ~0ull / S + 1;
+            r.F = F;
+            r.k = 32 - __builtin_clz(L - 1);
+            r.m = (uint32_t) ((((uint64_t) 1 << (31 + r.k)) + L - 1) / L);
+        }
+    }
+    *row_model(ws) = r;
+}
+
+// One slot of a line-structured row: its 16 model characters from the
+// window at its span, checked strictly (interior) or by the prefix rule
+// (the row's last slot, k model positions, nspan bytes of span); returns
+// whether it passes, G the groups (out-of-prefix characters zeroed), *j the
+// alphabet characters taken.
+DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w6[6], uint32_t o,
+                        uint32_t col, bool last, uint32_t k, uint32_t nspan, uint32_t G[4],
+                        uint32_t *j)
+{
+    const uint32_t L = rm.L, s = rm.s;
+    const bool hs = L - col <= 16;
+    const uint32_t c = hs ? L - col : 16u;
+    uint32_t sep;
+    const uint4 d = (L & 3) == 0 ? slot_chars4(w6, o, c >> 2, s, &sep)
+                                 : slot_chars(w6, o, c, s, &sep);
+    // separator bytes inside the span that must be outside the alphabet
+    const uint32_t nsep = !hs ? 0u : !last ? s : c > k ? 0u : (nspan - c < s ? nspan - c : s);
+    uint32_t sep_alpha = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kLinesMaxS; q++)
+        if (q < nsep) sep_alpha |= tab[(sep >> (8 * q)) & 0xFFu] < 64u ? 1u : 0u;
+    if (!last) {
+        uint32_t bad;
+        map_fast(tab, d, 16, G, bad);
+        *j = 16;
+        return bad == 0 && !sep_alpha;
+    }
+    LaneChunk lc;
+    map_chunk_lds(tab, d, k, lc);
+    const uint32_t mk = lc.vmask;
+#pragma unroll
+    for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+    *j = __popc(mk);
+    return (mk & (mk + 1)) == 0 && !sep_alpha;  // alphabet characters form a prefix
+}
+
+// The row kernel.  Clean rows (the model's L = 0): the block's first slot
+// gives its row b0 and slot q0 once, each lane's slot is a 32-bit offset
+// from there split with a 32-bit multiply-high (magic = ceil(2^32/S), exact
+// in range -- the launcher checks); lane slots load 16 characters and store
+// 12 bytes unconditionally (the last slot of a row over-writes past out_len
+// inside its own row; its length follows the prefix rule, row_last_slot).
+// Blocks that touch the last row ("tail", block-uniform) read page-safely
+// and store only decoded bytes, so one launch covers the batch.  Lengths and
+// marks go through atomicMax on the zeroed outlen[] as in k_decode_slots.
+// Line-structured rows: the same shape with the model's S, magic and m64,
+// and each slot's span (row_lines_slot).
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_decode_rows_lines(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
+    uint8_t *__restrict__ out, uint64_t out_stride,
+    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t magic, uint64_t m64,
+    uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws)
+{
+    __shared__ uint8_t tab[256];
+    const uint64_t *rmw = (const uint64_t *) row_model(ws);
+    const uint64_t r0 = scalar_load_u64(rmw);
+    build_dec_table(tab, a);
+    __syncthreads();
+    if ((uint32_t) r0 != 0) {
+        RowModel rm;
+        const uint64_t r1 = scalar_load_u64(rmw + 1), r2 = scalar_load_u64(rmw + 2),
+                       r3 = scalar_load_u64(rmw + 3), r4 = scalar_load_u64(rmw + 4),
+                       r5 = scalar_load_u64(rmw + 5);
+        rm.L = (uint32_t) r0;
+        rm.s = (uint32_t) (r0 >> 32);
+        rm.P = (uint32_t) r1;
+        rm.rcp = (uint32_t) (r1 >> 32);
+        rm.S = (uint32_t) r2;
+        rm.magic = (uint32_t) (r2 >> 32);
+        rm.m64 = r3;
+        rm.F = (uint32_t) r4;
+        rm.m = (uint32_t) (r4 >> 32);
+        rm.k = (uint32_t) r5;
+        const uint32_t Sm = rm.S;
+        const uint64_t ns_m = (uint64_t) Sm * nbuf;
+        const uint64_t tail_m = (uint64_t) Sm * (nbuf - 1);
+        const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
+        if (s0 >= ns_m) return;
+        const uint64_t b0 = __umul64hi(s0, rm.m64);
+        const uint32_t q0 = (uint32_t) (s0 - b0 * Sm);
+        const uint8_t *ib = in + b0 * in_stride;
+        uint8_t *ob = out + b0 * out_stride;
+        unsigned long long *olb = outlen + b0;
+        const bool tail = s0 + U * kThreads > tail_m;
+        const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
+        uint32_t bl[U], qq[U], oo[U], cl[U], pp[U];
+        uint4 win[U];
+        uint2 wx[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t rel = q0 + u * kThreads + threadIdx.x;
+            bl[u] = __umulhi(rel, rm.magic);
+            qq[u] = rel - bl[u] * Sm;
+            const uint32_t i = 16 * qq[u];
+            const uint32_t dl = (uint32_t) (((uint64_t) i * rm.m) >> (31 + rm.k));
+            cl[u] = i - dl * rm.L;
+            const uint32_t pos = dl * rm.P + cl[u];
+            pp[u] = pos;
+            oo[u] = pos & 3u;
+            const uint8_t *ab = ib + (uint64_t) bl[u] * in_stride + (pos & ~3u);
+            if (!tail) {
+                win[u] = load16_a4(ab);
+                const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+                wx[u] = make_uint2(v.x, v.y);
+            } else {
+                const bool live = s0 + u * kThreads + threadIdx.x < ns_m;
+                win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
+                wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t q = qq[u];
+            const bool last = q == Sm - 1;
+            const uint32_t i = 16 * q;
+            const uint32_t k = last ? rm.F - i : 16u;
+            const uint32_t pos = pp[u];
+            const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+            uint32_t G[4], j;
+            const bool ok = row_lines_slot(tab, rm, w6, oo[u], cl[u], last, k, len - pos, G, &j);
+            uint32_t o0, o1, o2;
+            groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+            uint8_t *dst = ob + (uint64_t) bl[u] * out_stride + 12 * q;
+            unsigned long long *ol = olb + bl[u];
+            const bool live = !tail || s0 + u * kThreads + threadIdx.x < ns_m;
+            if (!tail) {
+                __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+            } else if (live && ok) {
+                store_bytes12(dst, o0, o1, o2, last ? 3 * (j >> 2) + ((6 * (j & 3)) >> 3) : 12u);
+            }
+            const uint64_t junk = __ballot(live && !ok);
+            const uint32_t ln = lane_id();
+            const uint32_t rs = q < ln ? ln - q : 0u;
+            const uint64_t row_junk = junk & (~0ull << rs);
+            const bool marker = live && !ok && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln;
+            if (!live) {
+            } else if (!ok) {
+                if (marker) atomicMax(ol, (unsigned long long) kNeedsExact);
+            } else if (last) {
+                atomicMax(ol, (unsigned long long) ((16ull * q + j) * 6 / 8));
+            }
+        }
+        return;
+    }
+    // clean rows: k_decode_rows2's body
     const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
     const uint64_t b0 = __umul64hi(s0, m64);
     const uint32_t q0 = (uint32_t) (s0 - b0 * S);
@@ -2464,10 +2661,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows2(
         __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
                                     (u32x3a4 *) (ob + (uint64_t) bl[u] * out_stride + 12 * q));
         unsigned long long *ol = olb + bl[u];
-        // A row's slots sit on consecutive lanes (its first here at lane -
-        // q, or lane 0): only the first junk slot of each row in the wave
-        // marks it -- on MIME-formatted rows (CRLF every 76) that is one
-        // atomic per row and wave instead of one per junk slot.
+        // only the first junk slot of each row in the wave marks it
         const uint64_t junk = __ballot(!ok);
         const uint32_t ln = lane_id();
         const uint32_t rs = q < ln ? ln - q : 0u;
@@ -3056,31 +3250,42 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (!d) return -ENODEV;
     hipStream_t s = (hipStream_t) stream;
     const DecAlpha a = dec_alpha(abc);
-    int err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s));
-    if (err) return err;
     const bool rows = nbuf >= 2 && S >= 2 && out_stride >= 12 * S && (in_stride & 3) == 0 &&
                       (out_stride & 3) == 0 && (((uintptr_t) d_in) & 3) == 0 &&
                       (((uintptr_t) d_out) & 3) == 0;
     bool done = false;
+    int err = 0;
     if (rows && S < (1u << 20)) {
-        // rows with room, one launch (k_decode_rows2)
-        constexpr uint32_t U = 4;
+        // rows with room, one launch after the prep (k_rows_prep zeroes
+        // outlen[] and probes the line model from row 0; k_decode_rows_lines
+        // takes clean rows by k_decode_rows2's path and MIME-formatted rows by
+        // the model)
+        constexpr uint32_t U = kRowsU;
         const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
         const uint64_t e = (uint64_t) magic * S - (1ull << 32);
         const uint64_t relmax = S + (uint64_t) U * kThreads;
-        if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40)) {
+        void *ws = nullptr;
+        if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40) &&
+            (ws = library_workspace(stream, &err))) {
             const uint64_t m64 = ~0ull / S + 1;
             const uint64_t per = (uint64_t) U * kThreads;
             const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
+            hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nbuf + kThreads - 1) / kThreads, (uint64_t) d->cus * 4)),
+                               dim3(kThreads), 0, s, d_outlen, nbuf, (const uint8_t *) d_in,
+                               (uint32_t) len, in_stride, a, ws);
+            if ((err = launch_status())) return err;
             const dim3 g((uint32_t) ((slots + per - 1) / per));
-            hipLaunchKernelGGL(k_decode_rows2<U>, g, dim3(kThreads), 0, s, (const uint8_t *) d_in,
-                               in_stride, (uint32_t) len, (uint8_t *) d_out, out_stride,
-                               (unsigned long long *) d_outlen, (uint32_t) S, magic, m64, slots,
-                               tail_slot, a);
+            hipLaunchKernelGGL(k_decode_rows_lines<U>, g, dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, in_stride, (uint32_t) len, (uint8_t *) d_out,
+                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, magic, m64,
+                               slots, tail_slot, a, nbuf, ws);
             if ((err = launch_status())) return err;
             done = true;
+        } else if (err) {
+            return err;
         }
     }
+    if (!done && (err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s)))) return err;
     if (!done && slots) {
         // any other layout: one lane per (buffer, 16-character slot)
         constexpr int U = 2;

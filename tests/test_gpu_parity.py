@@ -635,3 +635,83 @@ def test_single_pass_decode_structured_and_alphabets():
         chars = orc.encode(rng.integers(0, 256, 100_000 + k, dtype=np.uint8))
         d = b"\r\n".join(chars[i:i + 76] for i in range(0, len(chars), 76))
         assert (gdec_j(d) if k % 2 else gdec(d))[0] == orc.decode(d)
+
+
+def _wrap(chars: bytes, L: int, sep: bytes, trailing=True) -> bytes:
+    lines = [chars[i:i + L] for i in range(0, len(chars), L)]
+    return sep.join(lines) + (sep if trailing and lines else b"")
+
+
+@pytest.mark.parametrize("L,sep", [(76, b"\r\n"), (64, b"\n"), (16, b"\r\n"), (20, b"\n\n\n\n"),
+                                   (17, b"\n"), (19, b"\r\n\n"), (252, b"\n"), (253, b"\n")])
+def test_decode_lines_shapes_vs_oracle(L, sep):
+    """The line-structured single pass (k_decode_lines) and its suffix decode
+    on many stream lengths around slot, line and window boundaries: with and
+    without a trailing separator, padded or not, HOLD_TAIL, input and output
+    at every alignment, and a stream that breaks the model once (a short
+    line, an '=' inside, a junk byte) -- every result against the oracle."""
+    rng = np.random.default_rng(L * 7 + len(sep))
+    for n in (0, 1, 2, 11, 12, 13, 47, 48, 300, 1001, 4096, 40_000):
+        host = rng.integers(0, 256, n, dtype=np.uint8)
+        chars = orc.encode(host)
+        for trailing in (True, False):
+            text = _wrap(chars, L, sep, trailing)
+            variants = [text]
+            if len(text) > 3 * (L + len(sep)):
+                k = (len(text) // (L + len(sep)) // 2) * (L + len(sep))
+                variants += [text[:k + 10] + text[k + 11:],          # one short line
+                             text[:k + 5] + b"=" + text[k + 6:],     # '=' at a model position
+                             text[:k + L] + b"\t" + text[k + L:]]    # one more separator byte
+            for v in variants:
+                want = orc.decode(v)
+                got, info = gdec(v)
+                assert got == want, (n, trailing, len(v))
+                gh, ih = gdec(v, hold=True)
+                assert ih.out_len == 3 * (ih.valid // 4) and ih.valid == info.valid
+                assert gh == want[:ih.out_len]
+    # alignment of input and output (decode into a slice of a larger buffer)
+    host = rng.integers(0, 256, 20_000, dtype=np.uint8)
+    text = _wrap(orc.encode(host), L, sep)
+    want = orc.decode(text)
+    for off in range(4):
+        xs = dev(bytes(off) + text)[off:]  # the text at offset `off` of a fresh buffer
+        outbuf = torch.empty(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+        d = b64.decode(xs, out=outbuf[off:], abc=(-1, -1, True, -1))
+        got = d.bytes().cpu().numpy().tobytes()
+        assert got == want, off
+
+
+def _mime_batch(nbuf, n, L, sep, rng, deviants=()):
+    rows = []
+    for i in range(nbuf):
+        c = orc.encode(rng.integers(0, 256, n, dtype=np.uint8))
+        t = _wrap(c, L, sep)
+        if i in deviants:
+            t = t[:7] + b"\t" + t[7:] if deviants[i] == "junk" else _wrap(c, L + 4, sep)
+        rows.append(t)
+    return rows
+
+
+@pytest.mark.parametrize("n,L,sep", [(1024, 76, b"\r\n"), (4096, 76, b"\r\n"), (1000, 64, b"\n"),
+                                     (777, 76, b"\r\n"), (3000, 19, b"\n"), (100, 16, b"\n\n")])
+def test_strided_mime_rows_vs_oracle(n, L, sep):
+    """MIME-formatted uniform batches (k_rows_prep's line model from row 0,
+    k_decode_rows_lines): every row against the oracle, including rows that
+    do not follow row 0's model (a junk byte, other line lengths) and so go
+    to the exact fix-up."""
+    rng = np.random.default_rng(n + L)
+    nbuf = 300
+    rows = _mime_batch(nbuf, n, L, sep, rng, deviants={3: "junk", 150: "len", nbuf - 1: "junk"})
+    stride = max(len(r) for r in rows)
+    flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
+    x = dev(flat)
+    cap = (b64.decoded_cap(stride) + 15) // 16 * 16
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen)
+    ol = outlen.cpu().tolist()
+    dh = dec.cpu().numpy()
+    for i, r in enumerate(rows):
+        want = orc.decode(r + b"\n" * (stride - len(r)))
+        assert ol[i] == len(want), i
+        assert dh[i * cap:i * cap + ol[i]].tobytes() == want, i
