@@ -1623,8 +1623,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
     const uint32_t col0 = i0 - line0 * L;
     // the wave's windows all end inside the input (24 bytes from a dword at
     // or below each span's start)
-    const bool safe = (uint64_t) (L ? line_div(m, i0 + 16 * ns) * P + (i0 + 16 * ns) % L
-                                    : i0 + 16 * ns) + 24 <= n;
+    const uint32_t ie = i0 + 16 * ns, le = L ? line_div(m, ie) : 0;
+    const bool safe = (uint64_t) (L ? le * P + (ie - le * L) : ie) + 24 <= n;
     if (ns && L == 0 && full && oal && ial) {
         // The hot path (clean input, a full wave, aligned buffers): lane t's
         // 16 characters are one non-temporal dwordx4 at 16t, its 12 bytes one

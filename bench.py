@@ -24,6 +24,8 @@ Also reported on the same JSON line:
                 the ranks by index range, strided encode + decode, plus the
                 one exchange step (allgather of per-rank output totals);
                 whole-job and per-rank GiB/s and roofline fractions;
+  mime_decode   MIME-formatted (CRLF-76) decode of config 2's characters and
+                config 4's rows, bit-checked (rank 0 at N=1);
   host_inclusive  the same 1 GiB round trip starting and ending in pinned
                 host memory (rank 0): the kernels read and write the pinned
                 buffers in place over PCIe (the sessions' zero-copy path),
@@ -53,7 +55,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s base64 encode+decode, device-resident, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ROUND = "r01"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
+ROUND = "r02"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
 
 
 def parse():
@@ -74,6 +76,7 @@ def parse():
     ap.add_argument("--no-batch", action="store_true")
     ap.add_argument("--batch-steps", type=int, default=20)
     ap.add_argument("--no-host", action="store_true", help="skip the host_inclusive leg")
+    ap.add_argument("--no-mime", action="store_true", help="skip the mime_decode leg")
     ap.add_argument("--host-block", type=int, default=24 << 20,
                     help="bytes per block of the host_inclusive leg (a multiple of 3)")
     ap.add_argument("--host-streams", type=int, default=4)
@@ -363,6 +366,91 @@ def bench_host_inclusive(args, b64):
     return out
 
 
+def crlf76(chars: torch.Tensor) -> torch.Tensor:
+    """RFC 2045 formatting on the device: 76-character lines, each followed
+    by CRLF (the last, shorter one too)."""
+    n = chars.numel()
+    rows = (n + 75) // 76
+    pad = rows * 76 - n
+    body = torch.cat([chars, torch.zeros(pad, dtype=torch.uint8, device=chars.device)])
+    crlf = torch.tensor([13, 10], dtype=torch.uint8, device=chars.device).expand(rows, 2)
+    out = torch.cat([body.view(rows, 76), crlf], dim=1).reshape(-1)
+    if pad:  # drop the zero padding of the last line (keep its CRLF)
+        keep = torch.ones(out.numel(), dtype=torch.bool, device=chars.device)
+        start = (rows - 1) * 78 + (76 - pad)
+        keep[start:start + pad] = False
+        out = out[keep]
+    return out.contiguous()
+
+
+def bench_mime(args, b64, steps=10):
+    """MIME-formatted decode (SURVEY.md §8(d) dirty input): config 2's
+    characters and config 4's rows in 76-character CRLF lines, decoded back
+    and checked; device-resident, HIP events around each call.  Algorithmic
+    bytes = characters read + bytes written."""
+    N = args.size
+    x = torch.empty(N, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    text = crlf76(b64.encode(x))
+    out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device="cuda")
+    res = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return statistics.median(ts)
+
+    ms = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream))
+    info = b64.Decoded(out, res).info()
+    if info.out_len != N or not torch.equal(out[:N], x):
+        raise SystemExit("mime decode mismatch")
+    alg = text.numel() + N
+    single = {"workload": f"cfg2 characters in CRLF-76 lines: {text.numel()} bytes -> {N}",
+              "ms": ms, "GiB_s": N / (ms * 1e-3) / 2**30,
+              "alg_GBps": alg / (ms * 1e-3) / 1e9,
+              "roofline_frac": alg / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9)}
+    del x, text, out, ws
+    # config 4's rows, each in CRLF-76 lines (1,368 characters -> 18 lines)
+    nbuf, L = 1 << 20, 1024
+    E = b64.encoded_len(L)
+    xr = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(xr, 0x5EED)
+    enc = torch.empty(nbuf * E, dtype=torch.uint8, device="cuda")
+    b64.encode_strided(xr, L, L, nbuf, enc, E, stream=stream)
+    lines = (E + 75) // 76
+    rows = enc.view(nbuf, E)
+    if lines * 76 != E:
+        rows = torch.cat([rows, torch.full((nbuf, lines * 76 - E), 10, dtype=torch.uint8,
+                                           device="cuda")], dim=1)
+    crlf = torch.tensor([13, 10], dtype=torch.uint8, device="cuda").expand(nbuf, lines, 2)
+    D = lines * 78
+    mime = torch.cat([rows.reshape(nbuf, lines, 76), crlf], dim=2).reshape(-1).contiguous()
+    del enc, rows
+    cap = 12 * ((D + 15) // 16)
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device="cuda")
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device="cuda")
+    ms4 = timed(lambda: b64.decode_strided(mime, D, D, nbuf, dec, cap, outlen, stream=stream))
+    if not (bool((outlen == L).all()) and
+            bool(torch.equal(dec.view(nbuf, cap)[:, :L], xr.view(nbuf, L)))):
+        raise SystemExit("mime batch decode mismatch")
+    alg4 = nbuf * (D + L)
+    batch = {"workload": f"cfg4 rows in CRLF-76 lines: {nbuf} x {D} bytes -> {L}",
+             "ms": ms4, "GiB_s": nbuf * L / (ms4 * 1e-3) / 2**30,
+             "alg_GBps": alg4 / (ms4 * 1e-3) / 1e9,
+             "roofline_frac": alg4 / (ms4 * 1e-3) / (HBM_PEAK_GBS * 1e9)}
+    return {"cfg2_crlf76": single, "cfg4_crlf76": batch, "unit": "ms, GiB/s payload"}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -504,6 +592,9 @@ def main():
     host = None
     if rank == 0 and not args.no_host:
         host = bench_host_inclusive(args, b64)
+    mime = None
+    if rank == 0 and world == 1 and not args.no_mime and args.size == 1 << 30:
+        mime = bench_mime(args, b64)
 
     if rank == 0:
         N, E, K = r["N"], r["E"], r["K"]
@@ -512,7 +603,7 @@ def main():
         dom_ms = max(r["enc_ms"], r["dec_ms"])
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         knames = ["k_encode_flat"] if dom == "encode" else \
-            ["k_decode_pass1", "k_decode_scan2", "k_decode_pass2d"]
+            ["k_decode_probe", "k_decode_lines", "k_decode_suffix"]
         out = {
             "metric": METRIC,
             "value": world * N * K / r["wall"] / 2**30,
@@ -557,6 +648,7 @@ def main():
             "cpu_baseline": cpu,
             "batch_cfg4": batch,
             "host_inclusive": host,
+            "mime_decode": mime,
             "process_group": {"backend": dist.get_backend() if world > 1 else None,
                               "world_size": dist.get_world_size() if world > 1 else 1},
         }

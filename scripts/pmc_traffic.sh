@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/$c" -o run \
-      -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --batch-steps 3 > "$OUT/$c.log" 2>&1
+      -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-host --no-mime --batch-steps 3 > "$OUT/$c.log" 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 exit 0

@@ -13,7 +13,7 @@ import sys
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out", "pmc_traffic")
-rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r02"
 vals = collections.defaultdict(dict)
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     per = collections.defaultdict(list)
@@ -36,13 +36,14 @@ for k, v in vals.items():
                   "hbm_bytes_per_launch": fetch + write,
                   "raw_FETCH_SIZE_KiB": v["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": v["WRITE_SIZE"]}
 # short aliases for the config-2 kernels bench.py names
-for alias in ("k_encode_flat", "k_decode_pass1"):
+for alias in ("k_encode_flat", "k_decode_pass1", "k_decode_lines", "k_decode_probe",
+              "k_decode_suffix", "k_encode_tight2", "k_decode_rows_lines", "k_rows_prep"):
     cands = sorted((k for k in kernels if k.startswith(alias + "@")),
                    key=lambda k: -kernels[k]["hbm_bytes_per_launch"])
     if cands:
         kernels[alias] = kernels[cands[0]]
 out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
-                 "`bench.py --steps 5 --warmup 1 --no-cpu --batch-steps 3`",
+                 "`bench.py --steps 5 --warmup 1 --no-cpu --no-host --no-mime --batch-steps 3`",
        "corrections": "fetch = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB",
        "kernels": kernels}
 dst = os.path.join(root, "profiles", f"pmc_{rnd}.json")
