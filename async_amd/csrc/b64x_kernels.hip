@@ -17,23 +17,26 @@
 //     regrouping is v_perm_b32, not shifts (k_encode_flat; batches:
 //     k_encode_tight2, k_encode_strided, k_encode_ragged).
 //   * decode is stateful only through the number of alphabet characters
-//     seen so far.  The input is cut into ranges of 2,048 characters, one
-//     wave each.  k_decode_pass1 assumes every earlier range was all
-//     alphabet (true for clean input): it decodes fast-path chunks straight
-//     to their final place, records each range's alphabet count and
-//     publishes the first chunk that is not fast-path.  k_decode_scan2 (a
-//     single-pass decoupled look-back over tiles of 1,024 ranges) turns the
-//     counts into each range's true base when that happened; clean input
-//     exits there.  k_decode_pass2d re-runs the ranges from the first dirty
-//     chunk on: per dword a v_perm compaction of the alphabet bytes, v_dot4
-//     into a left-aligned sextet field, ds_or into the wave's LDS window at
-//     bit 6 x (sextet index) -- the window's bytes are the output bytes --
-//     and a straight copy out.  B64X_DEC_EXPECT_JUNK selects the one-pass
-//     form of the same range body (k_decode_pass2d_t<true>).
-//   * batches: the row kernels (k_decode_rows2 for rows with room) take the
-//     fast paths lane by lane and mark rows with junk once per wave; the
-//     fix-up (k_decode_batch_fix2) decodes the marked rows with pass 2d's
-//     bit-stream step, one wave per row.
+//     seen so far.  For inputs up to 2^31 characters: k_decode_probe (one
+//     wave) reads the stream's first 256 bytes for a line model -- lines of
+//     L alphabet characters and s separator bytes, L = 0 for clean input --
+//     under which every character's output place is known in closed form;
+//     k_decode_lines is output-indexed (lane slot t = sextets [16t, 16t+16)
+//     = output bytes [12t, 12t+12)), loads each slot's span, drops the
+//     separator with funnel shifts, checks it and stores 12 bytes, and
+//     publishes the first slot that does not fit the model;
+//     k_decode_suffix decodes exactly whatever follows that slot (nothing,
+//     on clean and MIME-formatted text): persistent tiles of 64 ranges of
+//     2,048 characters, counts, a decoupled look-back, and the range body
+//     that ORs each lane's compacted sextet fields into a wave's LDS window
+//     (v_perm compaction, v_dot4 fields, ds_or) -- the window's bytes are
+//     the output bytes.  Larger inputs: pass 1 (input-indexed fast paths),
+//     a scan, pass 2 with the same range body.
+//   * batches: the row kernel (k_decode_rows_lines, rows with room) takes
+//     clean rows lane by lane and MIME-formatted rows by the same line
+//     model (k_rows_prep probes row 0), and marks rows with junk once per
+//     wave; the fix-up (k_decode_batch_fix2) decodes the marked rows with
+//     the bit-stream range body, one wave per row.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
