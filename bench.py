@@ -26,6 +26,9 @@ Also reported on the same JSON line:
                 whole-job and per-rank GiB/s and roofline fractions;
   mime_decode   MIME-formatted (CRLF-76) decode of config 2's characters and
                 config 4's rows, bit-checked (rank 0 at N=1);
+  cfg5_egress   BASELINE config 5 through the product's stage stack, host
+                memory in and out, 1 and 16 loops, with the oracle's stack
+                timed beside it (rank 0 at N=1; skipped with --no-cpu);
   host_inclusive  the same 1 GiB round trip starting and ending in pinned
                 host memory (rank 0): the kernels read and write the pinned
                 buffers in place over PCIe (the sessions' zero-copy path),
@@ -77,6 +80,7 @@ def parse():
     ap.add_argument("--batch-steps", type=int, default=20)
     ap.add_argument("--no-host", action="store_true", help="skip the host_inclusive leg")
     ap.add_argument("--no-mime", action="store_true", help="skip the mime_decode leg")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5_egress leg")
     ap.add_argument("--host-block", type=int, default=24 << 20,
                     help="bytes per block of the host_inclusive leg (a multiple of 3)")
     ap.add_argument("--host-streams", type=int, default=4)
@@ -451,6 +455,62 @@ def bench_mime(args, b64, steps=10):
     return {"cfg2_crlf76": single, "cfg4_crlf76": batch, "unit": "ms, GiB/s payload"}
 
 
+def bench_cfg5(args):
+    """BASELINE config 5 on this GPU: 16,384 Zipf messages (64 B - 1 MiB,
+    SURVEY.md §8(d)), each its own queuestream -> GPU base64encoder stage ->
+    chunkencoder(1 MiB) stack of the product's C API, drained 10,240 bytes
+    per read (the reference's tcp_connection.c:22 pull size); host memory in,
+    framed host memory out, so the rate includes every pinned copy and PCIe
+    crossing.  T event loops (threads, one batching hub each) share the
+    messages; T = 1 and 16 (the box's CPU share).  Beside it, the oracle's
+    restatement of the same stack on the same thread counts, whose outputs
+    check a sample of the GPU stacks' (cpu_baseline's checker role)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    from oracle import pyoracle as orc
+    from tests import util
+
+    lens = util.zipf_lengths()
+    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    nbytes = int(lens.sum())
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
+    out = {"workload": f"cfg5: {lens.size} Zipf messages, {nbytes} bytes, "
+                       "queuestream -> encoder -> chunkencoder(1 MiB), 10,240-byte reads",
+           "unit": "GiB/s of payload, host memory to host memory"}
+    sample = list(range(0, lens.size, lens.size // 64))
+    for T in (1, min(16, args.cpu_threads)):
+        times = np.zeros(2)
+        res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times, raw=True,
+                                      threads=T)
+        if res is None:
+            raise SystemExit(f"cfg5 egress failed: errno {err}")
+        framed, f_off, f_len = res
+        dt = float(times.sum())
+
+        def work(t, T=T):
+            cuts = np.searchsorted(offs, np.linspace(0, nbytes, T + 1))
+            for i in range(cuts[t], cuts[t + 1]):
+                orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
+                                   read_size=10240)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(T) as ex:
+            list(ex.map(work, range(T)))
+        cpu_dt = time.perf_counter() - t0
+        for i in sample:
+            want = orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
+                                      read_size=10240)
+            if framed[int(f_off[i]):int(f_off[i]) + int(f_len[i])].tobytes() != want:
+                raise SystemExit(f"cfg5 egress mismatch at message {i}")
+        out[f"loops_{T}"] = {"GiB_s": nbytes / dt / 2**30, "seconds": dt,
+                             "framed_bytes": int(f_len.sum()),
+                             "cpu_port_GiB_s": nbytes / cpu_dt / 2**30, "cpu_threads": T}
+        del framed, res
+    return out
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -595,6 +655,9 @@ def main():
     mime = None
     if rank == 0 and world == 1 and not args.no_mime and args.size == 1 << 30:
         mime = bench_mime(args, b64)
+    cfg5 = None
+    if rank == 0 and world == 1 and not args.no_cfg5 and not args.no_cpu:
+        cfg5 = bench_cfg5(args)
 
     if rank == 0:
         N, E, K = r["N"], r["E"], r["K"]
@@ -649,6 +712,7 @@ def main():
             "batch_cfg4": batch,
             "host_inclusive": host,
             "mime_decode": mime,
+            "cfg5_egress": cfg5,
             "process_group": {"backend": dist.get_backend() if world > 1 else None,
                               "world_size": dist.get_world_size() if world > 1 else 1},
         }
