@@ -11,7 +11,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 B="$ROOT/build_asan"
 if [ ! -f "$B/async_amd/libasync_b64.so" ] || [ -n "$(find "$ROOT/async_amd/csrc" "$ROOT/include" "$ROOT/tests/csrc" -newer "$B/async_amd/libasync_b64.so" -name '*.[ch]*' | head -1)" ]; then
   rm -rf "$B" && mkdir -p "$B"
-  cp -r "$ROOT/include" "$ROOT/async_amd" "$ROOT/tests" "$ROOT/oracle" "$ROOT/Makefile" "$B/"
+  cp -r "$ROOT/include" "$ROOT/async_amd" "$ROOT/tests" "$ROOT/oracle" "$ROOT/Makefile" "$ROOT/INTEGRATION.md" "$ROOT/bench.py" "$B/"
   rm -rf "$B/build" "$B"/async_amd/*.so "$B"/oracle/*.so "$B"/tests/csrc/*.so
   sed -i 's/^CFLAGS    = -O2 /CFLAGS    = -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer /' "$B/Makefile"
   make -C "$B" -j8 >/dev/null
