@@ -787,9 +787,17 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //   status  per scan tile: flag (bits 63..62: 1 aggregate, 2 inclusive
 //           prefix; 0 = not yet) | value, for the scan's decoupled
 //           look-back; zero between calls (the scan's last tile clears it)
-//   lfail   ~(first failing slot) of k_decode_lines, 0 = none (cleared by
-//           k_decode_suffix); model: the line model it used
+//   lfail   kFailWords words, kFailStride apart (one per 128-byte line):
+//           ~(first failing slot) of k_decode_lines, published by each wave
+//           into word (block mod kFailWords) so that failing waves do not all
+//           read one line; 0 = none (cleared by k_decode_suffix)
+//   model   the line model k_decode_probe found, for k_decode_lines and
+//           k_decode_suffix
 //   fticket, fstatus  k_decode_suffix's tile ticket and status words
+// The regions that must be zero between calls (status, fstatus, lfail) sit
+// at fixed offsets after the header, sized for the largest plan, so calls of
+// different sizes on one workspace never find another call's scratch
+// (counts, bases) where they expect zeros.
 // The line model of k_decode_lines (see there): lines of L alphabet
 // characters, each followed by s separator bytes; L = 0: no separators.
 struct LineModel {
@@ -798,12 +806,12 @@ struct LineModel {
     uint32_t T;     // the stream's interior slots (k_decode_lines)
     uint32_t m, k;  // i / L == (i * m) >> (31 + k) for every i < 2^31
     uint32_t rcp;   // ceil(2^20 / L): i / L == (i * rcp) >> 20 for i < 4,096
-    uint32_t pad;
+    uint32_t skip;  // 1: k_decode_probe already published slot T as failing (no tail)
 };
 static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of model");
 
 struct DecodeWs {
-    uint64_t *lfail;     // ~(first failing slot) of k_decode_lines, 0 = none
+    uint64_t *lfail;     // kFailWords words, kFailStride apart
     LineModel *model;    // k_decode_lines' model, for k_decode_suffix
     uint64_t *fd;
     uint64_t *fd_cur;
@@ -820,7 +828,15 @@ constexpr uint32_t kFusePer = 16;     // ranges per wave in the single-pass deco
 constexpr uint32_t kFuseLoad = 4;     // of them loaded at once for counting
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
-// Layout for `nranges` ranges: 64-byte header, counts, bases, tile status.
+constexpr uint32_t kFailWords = 64, kFailStride = 16;
+constexpr uint64_t kWsStatus = 64;                                        // scan tile status
+constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
+constexpr uint64_t kWsFail = kWsFStatus + kMaxRanges / kFuseTile * 8;     // lines failures
+constexpr uint64_t kWsScratch = kWsFail + kFailWords * kFailStride * 8;   // counts, bases
+
+// Layout: 64-byte header (fd, fd_cur, ticket, fticket, model), the
+// zero-between-calls regions at fixed offsets, then the scratch counts and
+// bases of `nranges` ranges.
 DEV DecodeWs ws_view(void *ws, uint32_t nranges)
 {
     DecodeWs w;
@@ -828,13 +844,13 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.fd = (uint64_t *) p;
     w.fd_cur = (uint64_t *) (p + 8);
     w.ticket = (uint32_t *) (p + 16);
-    w.counts = (uint32_t *) (p + 64);
-    w.bases = (uint64_t *) (p + 64 + ((uint64_t) nranges * 4 + 7) / 8 * 8);
-    w.status = w.bases + nranges;
-    w.fstatus = w.status + (nranges + kScanTile - 1) / kScanTile;
     w.fticket = (uint32_t *) (p + 20);
-    w.lfail = (uint64_t *) (p + 24);
     w.model = (LineModel *) (p + 32);
+    w.status = (uint64_t *) (p + kWsStatus);
+    w.fstatus = (uint64_t *) (p + kWsFStatus);
+    w.lfail = (uint64_t *) (p + kWsFail);
+    w.counts = (uint32_t *) (p + kWsScratch);
+    w.bases = (uint64_t *) (p + kWsScratch + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     return w;
 }
 
@@ -1453,7 +1469,8 @@ DEV uint32_t line_div(const LineModel &m, uint32_t i)  // i / L, i < 2^31
 // outside the alphabet, s = the run of such bytes after it.  Anything that
 // does not look like lines (L < 16 or > kLinesMaxL, s > kLinesMaxS, no
 // alphabet after the first run) gives the clean model.
-DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n)
+DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n,
+                          uint32_t *first_junk = nullptr)
 {
     const uint32_t lane = lane_id();
     const uint32_t p = 4 * lane;
@@ -1472,6 +1489,7 @@ DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n)
     const uint32_t lj = (uint32_t) __ffsll((unsigned long long) bj) - 1;
     const uint32_t L = 4 * lj + (uint32_t) __builtin_ctz(
                                     (uint32_t) __builtin_amdgcn_readlane((int) junk, (int) lj));
+    if (first_junk) *first_junk = L;
     // the first alphabet byte after L
     const uint32_t gt = p > L ? 0xFu : (p + 4 <= L + 1 ? 0u : (0xFu << (L + 1 - p)) & 0xFu);
     const uint32_t am = alpha & gt;
@@ -1482,6 +1500,13 @@ DEV LineModel probe_lines(const uint8_t *tab, const uint8_t *in, uint64_t n)
                                     (uint32_t) __builtin_amdgcn_readlane((int) am, (int) la));
     const uint32_t s = P - L;
     if (L < 16 || L > kLinesMaxL || s > kLinesMaxS) return m;
+    // the whole window must follow the model (unstructured junk whose first
+    // byte happens to look like a line end does not)
+    uint32_t expect = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if ((p + j) % P < L) expect |= 1u << j;
+    if (__ballot((expect & pres) != alpha)) return m;
     m.L = L;
     m.s = s;
     return m;
@@ -1571,10 +1596,19 @@ __global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
     __syncthreads();
-    LineModel m = probe_lines(tab, in, n);
+    uint32_t pj = 0xFFFFFFFFu;
+    LineModel m = probe_lines(tab, in, n, &pj);
     if (threadIdx.x != 0) return;
     const uint32_t n32 = (uint32_t) n;
-    if (m.L == 0) {
+    if (m.L == 0 && pj != 0xFFFFFFFFu) {
+        // junk in the window that no line model explains (unstructured
+        // junk, a short first line): under the clean model the slot holding
+        // it fails, so k_decode_lines takes only the slots before it, and
+        // k_decode_suffix everything from there
+        m.T = pj / 16;
+        m.skip = 1;
+        *ws_view(ws, nranges).lfail = ~(uint64_t) m.T;
+    } else if (m.L == 0) {
         m.T = n32 / 16;
     } else {
         m.P = m.L + m.s;
@@ -1611,6 +1645,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
     m.m = (uint32_t) mw2;
     m.k = (uint32_t) (mw2 >> 32);
     m.rcp = (uint32_t) mw3;
+    m.skip = (uint32_t) (mw3 >> 32);
     const uint32_t lane = lane_id();
     const uint32_t L = m.L, s = m.s, P = m.P, T = m.T;
     const uint32_t t0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kLinesSlots;
@@ -1747,12 +1782,13 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
         // publish the first failing slot; only an improvement (the
         // device-scope load sees what earlier waves published)
         const unsigned long long key = ~(unsigned long long) (t0 + fail_u * 64 + fail_lane);
-        unsigned long long *lf = (unsigned long long *) ws_view(ws, nranges).lfail;
+        unsigned long long *lf = (unsigned long long *) ws_view(ws, nranges).lfail +
+                                 (blockIdx.x % kFailWords) * kFailStride;
         const unsigned long long cur =
             __hip_atomic_load(lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (key > cur) atomicMax(lf, key);
     }
-    if (T >= t0 + kLinesSlots) return;
+    if (T >= t0 + kLinesSlots || m.skip) return;
     // This wave owns slot T: the < 16 + s bytes after the last interior
     // span, decoded exactly, and the result record (replaced by
     // k_decode_suffix when a slot failed).
@@ -2010,7 +2046,22 @@ __global__ __launch_bounds__(kThreads) void k_decode_suffix(
     DecodeWs w = ws_view(ws, nranges);
     uint64_t S = 0, Vb = 0;
     if (!WHOLE) {
-        const uint64_t key = scalar_load_u64(w.lfail);
+        // the first failing slot: the largest key over the failure words
+        // (one wave reads them all, every block)
+        uint64_t key = 0;
+        if (threadIdx.x < 64) {
+            key = __hip_atomic_load((unsigned long long *) w.lfail + (threadIdx.x % kFailWords) *
+                                    kFailStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint64_t o = __shfl_xor(key, d, 64);
+                key = o > key ? o : key;
+            }
+        }
+        __shared__ uint64_t s_key;
+        if (threadIdx.x == 0) s_key = key;
+        __syncthreads();
+        key = s_key;
         if (key == 0) {
             // k_decode_lines took everything: its record is final.  The host
             // mirror is written only now, so a completion never finds a
@@ -2146,7 +2197,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_suffix(
                                              __HIP_MEMORY_SCOPE_AGENT) != want)
                         __builtin_amdgcn_s_sleep(1);
                     __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!WHOLE) *w.lfail = 0;
+                    if (!WHOLE)
+                        for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
                 }
             }
             return;  // this block draws no further ticket
@@ -2416,7 +2468,7 @@ static_assert(sizeof(RowModel) == 48, "RowModel layout");
 
 // The library workspace of the stream holds the model, in the region pass 1
 // uses for its per-range counts (scratch between calls).
-DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + 64); }
+DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + kWsScratch); }
 
 constexpr uint32_t kRowsU = 4;  // slots per lane of the row kernels
 
@@ -3004,12 +3056,13 @@ uint64_t b64x_decoded_cap(uint64_t nchars) { return (nchars + 3) / 4 * 3; }
 
 uint64_t b64x_decode_workspace_size(uint64_t nchars)
 {
-    // header + counts + bases for as many ranges as any plan can use for
-    // nchars (ranges are at least one chunk; 0 = the largest input)
+    // the fixed regions, then counts + bases for as many ranges as any
+    // plan can use for nchars (ranges are at least one chunk; 0 = the
+    // largest input); at least room for a RowModel in the scratch
     uint64_t nr = nchars ? (nchars + kChunk - 1) / kChunk : kMaxRanges;
     if (nr > kMaxRanges) nr = kMaxRanges;
-    return 64 + (nr * 4 + 7) / 8 * 8 + nr * 8 + (nr + kScanTile - 1) / kScanTile * 8 +
-           (nr + kFuseTile - 1) / kFuseTile * 8;
+    const uint64_t scratch = (nr * 4 + 7) / 8 * 8 + nr * 8;
+    return kWsScratch + (scratch > 64 ? scratch : 64);
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }

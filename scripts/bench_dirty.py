@@ -35,10 +35,24 @@ def crlf76(chars: torch.Tensor) -> torch.Tensor:
     return out.contiguous()
 
 
+def sprinkle(chars: torch.Tensor, density: float, seed=7) -> torch.Tensor:
+    """Unstructured junk: a byte outside the alphabet ('!') before each
+    character with probability `density`."""
+    g = torch.Generator(device=chars.device).manual_seed(seed)
+    mask = (torch.rand(chars.numel(), device=chars.device, generator=g) < density)
+    idx = torch.arange(chars.numel(), device=chars.device) + torch.cumsum(mask, 0)
+    out = torch.full((chars.numel() + int(mask.sum()),), ord("!"), dtype=torch.uint8,
+                     device=chars.device)
+    out[idx] = chars
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, nargs="*", default=[64, 1024])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--junk", type=float, default=0.0,
+                    help="unstructured junk density instead of CRLF-76 lines")
     ap.add_argument("--expect-junk", action="store_true",
                     help="B64X_DEC_EXPECT_JUNK: the single-pass decode")
     args = ap.parse_args()
@@ -47,7 +61,7 @@ def main():
         x = torch.empty(n, dtype=torch.uint8, device="cuda")
         b64.fill_splitmix64(x, 0x5EED)
         enc = b64.encode(x)
-        dirty = crlf76(enc)
+        dirty = sprinkle(enc, args.junk) if args.junk else crlf76(enc)
         del enc
         ws = torch.zeros(b64.workspace_size(dirty.numel()), dtype=torch.uint8, device="cuda")
         out = torch.empty(b64.decoded_cap(dirty.numel()), dtype=torch.uint8, device="cuda")
@@ -63,7 +77,8 @@ def main():
             times.append(a.elapsed_time(b))
         ms = sorted(times)[len(times) // 2]
         alg = dirty.numel() + n
-        print(json.dumps({"measure": "decode_crlf76", "expect_junk": args.expect_junk,
+        print(json.dumps({"measure": f"decode_junk{args.junk:g}" if args.junk else "decode_crlf76",
+                          "expect_junk": args.expect_junk,
                           "payload_bytes": n, "chars": dirty.numel(),
                           "ms": ms, "GiB_s_payload": n / ms / 1e-3 / 2**30,
                           "alg_TB_s": alg / ms / 1e-3 / 1e12, "exact": bool(ok)}), flush=True)
