@@ -29,6 +29,8 @@ Also reported on the same JSON line:
   cfg5_egress   BASELINE config 5 through the product's stage stack, host
                 memory in and out, 1 and 16 loops, with the oracle's stack
                 timed beside it (rank 0 at N=1; skipped with --no-cpu);
+  root_scatter  N > 1: rank 0 scatters config 4's 1 GiB to the ranks (reported,
+                not used by the primary metric: SURVEY.md §8(e));
   host_inclusive  the same 1 GiB round trip starting and ending in pinned
                 host memory (rank 0): the kernels read and write the pinned
                 buffers in place over PCIe (the sessions' zero-copy path),
@@ -514,6 +516,34 @@ def bench_cfg5(args):
     return out
 
 
+def bench_root_scatter(world, rank, nbytes=1 << 30, steps=3):
+    """SURVEY.md §8(e), reported, not optimised: rank 0 holds config 4's
+    1 GiB and scatters each rank its 1/N share over the process group (RCCL
+    over xGMI on a node).  Compare with `batch_cfg4`: encoding a share
+    locally takes far less time than moving it, so the primary metric keeps
+    inputs resident per rank."""
+    if world == 1:
+        return None
+    dev = coll_device()
+    share = nbytes // world
+    mine = torch.empty(share, dtype=torch.uint8, device=dev)
+    parts = [torch.empty(share, dtype=torch.uint8, device=dev) for _ in range(world)] \
+        if rank == 0 else None
+    try:
+        dist.scatter(mine, parts, src=0)  # warm-up
+        sync_all(world) if dev == "cuda" else dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dist.scatter(mine, parts, src=0)
+        sync_all(world) if dev == "cuda" else dist.barrier()
+        dt = max_over_ranks((time.perf_counter() - t0) / steps, world)
+    except RuntimeError as e:  # reported, never fatal to the line
+        return {"error": str(e)[:200]}
+    moved = share * (world - 1)
+    return {"workload": f"{nbytes} B on rank 0, {share} B to each of {world - 1} ranks",
+            "ms": dt * 1e3, "GB_s_out_of_rank0": moved / dt / 1e9}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -636,11 +666,13 @@ def main():
     if args.dry_run:
         # the launch and the process group only (CPU tests, gloo): no GPU work
         ranks = gather_floats([float(rank)], world)
+        scatter = bench_root_scatter(world, rank, nbytes=1 << 20, steps=2)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world,
                               "process_group": {"backend": dist.get_backend() if world > 1
                                                 else None, "world_size": world},
-                              "ranks_seen": [int(r[0]) for r in ranks]}), flush=True)
+                              "ranks_seen": [int(r[0]) for r in ranks],
+                              "root_scatter": scatter}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -649,6 +681,7 @@ def main():
     b64.device_check()
     r = bench_single(args, world, rank, b64)
     batch = None if args.no_batch else bench_batch(args, world, rank, b64)
+    scatter = bench_root_scatter(world, rank)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, b64)
@@ -714,6 +747,7 @@ def main():
             "cpu_baseline": cpu,
             "batch_cfg4": batch,
             "host_inclusive": host,
+            "root_scatter": scatter,
             "mime_decode": mime,
             "cfg5_egress": cfg5,
             "process_group": {"backend": dist.get_backend() if world > 1 else None,

@@ -118,6 +118,8 @@ def test_bench_self_launches_ranks():
     assert lines[0]["n_gpus"] == 2
     assert lines[0]["process_group"] == {"backend": "gloo", "world_size": 2}
     assert lines[0]["ranks_seen"] == [0, 1]
+    sc = lines[0]["root_scatter"]  # the scatter leg runs over the same group
+    assert "error" not in sc and sc["ms"] > 0
 
 
 def test_bench_refuses_a_mismatched_world():
