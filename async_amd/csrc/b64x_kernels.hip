@@ -2211,6 +2211,7 @@ struct BatchLayout {
     const uint64_t *in_off;   // nbuf+1 offsets, or null for a uniform stride
     const uint64_t *out_off;  // nbuf offsets, or null
     uint64_t in_stride, out_stride, len;
+    uint64_t big;             // ragged: jobs of >= big characters are skipped (0: none)
 };
 
 DEV void batch_buf(const BatchLayout &L, uint32_t b, uint64_t &beg, uint64_t &len,
@@ -2220,6 +2221,7 @@ DEV void batch_buf(const BatchLayout &L, uint32_t b, uint64_t &beg, uint64_t &le
         beg = L.in_off[b];
         len = L.in_off[b + 1] - beg;
         obeg = L.out_off[b];
+        if (L.big && len >= L.big) len = 0;  // decoded by the single-buffer pipeline
     } else {
         beg = (uint64_t) b * L.in_stride;
         len = L.len;
@@ -2838,7 +2840,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
 __global__ __launch_bounds__(kThreads) void k_batch_finish(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
     const uint8_t *__restrict__ flags, const uint64_t *__restrict__ vcount, uint32_t njobs,
-    DecAlpha a, b64x_dec_result *__restrict__ hres)
+    uint64_t big, DecAlpha a, b64x_dec_result *__restrict__ hres)
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
@@ -2848,6 +2850,7 @@ __global__ __launch_bounds__(kThreads) void k_batch_finish(
     for (uint32_t j = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
          j < njobs; j += nw) {
         const uint64_t beg = in_off[j], n = in_off[j + 1] - beg, V = vcount[j];
+        if (big && n >= big) continue;  // its pipeline wrote the record
         const bool hold = flags[j] & 1;
         int need = hold ? (int) (V & 3) : 0;
         uint8_t got[4] = {0, 0, 0, 0};
@@ -3790,6 +3793,8 @@ struct b64x_lane {
     uint64_t *h_stamp;    // fine-grained pinned: the last finished encode batch
     uint64_t seq;         // the last encode batch queued
     uint64_t in_cap, offs_cap, flags_cap;  // bytes allocated
+    b64x_dec_result *d_res;  // big decode jobs: the pipeline's record ...
+    void *d_ws;              // ... and workspace (allocated at the first)
 };
 
 b64x_lane *b64x_lane_open(void)
@@ -3824,6 +3829,8 @@ void b64x_lane_close(b64x_lane *l)
     if (l->d_in) (void) hipFree(l->d_in);
     if (l->d_offs) (void) hipFree(l->d_offs);
     if (l->d_flags) (void) hipFree(l->d_flags);
+    if (l->d_res) (void) hipFree(l->d_res);
+    if (l->d_ws) (void) hipFree(l->d_ws);
     if (l->h_stamp) (void) hipHostFree(l->h_stamp);
     (void) hipStreamDestroy(l->stream);
     free(l);
@@ -3928,6 +3935,9 @@ int b64x_lane_encode_check(b64x_lane *l)
     return *(volatile uint64_t *) l->h_stamp == l->seq ? 0 : -EIO;
 }
 
+// Hub decode jobs this long go through the single-buffer pipeline.
+static constexpr uint64_t kBigJob = 128u << 10;
+
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const uint8_t *h_flags,
@@ -3948,17 +3958,39 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
             return err;
         uint64_t *d_in_off = l->d_offs, *d_out_off = l->d_offs + words,
                  *d_vcount = l->d_offs + 2 * words;
-        const BatchLayout L{d_in_off, d_out_off, 0, 0, 0};
+        // Jobs of kBigJob characters or more (whole stage blocks) would each
+        // keep one wave of the batch kernel busy for hundreds of us: they
+        // take the single-buffer pipeline instead, in job order on the lane's
+        // stream, which writes their records itself; the batch kernels skip them.
+        uint32_t nbig = 0;
+        for (uint32_t j = 0; j < njobs; j++) nbig += h_in_off[j + 1] - h_in_off[j] >= kBigJob;
+        const BatchLayout L{d_in_off, d_out_off, 0, 0, 0, nbig ? kBigJob : 0};
         const uint8_t *src = h_in_off[njobs] ? l->d_in : (const uint8_t *) l->d_offs;
-        if ((err = launch_batch_decode(src, L, njobs, h_out, d_vcount, abc, l->stream, true)))
-            return err;
-        const DeviceInfo *d = device_info();
-        const uint32_t grid = cap_grid((njobs + kWavesPerBlock - 1) / kWavesPerBlock,
-                                       (uint64_t) d->cus * 8);
-        hipLaunchKernelGGL(k_batch_finish, dim3(grid), dim3(kThreads), 0, l->stream, src, d_in_off,
-                           (const uint8_t *) l->d_flags, (const uint64_t *) d_vcount, njobs,
-                           dec_alpha(abc), h_res);
-        if ((err = launch_status())) return err;
+        if (nbig < njobs) {
+            if ((err = launch_batch_decode(src, L, njobs, h_out, d_vcount, abc, l->stream, true)))
+                return err;
+            const DeviceInfo *d = device_info();
+            const uint32_t grid = cap_grid((njobs + kWavesPerBlock - 1) / kWavesPerBlock,
+                                           (uint64_t) d->cus * 8);
+            hipLaunchKernelGGL(k_batch_finish, dim3(grid), dim3(kThreads), 0, l->stream, src,
+                               d_in_off, (const uint8_t *) l->d_flags,
+                               (const uint64_t *) d_vcount, njobs, L.big, dec_alpha(abc), h_res);
+            if ((err = launch_status())) return err;
+        }
+        if (nbig && !l->d_ws) {
+            const uint64_t wsz = b64x_decode_workspace_size(0);
+            if (hipMalloc(&l->d_res, sizeof *l->d_res) != hipSuccess) return -ENOMEM;
+            if (hipMalloc(&l->d_ws, wsz) != hipSuccess) return -ENOMEM;
+            if ((err = hip_err(hipMemsetAsync(l->d_ws, 0, wsz, l->stream)))) return err;
+        }
+        for (uint32_t j = 0; nbig && j < njobs; j++) {
+            const uint64_t n = h_in_off[j + 1] - h_in_off[j];
+            if (n < kBigJob) continue;
+            if ((err = decode_dev_impl(l->d_in + h_in_off[j], n, h_out + h_out_off[j], l->d_res,
+                                       h_res + j, abc, h_flags[j] & 1 ? B64X_DEC_HOLD_TAIL : 0,
+                                       l->d_ws, l->stream)))
+                return err;
+        }
     }
     if (done) return hip_err(hipLaunchHostFunc(l->stream, done, arg));
     return 0;
