@@ -108,3 +108,42 @@ def test_many_long_decoder_streams_on_one_loop(monkeypatch):
             bad.append((i, len(m), len(g), len(want), first, last))
     # (stream, chars, got bytes, want bytes, first/last differing byte)
     assert not bad, bad
+
+
+def _dirty(rng, n):
+    """Random bytes encoded, broken into 77-character lines with a '*' every
+    ~1,000 characters: blocks cut anywhere leave 0-3 sextets over."""
+    chars = orc.encode(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    lines = b"\r\n".join(chars[i:i + 77] for i in range(0, len(chars), 77))
+    cut = sorted(rng.integers(0, len(lines), len(lines) // 1000))
+    return b"*".join(lines[a:b] for a, b in zip([0] + cut, cut + [len(lines)]))
+
+
+@pytest.mark.parametrize("cap,read_size", [(200_000, 65536), (300_001, 1 << 20), (1 << 20, 4096)])
+def test_decoder_stage_big_blocks_with_carries(monkeypatch, cap, read_size):
+    """Streams of many blocks of >= 128 KiB, each decoded by the single-buffer
+    pipeline inside its hub batch, with held sextets carried from block to
+    block: the stream's bytes equal the oracle's."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    rng = np.random.default_rng(cap + read_size)
+    dirty = _dirty(rng, 2_500_000 + cap % 7)
+    got, err = util.stage_decode(dirty, 0, read_size)
+    assert err == 0
+    assert got == orc.decode_stream(dirty, 0, 0, 200)
+
+
+def test_decoder_streams_big_and_small_jobs_in_one_batch(monkeypatch):
+    """Long and short decoder streams on one loop share hub batches: the big
+    jobs take the pipeline, the rest the batch kernel, and every stream's
+    bytes equal the oracle's."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(150_000))
+    rng = np.random.default_rng(29)
+    msgs = []
+    for i in range(48):
+        n = int(rng.integers(200_000, 700_000)) if i % 3 == 0 else int(rng.integers(0, 5000))
+        msgs.append(_dirty(rng, n) if i % 2 else orc.encode(
+            rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+    got, err = util.ingress_stacks(msgs, 65536)
+    assert err == 0
+    for i, m in enumerate(msgs):
+        assert got[i] == orc.decode_stream(m, 0, 0, 200), i
