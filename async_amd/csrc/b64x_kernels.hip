@@ -402,7 +402,10 @@ DEV u32x3a4 ld12(const uint8_t *p)
 // n mod 12 bytes (with padding) are done by the last block.  Round 1's A/B
 // of tile depth (1-8 quads), software pipelining and cached loads picked
 // this form (profiles/r01_v6_*).
-constexpr int kFlatU = 2;
+#ifndef B64X_FLAT_U  // A/B builds only (scripts/ab_variants.sh)
+#define B64X_FLAT_U 2
+#endif
+constexpr int kFlatU = B64X_FLAT_U;
 
 __global__ __launch_bounds__(kThreads) void k_encode_flat(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
@@ -794,6 +797,9 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //   model   the line model k_decode_probe found, for k_decode_lines and
 //           k_decode_suffix
 //   fticket, fstatus  k_decode_suffix's tile ticket and status words
+//   sfx_start  where the last call's k_decode_suffix<false> started (its
+//           first failing slot's span), ~0 when it had nothing to do; read
+//           by the tests only (clean and MIME input must never need it)
 // The regions that must be zero between calls (status, fstatus, lfail) sit
 // at fixed offsets after the header, sized for the largest plan, so calls of
 // different sizes on one workspace never find another call's scratch
@@ -817,6 +823,7 @@ struct DecodeWs {
     uint64_t *fd_cur;
     uint32_t *ticket;
     uint32_t *fticket;   // the single-pass decode's tile ticket (zero between calls)
+    uint64_t *sfx_start; // where k_decode_suffix<false> started, ~0 = nothing to do
     uint32_t *counts;
     uint64_t *bases;
     uint64_t *status;
@@ -834,7 +841,7 @@ constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suf
 constexpr uint64_t kWsFail = kWsFStatus + kMaxRanges / kFuseTile * 8;     // lines failures
 constexpr uint64_t kWsScratch = kWsFail + kFailWords * kFailStride * 8;   // counts, bases
 
-// Layout: 64-byte header (fd, fd_cur, ticket, fticket, model), the
+// Layout: 64-byte header (fd, fd_cur, ticket, fticket, sfx_start, model), the
 // zero-between-calls regions at fixed offsets, then the scratch counts and
 // bases of `nranges` ranges.
 DEV DecodeWs ws_view(void *ws, uint32_t nranges)
@@ -845,6 +852,7 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.fd_cur = (uint64_t *) (p + 8);
     w.ticket = (uint32_t *) (p + 16);
     w.fticket = (uint32_t *) (p + 20);
+    w.sfx_start = (uint64_t *) (p + 24);
     w.model = (LineModel *) (p + 32);
     w.status = (uint64_t *) (p + kWsStatus);
     w.fstatus = (uint64_t *) (p + kWsFStatus);
@@ -1450,7 +1458,10 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
 //
 // Reference: the per-character loop of decoder_read(), src/base64decoder.c:
 // 52-80 (skip non-alphabet bytes, 8 bits out per 4 characters' 24).
-constexpr uint32_t kLinesU = 2;                     // slots per lane
+#ifndef B64X_LINES_U  // A/B builds only (scripts/ab_variants.sh)
+#define B64X_LINES_U 4
+#endif
+constexpr uint32_t kLinesU = B64X_LINES_U;          // slots per lane (2: +1-3 %, 8: +7 %)
 constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
 constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
 
@@ -2066,9 +2077,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_suffix(
             // k_decode_lines took everything: its record is final.  The host
             // mirror is written only now, so a completion never finds a
             // consistent but provisional record there.
-            if (hres && blockIdx.x == 0 && threadIdx.x == 0) {
-                const b64x_dec_result r = *res;
-                *hres = r;
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                if (hres) {
+                    const b64x_dec_result r = *res;
+                    *hres = r;
+                }
+                *w.sfx_start = ~0ull;
             }
             return;
         }
@@ -2080,6 +2094,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_suffix(
     uint8_t *base_out = out + Vb / 4 * 3;
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
+    if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
     __shared__ P2dSmem sm;
     __shared__ uint32_t s_tile;
     __shared__ uint32_t s_cnt[kFuseTile];

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of library builds (scripts/ab_variants.sh):
+config 2's encode and clean decode, and the 1 GiB CRLF-76 decode, K steps
+each with HIP events, in a child process per (round, variant) so that the
+variants alternate on the same box.
+
+    python scripts/ab_time.py [--rounds 3] [--steps 20] LIB [LIB ...]
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib, steps):
+    sys.path.insert(0, ROOT)
+    import torch
+    from async_amd import _lib
+    _lib.LIB_PATH = os.path.abspath(lib)
+    from async_amd import b64
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from bench_dirty import crlf76, sprinkle
+    n = 1 << 30
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    enc = b64.encode(x)
+    dirty = crlf76(enc)
+    junk = sprinkle(enc, 0.05)
+    out = torch.empty(b64.decoded_cap(junk.numel()), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(b64.workspace_size(junk.numel()), dtype=torch.uint8, device="cuda")
+    res = {}
+
+    def timeit(name, fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(steps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+        res[name] = (statistics.median(ts), statistics.mean(ts), min(ts))
+
+    timeit("encode", lambda: b64.encode(x, out=enc))
+    timeit("decode", lambda: b64.decode(enc, out=out, workspace=ws, result=rr))
+    ok = torch.equal(out[:n], x)
+    timeit("crlf", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr))
+    ok = ok and torch.equal(out[:n], x)
+    timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
+    ok = ok and torch.equal(out[:n], x)
+    print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    if a.child:
+        return child(a.libs[0], a.steps)
+    agg = {lib: {} for lib in a.libs}
+    for r in range(a.rounds):
+        for lib in a.libs:
+            p = subprocess.run([sys.executable, __file__, "--child", "--steps", str(a.steps), lib],
+                               capture_output=True, text=True, timeout=300)
+            line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+            if p.returncode or not line:
+                print(p.stdout, p.stderr, file=sys.stderr)
+                sys.exit(p.returncode or 1)
+            d = json.loads(line[-1])
+            print(json.dumps(d), flush=True)
+            for k in ("encode", "decode", "crlf", "junk"):
+                agg[lib].setdefault(k, []).append(d[k][0])
+    for lib in a.libs:
+        print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
+                                             for k, v in agg[lib].items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -681,6 +681,41 @@ def test_decode_lines_shapes_vs_oracle(L, sep):
         assert got == want, off
 
 
+def _sfx_start(ws: torch.Tensor) -> int:
+    """The workspace's record of where the last call's exact suffix decode
+    started (header bytes 24..31; 2**64 - 1: it had nothing to do)."""
+    torch.cuda.synchronize()
+    return int(np.frombuffer(ws[24:32].cpu().numpy().tobytes(), np.uint64)[0])
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_decode_lines_takes_clean_and_mime_whole(aligned):
+    """Clean text and MIME/PEM-formatted text are decoded by k_decode_lines
+    alone -- the exact suffix decode has nothing to do (a speed property the
+    results alone cannot show: the suffix would decode them exactly too) --
+    while a stream that breaks the model hands over at its first failing
+    slot, at or before the break."""
+    rng = np.random.default_rng(41)
+    chars = orc.encode(rng.integers(0, 256, 3_000_000, dtype=np.uint8))
+    ws = torch.zeros(b64.workspace_size(len(chars) * 2), dtype=torch.uint8, device=DEV)
+    off = 0 if aligned else 1
+    cases = [(chars, None), (_wrap(chars, 76, b"\r\n"), None), (_wrap(chars, 64, b"\n"), None)]
+    k = 2_000_000
+    cases.append((chars[:k] + b"!" + chars[k:], k))
+    mime = _wrap(chars, 76, b"\r\n")
+    cases.append((mime[:k] + b"=" + mime[k + 1:], k))
+    for text, brk in cases:
+        x = dev(bytes(off) + text)[off:]
+        out = torch.empty(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+        d = b64.decode(x, out=out, workspace=ws)
+        assert d.bytes().cpu().numpy().tobytes() == orc.decode(text)
+        start = _sfx_start(ws)
+        if brk is None:
+            assert start == 2**64 - 1, (len(text), start)
+        else:
+            assert start <= brk and brk - start < 1 << 12, (brk, start)
+
+
 def _mime_batch(nbuf, n, L, sep, rng, deviants=()):
     rows = []
     for i in range(nbuf):
