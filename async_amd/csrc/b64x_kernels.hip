@@ -406,6 +406,12 @@ DEV u32x3a4 ld12(const uint8_t *p)
 #define B64X_FLAT_U 2
 #endif
 constexpr int kFlatU = B64X_FLAT_U;
+#ifndef B64X_ENC_NTL  // A/B builds only: non-temporal loads / stores
+#define B64X_ENC_NTL true
+#endif
+#ifndef B64X_ENC_NTS
+#define B64X_ENC_NTS true
+#endif
 
 __global__ __launch_bounds__(kThreads) void k_encode_flat(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
@@ -421,11 +427,11 @@ __global__ __launch_bounds__(kThreads) void k_encode_flat(
         u32x3a4 cur[kFlatU];
         const uint8_t *src = in + (t * tile + tid) * 12;
 #pragma unroll
-        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<true>(src + u * kThreads * 12);
+        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<B64X_ENC_NTL>(src + u * kThreads * 12);
         uint8_t *dst = out + (t * tile + tid) * 16;
 #pragma unroll
         for (int u = 0; u < kFlatU; u++)
-            store16<true>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
+            store16<B64X_ENC_NTS>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
     }
     if (blockIdx.x == gridDim.x - 1) {
         for (uint64_t q = full * tile + tid; q < nq; q += kThreads) {
@@ -4038,6 +4044,30 @@ int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t
 }
 
 #ifdef B64X_TEST_HOOKS
+// Test builds only: the copy ceiling bench.py reads the roofline against
+// (SURVEY.md 8(d)): 16-byte non-temporal loads and stores, 4 per lane in
+// flight, a non-persistent grid -- the kernels' own access shape with no
+// arithmetic.  n a multiple of 16 * 256 * 4, buffers 16-byte aligned.
+__global__ __launch_bounds__(kThreads) void k_test_copy(const uint8_t *__restrict__ in,
+                                                        uint8_t *__restrict__ out)
+{
+    const uint64_t base = (uint64_t) blockIdx.x * kThreads * 4 * 16 + 16 * threadIdx.x;
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = ld16<true>(in + base + (uint64_t) u * kThreads * 16);
+#pragma unroll
+    for (int u = 0; u < 4; u++) store16<true>(out + base + (uint64_t) u * kThreads * 16, v[u]);
+}
+
+int b64x__test_copy(const void *src, void *dst, uint64_t n, void *stream)
+{
+    const uint64_t per = (uint64_t) kThreads * 4 * 16;
+    if (n % per || ((((uintptr_t) src) | ((uintptr_t) dst)) & 15)) return -EINVAL;
+    hipLaunchKernelGGL(k_test_copy, dim3((uint32_t) (n / per)), dim3(kThreads), 0,
+                       (hipStream_t) stream, (const uint8_t *) src, (uint8_t *) dst);
+    return launch_status();
+}
+
 // Test builds only: decode ranges of `chunks` chunks (0 = the default);
 // returns the previous setting.
 uint64_t b64x__test_range_chunks(uint64_t chunks)

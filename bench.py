@@ -516,6 +516,49 @@ def bench_cfg5(args):
     return out
 
 
+def copy_ceiling(nbytes: int, steps: int = 20) -> dict | None:
+    """The measured copy bandwidth SURVEY.md 8(d) asks the roofline to be
+    read against: a copy moving the same bytes as one launch of the path
+    (nbytes read + written in total) with the kernels' own access shape --
+    16-byte non-temporal loads and stores, 4 per lane in flight, a
+    non-persistent grid (k_test_copy in the test-hooks build of the kernels,
+    tests/csrc/libb64x_hooks.so; HIP's blit copy reaches only ~5.1 TB/s) --
+    median of `steps` runs after 3 warm-ups, HIP events on torch's stream."""
+    import ctypes
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "csrc",
+                        "libb64x_hooks.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.b64x__test_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_void_p]
+    lib.b64x__test_copy.restype = ctypes.c_int
+    per = 256 * 4 * 16
+    half = nbytes // 2 // per * per
+    src = torch.empty(half, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    src.fill_(7)
+    stream = torch.cuda.current_stream().cuda_stream
+    ts = []
+    for i in range(steps + 3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = lib.b64x__test_copy(src.data_ptr(), dst.data_ptr(), half, stream)
+        b.record()
+        b.synchronize()
+        if rc:
+            raise RuntimeError(f"b64x__test_copy: {rc}")
+        if i >= 3:
+            ts.append(a.elapsed_time(b))
+    ok = bool(torch.equal(dst[:: 1 << 20], src[:: 1 << 20]))
+    ms = sorted(ts)[len(ts) // 2]
+    del src, dst
+    return {"GBps": 2 * half / (ms * 1e-3) / 1e9, "ms": ms, "bytes_moved": 2 * half,
+            "checked": ok,
+            "how": "k_test_copy (tests/csrc/libb64x_hooks.so): 16-B nt loads/stores, 4 per "
+                   f"lane, median of {steps} after 3 warm-ups"}
+
+
 def bench_root_scatter(world, rank, nbytes=1 << 30, steps=3):
     """SURVEY.md §8(e), reported, not optimised: rank 0 holds config 4's
     1 GiB and scatters each rank its 1/N share over the process group (RCCL
@@ -680,6 +723,7 @@ def main():
 
     b64.device_check()
     r = bench_single(args, world, rank, b64)
+    ceiling = copy_ceiling(r["N"] + r["E"]) if rank == 0 else None
     batch = None if args.no_batch else bench_batch(args, world, rank, b64)
     scatter = bench_root_scatter(world, rank)
     cpu = None
@@ -741,6 +785,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
+                "copy_ceiling_GBps": ceiling["GBps"] if ceiling else None,
+                "frac_of_copy": achieved / ceiling["GBps"] if ceiling else None,
+                "copy_ceiling": ceiling,
                 # the committed PMC summary is for the 1 GiB workload
                 "traffic": load_traffic(knames) if N == 1 << 30 else None,
             },
