@@ -29,7 +29,11 @@ enum {
     HUB_LANES = 4,          /* batches in flight per loop */
     HUB_MAX_LIVE = HUB_LANES + 4, /* arenas a hub holds before idle
                                      stages are made to wait */
-    POOL_MAX = 16,          /* idle arenas kept process-wide for reuse */
+    POOL_MAX = 128,         /* idle arenas kept process-wide for reuse (~41 MB
+                               pinned each; 16 loops on one GPU hold ~50 at
+                               once, and every arena freed and allocated again
+                               costs milliseconds of pinned-memory calls that
+                               stall the other loops) */
     HUB_JOBS = 1 << 16,     /* jobs per arena */
     HUB_DEPTH = 8,          /* reservations open at once (stages reading
                                through stages, see b64_hub_reserve) */

@@ -510,6 +510,7 @@ def bench_cfg5(args):
             if framed[int(f_off[i]):int(f_off[i]) + int(f_len[i])].tobytes() != want:
                 raise SystemExit(f"cfg5 egress mismatch at message {i}")
         out[f"loops_{T}"] = {"GiB_s": nbytes / dt / 2**30, "seconds": dt,
+                             "setup_s": float(times[0]), "loop_s": float(times[1]),
                              "framed_bytes": int(f_len.sum()),
                              "cpu_port_GiB_s": nbytes / cpu_dt / 2**30, "cpu_threads": T}
         del framed, res
