@@ -55,6 +55,19 @@ def child(lib, steps):
     ok = ok and torch.equal(out[:n], x)
     timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
     ok = ok and torch.equal(out[:n], x)
+    # config 4: 1 M x 1 KiB rows, strided decode (clean)
+    del dirty, junk, enc, out, x
+    nb, L = 1 << 20, 1024
+    Es = b64.encoded_len(L)
+    cap = 12 * ((Es + 15) // 16)
+    xb = torch.empty(nb * L, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(xb, 0x5EED)
+    eb = torch.empty(nb * Es, dtype=torch.uint8, device="cuda")
+    db = torch.empty(nb * cap, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    timeit("rows_enc", lambda: b64.encode_strided(xb, L, L, nb, eb, Es))
+    timeit("rows_dec", lambda: b64.decode_strided(eb, Es, Es, nb, db, cap, ol))
+    ok = ok and bool((ol == L).all()) and torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L))
     print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
 
 
@@ -78,7 +91,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("encode", "decode", "crlf", "junk"):
+            for k in ("encode", "decode", "crlf", "junk", "rows_enc", "rows_dec"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
