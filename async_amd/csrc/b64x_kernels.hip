@@ -13,7 +13,9 @@
 // How it runs here (DESIGN.md §5 has the byte budget and the rooflines):
 //   * encode is stateless per 3-byte group.  One lane turns 12 input bytes
 //     (one dwordx3 load) into 16 characters (one dwordx4 store); the
-//     64-entry alphabet sits in LDS and is read with ds_read_u8.  Byte
+//     64-entry alphabet is held one character per lane and read across
+//     lanes with ds_bpermute (k_encode_flat; the batch kernels keep it in
+//     LDS and read it with ds_read_u8).  Byte
 //     regrouping is v_perm_b32, not shifts (k_encode_flat; batches:
 //     k_encode_tight2, k_encode_strided, k_encode_ragged).
 //   * decode is stateful only through the number of alphabet characters
@@ -213,6 +215,28 @@ DEV uint4 enc_quad(const uint8_t *tab, uint32_t a, uint32_t b, uint32_t c)
     o.z = enc_group(tab, g2);
     o.w = enc_group(tab, g3);
     return o;
+}
+
+// enc_quad with the alphabet held one character per lane (lane i: the
+// character of sextet i) and read across lanes with ds_bpermute -- no LDS
+// table, so no block barrier before the first lookup.
+DEV uint32_t enc_group_bp(uint32_t lc, uint32_t g)
+{
+    const uint32_t c0 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 16) & 0xFCu), (int) lc);
+    const uint32_t c1 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 10) & 0xFCu), (int) lc);
+    const uint32_t c2 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 4) & 0xFCu), (int) lc);
+    const uint32_t c3 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g << 2) & 0xFCu), (int) lc);
+    return c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+}
+
+DEV uint4 enc_quad_bp(uint32_t lc, uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t g0 = __builtin_amdgcn_perm(0u, a, 0x0c000102u);
+    uint32_t g1 = __builtin_amdgcn_perm(b, a, 0x0c030405u);
+    uint32_t g2 = __builtin_amdgcn_perm(c, b, 0x0c020304u);
+    uint32_t g3 = __builtin_amdgcn_perm(0u, c, 0x0c010203u);
+    return make_uint4(enc_group_bp(lc, g0), enc_group_bp(lc, g1), enc_group_bp(lc, g2),
+                      enc_group_bp(lc, g3));
 }
 
 // Encode r (1..12) bytes at `src` byte by byte; `last` = these are the
@@ -417,12 +441,13 @@ __global__ __launch_bounds__(kThreads) void k_encode_flat(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
 {
     __shared__ uint8_t tab[64];
-    build_enc_table(tab, a);
-    __syncthreads();
     const uint64_t nq = n / 12;
     const uint64_t tile = (uint64_t) kThreads * kFlatU;
     const uint64_t full = nq / tile;
     const uint32_t tid = threadIdx.x;
+    // the alphabet one character per lane, read across lanes (enc_quad_bp):
+    // no LDS table and no block barrier before the first load (1 % faster)
+    const uint32_t lc = (uint32_t) enc_char(threadIdx.x & 63u, a);
     for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
         u32x3a4 cur[kFlatU];
         const uint8_t *src = in + (t * tile + tid) * 12;
@@ -431,9 +456,11 @@ __global__ __launch_bounds__(kThreads) void k_encode_flat(
         uint8_t *dst = out + (t * tile + tid) * 16;
 #pragma unroll
         for (int u = 0; u < kFlatU; u++)
-            store16<B64X_ENC_NTS>(dst + u * kThreads * 16, enc_quad(tab, cur[u].x, cur[u].y, cur[u].z));
+            store16<B64X_ENC_NTS>(dst + u * kThreads * 16, enc_quad_bp(lc, cur[u].x, cur[u].y, cur[u].z));
     }
     if (blockIdx.x == gridDim.x - 1) {
+        build_enc_table(tab, a);
+        __syncthreads();
         for (uint64_t q = full * tile + tid; q < nq; q += kThreads) {
             const u32x3a4 v = *(const u32x3a4 *) (in + q * 12);
             store16<true>(out + q * 16, enc_quad(tab, v.x, v.y, v.z));
@@ -4045,27 +4072,54 @@ int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t
 
 #ifdef B64X_TEST_HOOKS
 // Test builds only: the copy ceiling bench.py reads the roofline against
-// (SURVEY.md 8(d)): 16-byte non-temporal loads and stores, 4 per lane in
-// flight, a non-persistent grid -- the kernels' own access shape with no
-// arithmetic.  n a multiple of 16 * 256 * 4, buffers 16-byte aligned.
-__global__ __launch_bounds__(kThreads) void k_test_copy(const uint8_t *__restrict__ in,
-                                                        uint8_t *__restrict__ out)
+// (SURVEY.md 8(d)): 16-byte loads and stores, U per lane in flight, a
+// non-persistent grid of TH-thread blocks -- the kernels' own access shape
+// with no arithmetic (mode 0: U = 4, TH = 256, non-temporal; the other modes
+// are the shapes b64x__test_copy_mode sweeps).  n a multiple of
+// 16 * TH * U, buffers 16-byte aligned.
+extern "C++" {
+template <int U, int TH, bool NT>
+__global__ __launch_bounds__(TH) void k_test_copy(const uint8_t *__restrict__ in,
+                                                  uint8_t *__restrict__ out)
 {
-    const uint64_t base = (uint64_t) blockIdx.x * kThreads * 4 * 16 + 16 * threadIdx.x;
-    uint4 v[4];
+    const uint64_t base = (uint64_t) blockIdx.x * TH * U * 16 + 16 * threadIdx.x;
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) v[u] = ld16<true>(in + base + (uint64_t) u * kThreads * 16);
+    for (int u = 0; u < U; u++) v[u] = ld16<NT>(in + base + (uint64_t) u * TH * 16);
 #pragma unroll
-    for (int u = 0; u < 4; u++) store16<true>(out + base + (uint64_t) u * kThreads * 16, v[u]);
+    for (int u = 0; u < U; u++) store16<NT>(out + base + (uint64_t) u * TH * 16, v[u]);
+}
+
+template <int U, int TH, bool NT>
+static int test_copy(const void *src, void *dst, uint64_t n, void *stream)
+{
+    const uint64_t per = (uint64_t) TH * U * 16;
+    if (n % per || ((((uintptr_t) src) | ((uintptr_t) dst)) & 15)) return -EINVAL;
+    hipLaunchKernelGGL((k_test_copy<U, TH, NT>), dim3((uint32_t) (n / per)), dim3(TH), 0,
+                       (hipStream_t) stream, (const uint8_t *) src, (uint8_t *) dst);
+    return launch_status();
+}
+}  // extern "C++"
+
+int b64x__test_copy_mode(const void *src, void *dst, uint64_t n, void *stream, int mode)
+{
+    switch (mode) {
+    case 0: return test_copy<4, 256, true>(src, dst, n, stream);
+    case 1: return test_copy<1, 256, true>(src, dst, n, stream);
+    case 2: return test_copy<2, 256, true>(src, dst, n, stream);
+    case 3: return test_copy<8, 256, true>(src, dst, n, stream);
+    case 4: return test_copy<4, 512, true>(src, dst, n, stream);
+    case 5: return test_copy<4, 1024, true>(src, dst, n, stream);
+    case 6: return test_copy<4, 256, false>(src, dst, n, stream);
+    case 7: return test_copy<2, 1024, true>(src, dst, n, stream);
+    case 8: return test_copy<1, 1024, true>(src, dst, n, stream);
+    default: return -EINVAL;
+    }
 }
 
 int b64x__test_copy(const void *src, void *dst, uint64_t n, void *stream)
 {
-    const uint64_t per = (uint64_t) kThreads * 4 * 16;
-    if (n % per || ((((uintptr_t) src) | ((uintptr_t) dst)) & 15)) return -EINVAL;
-    hipLaunchKernelGGL(k_test_copy, dim3((uint32_t) (n / per)), dim3(kThreads), 0,
-                       (hipStream_t) stream, (const uint8_t *) src, (uint8_t *) dst);
-    return launch_status();
+    return b64x__test_copy_mode(src, dst, n, stream, 0);
 }
 
 // Test builds only: decode ranges of `chunks` chunks (0 = the default);
