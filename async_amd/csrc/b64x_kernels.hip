@@ -1602,8 +1602,12 @@ DEV uint4 slot_chars(const uint32_t w[6], uint32_t o, uint32_t c, uint32_t s, ui
     }
     // separator bytes at A[c .. c + s)
     const uint32_t q = c >> 2, r = c & 3u;
-    const uint32_t lo = q == 0 ? A[0] : q == 1 ? A[1] : q == 2 ? A[2] : q == 3 ? A[3] : A[4];
-    const uint32_t hi = q == 0 ? A[1] : q == 1 ? A[2] : q == 2 ? A[3] : q == 3 ? A[4] : A[5];
+    // A[q] and A[q + 1], q = 0..4, as levels of selects on q's bits
+    const bool b0 = q & 1u, b1 = q & 2u, b2 = q & 4u;
+    const uint32_t a01 = b0 ? A[1] : A[0], a23 = b0 ? A[3] : A[2], a45 = b0 ? A[5] : A[4];
+    const uint32_t a12 = b0 ? A[2] : A[1], a34 = b0 ? A[4] : A[3];
+    const uint32_t lo = b2 ? a45 : b1 ? a23 : a01;
+    const uint32_t hi = b2 ? A[5] : b1 ? a34 : a12;
     *sep = __builtin_amdgcn_alignbyte(hi, lo, r);
     return make_uint4(D[0], D[1], D[2], D[3]);
 }
@@ -1623,8 +1627,28 @@ DEV uint4 slot_chars4(const uint32_t w[6], uint32_t o, uint32_t c4, uint32_t s, 
         const uint32_t Bj = s >= 4 ? A[j + 1] : __builtin_amdgcn_alignbyte(A[j + 1], A[j], s);
         D[j] = (uint32_t) j < c4 ? A[j] : Bj;
     }
-    *sep = c4 == 1 ? A[1] : c4 == 2 ? A[2] : c4 == 3 ? A[3] : A[4];
+    // A[c4], c4 = 1..4, as two levels of selects (an equality chain here
+    // compiled to exec-mask branches per slot)
+    const uint32_t x = c4 - 1;
+    const uint32_t lo = (x & 1u) ? A[2] : A[1];
+    const uint32_t hi = (x & 1u) ? A[4] : A[3];
+    *sep = (x & 2u) ? hi : lo;
     return make_uint4(D[0], D[1], D[2], D[3]);
+}
+
+// Bit 8k set when byte k of `sep` is outside the alphabet (table value
+// 0xFF), for all four bytes: four lookups, no wait between them.
+DEV uint32_t sep_nonalpha(const uint8_t *tab, uint32_t sep)
+{
+    const uint32_t v = (uint32_t) tab[sep & 0xFFu] | ((uint32_t) tab[(sep >> 8) & 0xFFu] << 8) |
+                       ((uint32_t) tab[(sep >> 16) & 0xFFu] << 16) | ((uint32_t) tab[sep >> 24] << 24);
+    return (v >> 7) & 0x01010101u;
+}
+
+// The sep_nonalpha bits of the first n (0..4) separator bytes.
+DEV uint32_t sep_need(uint32_t n)
+{
+    return n >= 4 ? 0x01010101u : 0x01010101u & ((1u << (8 * n)) - 1u);
 }
 
 // One wave: the model, the stream's interior slot count T and the division
@@ -1669,7 +1693,14 @@ __global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__
     *ws_view(ws, nranges).model = m;
 }
 
-__global__ __launch_bounds__(kThreads) void k_decode_lines(
+// At least 6 waves per SIMD (80 VGPRs): unconstrained, the rarely taken
+// generic and tail paths pushed the kernel to 81 VGPRs and 5 waves, which
+// cost the clean path 5 us per 1 GiB; 8 waves (64 VGPRs) spill.
+#ifndef B64X_LINES_WPE  // A/B builds only: minimum waves per SIMD
+#define B64X_LINES_WPE 6
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
+void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res)
 {
@@ -1759,11 +1790,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
             map_fast(tab, d, 16, G, bad);
             // the separator bytes of a line that ends here must all be
             // outside the alphabet (looked up by every lane, kept by those)
-            uint32_t sep_alpha = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kLinesMaxS; k++)
-                if (k < s) sep_alpha |= tab[(sep >> (8 * k)) & 0xFFu] < 64u ? 1u : 0u;
-            if (hs[u]) bad |= sep_alpha << 8;
+            const uint32_t need = sep_need(s);
+            if (hs[u] && (sep_nonalpha(tab, sep) & need) != need) bad |= 0x100u;
             const uint64_t fb = __ballot(bad != 0);
             if (fb && fail_u == kLinesU) {
                 fail_u = u;
@@ -1801,11 +1829,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_lines(
             uint32_t sep;
             const uint4 d = slot_chars(w6, oo[u], cc[u], s, &sep);
             map_fast(tab, d, 16, G[u], bad[u]);
-            if (hs[u]) {
-#pragma unroll
-                for (uint32_t k = 0; k < kLinesMaxS; k++)
-                    if (k < s && tab[(sep >> (8 * k)) & 0xFFu] < 64u) bad[u] |= 0x100u;
-            }
+            const uint32_t need = sep_need(s);
+            if (hs[u] && (sep_nonalpha(tab, sep) & need) != need) bad[u] |= 0x100u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
@@ -2580,10 +2605,8 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
                                  : slot_chars(w6, o, c, s, &sep);
     // separator bytes inside the span that must be outside the alphabet
     const uint32_t nsep = !hs ? 0u : !last ? s : c > k ? 0u : (nspan - c < s ? nspan - c : s);
-    uint32_t sep_alpha = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kLinesMaxS; q++)
-        if (q < nsep) sep_alpha |= tab[(sep >> (8 * q)) & 0xFFu] < 64u ? 1u : 0u;
+    const uint32_t need = sep_need(nsep);
+    const bool sep_alpha = (sep_nonalpha(tab, sep) & need) != need;
     if (!last) {
         uint32_t bad;
         map_fast(tab, d, 16, G, bad);
