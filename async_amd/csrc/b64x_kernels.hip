@@ -758,6 +758,34 @@ DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
     lc.vmask = m;
 }
 
+// A slot's 16 characters of which the first k (0..16) count, for every
+// slot of a row alike (no per-lane branch between interior slots and a
+// row's last): G the four groups with characters outside the alphabet or
+// past k zeroed, *valid bit i set when character i counts and is in the
+// alphabet.  Per dword: four lookups packed into P, the in-alphabet bytes
+// (table values below 0x80) limited to k spread to byte flags, P masked by
+// them, the group by two v_dot4, the flags gathered by one multiply.
+DEV void map_slot(const uint8_t *tab, uint4 w, uint32_t k, uint32_t G[4], uint32_t &valid)
+{
+    const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+    const uint32_t km = k >= 16 ? 0xFFFFu : (1u << k) - 1u;
+    uint32_t v = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const uint32_t P = (uint32_t) tab[dw[g] & 0xFFu] | ((uint32_t) tab[(dw[g] >> 8) & 0xFFu] << 8) |
+                           ((uint32_t) tab[(dw[g] >> 16) & 0xFFu] << 16) |
+                           ((uint32_t) tab[dw[g] >> 24] << 24);
+        const uint32_t kin = (((km >> (4 * g)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        const uint32_t ok = ~(P >> 7) & kin;  // byte flags
+        const uint32_t Pz = P & (ok * 0xFFu);
+        const uint32_t hi = __builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false);  // s0*64 + s1
+        const uint32_t lo = __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);  // s2*64 + s3
+        G[g] = (hi << 12) | lo;
+        v |= ((ok * 0x10204080u) >> 28) << (4 * g);
+    }
+    valid = v;
+}
+
 // Fast path (a): a lane's 16 alphabet characters, as 4 groups, to 12 bytes.
 DEV void emit_full(const uint32_t G[4], uint8_t *out)
 {
@@ -2607,19 +2635,14 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
     const uint32_t nsep = !hs ? 0u : !last ? s : c > k ? 0u : (nspan - c < s ? nspan - c : s);
     const uint32_t need = sep_need(nsep);
     const bool sep_alpha = (sep_nonalpha(tab, sep) & need) != need;
-    if (!last) {
-        uint32_t bad;
-        map_fast(tab, d, 16, G, bad);
-        *j = 16;
-        return bad == 0 && !sep_alpha;
-    }
-    LaneChunk lc;
-    map_chunk_lds(tab, d, k, lc);
-    const uint32_t mk = lc.vmask;
-#pragma unroll
-    for (int g = 0; g < 4; g++) G[g] = lc.G[g];
+    // interior slots: all 16 alphabet; the last: the alphabet characters of
+    // its k model positions form a prefix (one rule, no branch: k = 16 for
+    // interior slots makes it "all 16")
+    uint32_t mk;
+    map_slot(tab, d, last ? k : 16u, G, mk);
     *j = __popc(mk);
-    return (mk & (mk + 1)) == 0 && !sep_alpha;  // alphabet characters form a prefix
+    const bool shape = last ? (mk & (mk + 1)) == 0 : mk == 0xFFFFu;
+    return shape && !sep_alpha;
 }
 
 // The row kernel.  Clean rows (the model's L = 0): the block's first slot
@@ -2633,8 +2656,12 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
 // marks go through atomicMax on the zeroed outlen[] as in k_decode_slots.
 // Line-structured rows: the same shape with the model's S, magic and m64,
 // and each slot's span (row_lines_slot).
+#ifndef B64X_ROWS_WPE  // A/B builds only: minimum waves per SIMD
+#define B64X_ROWS_WPE 1
+#endif
 template <int U>
-__global__ __launch_bounds__(kThreads) void k_decode_rows_lines(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
+void k_decode_rows_lines(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
     uint8_t *__restrict__ out, uint64_t out_stride,
     unsigned long long *__restrict__ outlen, uint32_t S, uint32_t magic, uint64_t m64,

@@ -68,6 +68,20 @@ def child(lib, steps):
     timeit("rows_enc", lambda: b64.encode_strided(xb, L, L, nb, eb, Es))
     timeit("rows_dec", lambda: b64.decode_strided(eb, Es, Es, nb, db, cap, ol))
     ok = ok and bool((ol == L).all()) and torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L))
+    # the same rows MIME-formatted (76-character lines, CRLF)
+    lines = (Es + 75) // 76
+    rows = eb.view(nb, Es)
+    if lines * 76 > Es:
+        rows = torch.cat([rows, torch.full((nb, lines * 76 - Es), 10, dtype=torch.uint8,
+                                           device="cuda")], dim=1)
+    crlf = torch.tensor([13, 10], dtype=torch.uint8, device="cuda").expand(nb, lines, 2)
+    D = lines * 78
+    mb = torch.cat([rows.reshape(nb, lines, 76), crlf], dim=2).reshape(-1).contiguous()
+    del rows, crlf
+    cap2 = 12 * ((D + 15) // 16)
+    db2 = torch.empty(nb * cap2, dtype=torch.uint8, device="cuda")
+    timeit("rows_crlf", lambda: b64.decode_strided(mb, D, D, nb, db2, cap2, ol))
+    ok = ok and bool((ol == L).all()) and torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L))
     print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
 
 
@@ -91,7 +105,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("encode", "decode", "crlf", "junk", "rows_enc", "rows_dec"):
+            for k in ("encode", "decode", "crlf", "junk", "rows_enc", "rows_dec", "rows_crlf"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
