@@ -2134,8 +2134,16 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // L2/MALL hits).  The last tile writes the result record, waits until every
 // tile is inclusive and every other block has drawn its final ticket, then
 // clears the status words, the ticket and the failure word.
+// At least 6 waves per SIMD (80 VGPRs; WHOLE took 96 and 5 waves): 1 GiB of
+// CRLF-76 under EXPECT_JUNK 998 -> 947 us, junk density 0.05 1045 -> 1026 us.
+// (Prefetching each range's chunks during the previous range's decode needed
+// 107 VGPRs and lost, with or without this bound.)
+#ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD
+#define B64X_SFX_WPE 6
+#endif
 template <bool WHOLE>
-__global__ __launch_bounds__(kThreads) void k_decode_suffix(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
+void k_decode_suffix(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres)
 {
@@ -2348,8 +2356,12 @@ DEV uint4 load_lane(const uint8_t *src, uint64_t p, uint64_t len, bool aligned, 
 // latency.  A buffer any of whose chunks needs the exact path is marked in
 // outlen[] for the fix-up.  RV: outlen[] receives the alphabet count V
 // instead of floor(6V/8) bytes (the hub's jobs, k_batch_finish).
+#ifndef B64X_BF_WPE  // A/B builds only: minimum waves per SIMD
+#define B64X_BF_WPE 1
+#endif
 template <bool RV>
-__global__ __launch_bounds__(kThreads) void k_decode_batch_fast(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_BF_WPE)))
+void k_decode_batch_fast(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
     uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
 {

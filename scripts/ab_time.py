@@ -55,6 +55,9 @@ def child(lib, steps):
     ok = ok and torch.equal(out[:n], x)
     timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
     ok = ok and torch.equal(out[:n], x)
+    timeit("crlf_ej", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr,
+                                         expect_junk=True))
+    ok = ok and torch.equal(out[:n], x)
     # config 4: 1 M x 1 KiB rows, strided decode (clean)
     del dirty, junk, enc, out, x
     nb, L = 1 << 20, 1024
@@ -82,6 +85,31 @@ def child(lib, steps):
     db2 = torch.empty(nb * cap2, dtype=torch.uint8, device="cuda")
     timeit("rows_crlf", lambda: b64.decode_strided(mb, D, D, nb, db2, cap2, ol))
     ok = ok and bool((ol == L).all()) and torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L))
+    # a ragged batch of 65,536 messages of 100-4,000 bytes (the hub's shape)
+    del mb, db2, db, eb, xb
+    g = torch.Generator().manual_seed(5)
+    lens = torch.randint(100, 4000, (65536,), generator=g, dtype=torch.int64)
+    ioff = torch.zeros(65537, dtype=torch.int64)
+    ioff[1:] = torch.cumsum(lens, 0)
+    elen = (lens + 2) // 3 * 4
+    eoff = torch.zeros(65537, dtype=torch.int64)
+    eoff[1:] = torch.cumsum(elen, 0)
+    xr = torch.empty(int(ioff[-1]), dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(xr, 7)
+    er = torch.empty(int(eoff[-1]), dtype=torch.uint8, device="cuda")
+    ioff_d, eoff_d = ioff.cuda(), eoff.cuda()
+    b64.encode_batch(xr, ioff_d, er, eoff_d)
+    cap = (elen + 3) // 4 * 3
+    doff = torch.zeros(65537, dtype=torch.int64)
+    doff[1:] = torch.cumsum(cap, 0)
+    dr = torch.empty(int(doff[-1]) + 16, dtype=torch.uint8, device="cuda")
+    doff_d = doff.cuda()
+    olr = torch.zeros(65536, dtype=torch.int64, device="cuda")
+    timeit("ragged_dec", lambda: b64.decode_batch(er, eoff_d, dr, doff_d[:-1], olr))
+    ok = ok and bool((olr.cpu() == lens).all())
+    for i in (0, 1, 777, 65535):
+        a0, d0 = int(ioff[i]), int(doff[i])
+        ok = ok and torch.equal(dr[d0:d0 + int(lens[i])], xr[a0:a0 + int(lens[i])])
     print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
 
 
@@ -105,7 +133,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("encode", "decode", "crlf", "junk", "rows_enc", "rows_dec", "rows_crlf"):
+            for k in ("encode", "decode", "crlf", "junk", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
