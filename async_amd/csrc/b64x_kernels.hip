@@ -758,32 +758,31 @@ DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
     lc.vmask = m;
 }
 
-// A slot's 16 characters of which the first k (0..16) count, for every
-// slot of a row alike (no per-lane branch between interior slots and a
-// row's last): G the four groups with characters outside the alphabet or
-// past k zeroed, *valid bit i set when character i counts and is in the
-// alphabet.  Per dword: four lookups packed into P, the in-alphabet bytes
-// (table values below 0x80) limited to k spread to byte flags, P masked by
-// them, the group by two v_dot4, the flags gathered by one multiply.
-DEV void map_slot(const uint8_t *tab, uint4 w, uint32_t k, uint32_t G[4], uint32_t &valid)
+// A row slot's 16 characters for the line-structured row kernel: G the four
+// groups with each non-alphabet character's sextet replaced by 0x3F, *im bit
+// i set when character i is not in the alphabet.  In a slot that passes, the
+// replaced sextets all sit after its alphabet prefix (j characters), so they
+// only reach output bits past its floor(6j/8) counted bytes.  Per dword: the
+// four table values packed, the group by two v_dot4 of their low 6 bits, the
+// bit-7s gathered by a third (no 32-bit multiply: those issue at a quarter
+// of the VALU rate, and map_slot's two per dword made the MIME rows VALU-bound).
+DEV void map_row_slot(const uint8_t *tab, uint4 w, uint32_t G[4], uint32_t &im)
 {
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
-    const uint32_t km = k >= 16 ? 0xFFFFu : (1u << k) - 1u;
-    uint32_t v = 0;
+    uint32_t m = 0;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
         const uint32_t P = (uint32_t) tab[dw[g] & 0xFFu] | ((uint32_t) tab[(dw[g] >> 8) & 0xFFu] << 8) |
                            ((uint32_t) tab[(dw[g] >> 16) & 0xFFu] << 16) |
                            ((uint32_t) tab[dw[g] >> 24] << 24);
-        const uint32_t kin = (((km >> (4 * g)) & 0xFu) * 0x00204081u) & 0x01010101u;
-        const uint32_t ok = ~(P >> 7) & kin;  // byte flags
-        const uint32_t Pz = P & (ok * 0xFFu);
+        const uint32_t Pz = P & 0x3F3F3F3Fu;
         const uint32_t hi = __builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false);  // s0*64 + s1
         const uint32_t lo = __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);  // s2*64 + s3
         G[g] = (hi << 12) | lo;
-        v |= ((ok * 0x10204080u) >> 28) << (4 * g);
+        // 128 x (the dword's 4-bit non-alphabet mask)
+        m |= __builtin_amdgcn_udot4(P & 0x80808080u, 0x08040201u, 0u, false) << (4 * g);
     }
-    valid = v;
+    im = m >> 7;
 }
 
 // Fast path (a): a lane's 16 alphabet characters, as 4 groups, to 12 bytes.
@@ -2577,7 +2576,7 @@ struct RowModel {
     uint64_t m64;           // ceil(2^64 / S)
     uint32_t F;             // model positions per row
     uint32_t m, k;          // i / L == (i * m) >> (31 + k)
-    uint32_t pad;
+    uint32_t mL;            // ceil(2^32 / L): i / L == umulhi(i, mL) for i < 2^24
 };
 static_assert(sizeof(RowModel) == 48, "RowModel layout");
 
@@ -2623,6 +2622,8 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
             r.F = F;
             r.k = 32 - __builtin_clz(L - 1);
             r.m = (uint32_t) ((((uint64_t) 1 << (31 + r.k)) + L - 1) / L);
+            // exact for i < 16 S <= 2^24: i (mL L - 2^32) < 2^24 * 252 < 2^32
+            r.mL = (uint32_t) ((0xFFFFFFFFull + L) / L);
         }
     }
     *row_model(ws) = r;
@@ -2650,10 +2651,12 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
     // interior slots: all 16 alphabet; the last: the alphabet characters of
     // its k model positions form a prefix (one rule, no branch: k = 16 for
     // interior slots makes it "all 16")
-    uint32_t mk;
-    map_slot(tab, d, last ? k : 16u, G, mk);
+    uint32_t im;
+    map_row_slot(tab, d, G, im);
+    const uint32_t kk = last ? k : 16u;
+    const uint32_t mk = ~im & (kk >= 16 ? 0xFFFFu : (1u << kk) - 1u);
     *j = __popc(mk);
-    const bool shape = last ? (mk & (mk + 1)) == 0 : mk == 0xFFFFu;
+    const bool shape = last ? (mk & (mk + 1)) == 0 : im == 0;
     return shape && !sep_alpha;
 }
 
@@ -2671,7 +2674,7 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
 #ifndef B64X_ROWS_WPE  // A/B builds only: minimum waves per SIMD
 #define B64X_ROWS_WPE 1
 #endif
-template <int U>
+template <int U, bool O32>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
 void k_decode_rows_lines(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
@@ -2699,6 +2702,7 @@ void k_decode_rows_lines(
         rm.F = (uint32_t) r4;
         rm.m = (uint32_t) (r4 >> 32);
         rm.k = (uint32_t) r5;
+        rm.mL = (uint32_t) (r5 >> 32);
         const uint32_t Sm = rm.S;
         const uint64_t ns_m = (uint64_t) Sm * nbuf;
         const uint64_t tail_m = (uint64_t) Sm * (nbuf - 1);
@@ -2720,12 +2724,16 @@ void k_decode_rows_lines(
             bl[u] = __umulhi(rel, rm.magic);
             qq[u] = rel - bl[u] * Sm;
             const uint32_t i = 16 * qq[u];
-            const uint32_t dl = (uint32_t) (((uint64_t) i * rm.m) >> (31 + rm.k));
+            const uint32_t dl = __umulhi(i, rm.mL);
             cl[u] = i - dl * rm.L;
             const uint32_t pos = dl * rm.P + cl[u];
             pp[u] = pos;
             oo[u] = pos & 3u;
-            const uint8_t *ab = ib + (uint64_t) bl[u] * in_stride + (pos & ~3u);
+            // O32: the block's rows lie within 2^31 bytes of its first and
+            // the strides below 2^24 (the launcher checks), so offsets are
+            // 32-bit from a uniform base and the products full-rate 24-bit
+            const uint8_t *ab = O32 ? ib + (__umul24(bl[u], (uint32_t) in_stride) + (pos & ~3u))
+                                    : ib + (uint64_t) bl[u] * in_stride + (pos & ~3u);
             if (!tail) {
                 win[u] = load16_a4(ab);
                 const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
@@ -2748,7 +2756,8 @@ void k_decode_rows_lines(
             const bool ok = row_lines_slot(tab, rm, w6, oo[u], cl[u], last, k, len - pos, G, &j);
             uint32_t o0, o1, o2;
             groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-            uint8_t *dst = ob + (uint64_t) bl[u] * out_stride + 12 * q;
+            uint8_t *dst = O32 ? ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u))
+                               : ob + (uint64_t) bl[u] * out_stride + 12 * q;
             unsigned long long *ol = olb + bl[u];
             const bool live = !tail || s0 + u * kThreads + threadIdx.x < ns_m;
             if (!tail) {
@@ -2813,7 +2822,9 @@ void k_decode_rows_lines(
     }
     uint4 w[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) w[u] = ld16<true>(ib + (uint64_t) bl[u] * in_stride + 16 * qq[u]);
+    for (int u = 0; u < U; u++)
+        w[u] = ld16<true>(O32 ? ib + (__umul24(bl[u], (uint32_t) in_stride) + 16 * qq[u])
+                              : ib + (uint64_t) bl[u] * in_stride + 16 * qq[u]);
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t q = qq[u];
@@ -2825,8 +2836,9 @@ void k_decode_rows_lines(
         if (last) ok = row_last_slot(tab, w[u], A, G, nlast, k);
         uint32_t o0, o1, o2;
         groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-        __builtin_nontemporal_store(u32x3a4{o0, o1, o2},
-                                    (u32x3a4 *) (ob + (uint64_t) bl[u] * out_stride + 12 * q));
+        uint8_t *dst = O32 ? ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u))
+                           : ob + (uint64_t) bl[u] * out_stride + 12 * q;
+        __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
         unsigned long long *ol = olb + bl[u];
         // only the first junk slot of each row in the wave marks it
         const uint64_t junk = __ballot(!ok);
@@ -3444,7 +3456,12 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                                (uint32_t) len, in_stride, a, ws);
             if ((err = launch_status())) return err;
             const dim3 g((uint32_t) ((slots + per - 1) / per));
-            hipLaunchKernelGGL(k_decode_rows_lines<U>, g, dim3(kThreads), 0, s,
+            // 32-bit offsets within a block's rows (relmax / S + 1 rows at most)
+            const uint64_t brows = relmax / S + 1;
+            const bool o32 = in_stride < (1u << 24) && out_stride < (1u << 24) &&
+                             brows * in_stride < (1ull << 31) && brows * out_stride < (1ull << 31);
+            hipLaunchKernelGGL((o32 ? k_decode_rows_lines<U, true> : k_decode_rows_lines<U, false>),
+                               g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, (uint32_t) len, (uint8_t *) d_out,
                                out_stride, (unsigned long long *) d_outlen, (uint32_t) S, magic, m64,
                                slots, tail_slot, a, nbuf, ws);
