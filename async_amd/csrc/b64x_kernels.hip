@@ -807,6 +807,20 @@ DEV void emit_full_a4(const uint32_t G[4], uint8_t *out)
         *p = u32x3a4{o0, o1, o2};
 }
 
+// emit_full_a4 at out + off, off a 32-bit byte offset (a uniform base plus a
+// 32-bit vector offset: no 64-bit address arithmetic per store)
+template <bool NT>
+DEV void emit_full_off(const uint32_t G[4], uint8_t *out, uint32_t off)
+{
+    uint32_t o0, o1, o2;
+    groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+    u32x3a4 *p = (u32x3a4 *) (out + off);
+    if (NT)
+        __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, p);
+    else
+        *p = u32x3a4{o0, o1, o2};
+}
+
 // Fast path (b), for the stream's final chunk when it starts on a group
 // boundary: if its alphabet characters form a prefix -- lanes 0..f-1 full,
 // lane f a prefix of its 16, no alphabet character after that (the shape
@@ -1750,7 +1764,11 @@ void k_decode_lines(
     m.skip = (uint32_t) (mw3 >> 32);
     const uint32_t lane = lane_id();
     const uint32_t L = m.L, s = m.s, P = m.P, T = m.T;
-    const uint32_t t0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kLinesSlots;
+    // the wave's first slot, made visibly wave-uniform: its line coordinates
+    // and output address are then scalar (a vector t0 cost a 64-bit
+    // multiply-add per slot store and a 32-bit multiply per wave)
+    const uint32_t wv = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
+    const uint32_t t0 = (blockIdx.x * kWavesPerBlock + wv) * kLinesSlots;
     if (t0 > T) return;
     const uint32_t ns = T - t0 >= kLinesSlots ? kLinesSlots : T - t0;  // interior slots here
     const bool full = ns == kLinesSlots;
@@ -1784,7 +1802,7 @@ void k_decode_lines(
                 fail_u = u;
                 fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
             }
-            emit_full_a4<true>(G, out + 12 * (uint64_t) (t0 + u * 64));
+            emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
         }
     } else if (ns && L != 0 && full && oal && ial && safe) {
         // The hot path of line-structured text: 32-bit offsets from the
@@ -1794,12 +1812,15 @@ void k_decode_lines(
         uint2 wx[kLinesU];
         uint32_t oo[kLinesU], cc[kLinesU];
         bool hs[kLinesU];
+        const uint32_t pos0 = line0 * P;  // wave-uniform
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
+            // rel < L + 4,096 and rcp < 2^16: 24-bit products (full rate;
+            // a 32-bit multiply issues at a quarter of it), exact
             const uint32_t rel = col0 + 16 * (u * 64 + lane);
-            const uint32_t dl = (rel * m.rcp) >> 20;
-            const uint32_t col = rel - dl * L;
-            const uint32_t pos = (line0 + dl) * P + col;
+            const uint32_t dl = __umul24(rel, m.rcp) >> 20;
+            const uint32_t col = rel - __umul24(dl, L);
+            const uint32_t pos = pos0 + __umul24(dl, P) + col;
             hs[u] = L - col <= 16;  // a line ends in (or right after) the slot
             cc[u] = hs[u] ? L - col : 16u;
             oo[u] = pos & 3u;
@@ -1824,7 +1845,7 @@ void k_decode_lines(
                 fail_u = u;
                 fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
             }
-            emit_full_a4<true>(G, out + 12 * (uint64_t) (t0 + u * 64));
+            emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
         }
     } else if (ns) {
         // Everything else (a partial wave, the input's end, misaligned

@@ -728,7 +728,8 @@ def _mime_batch(nbuf, n, L, sep, rng, deviants=()):
 
 
 @pytest.mark.parametrize("n,L,sep", [(1024, 76, b"\r\n"), (4096, 76, b"\r\n"), (1000, 64, b"\n"),
-                                     (777, 76, b"\r\n"), (3000, 19, b"\n"), (100, 16, b"\n\n")])
+                                     (777, 76, b"\r\n"), (3000, 19, b"\n"), (100, 16, b"\n\n"),
+                                     (22, 16, b"\n\n"), (40, 16, b"\r\n")])
 def test_strided_mime_rows_vs_oracle(n, L, sep):
     """MIME-formatted uniform batches (k_rows_prep's line model from row 0,
     k_decode_rows_lines): every row against the oracle, including rows that
