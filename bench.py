@@ -487,13 +487,21 @@ def bench_cfg5(args):
         # one untimed pass first: T loops' hubs, lanes (HIP streams) and pinned
         # arenas come from process-wide pools, filled on first use
         util.egress_stacks(payload, lens, 1 << 20, 10240, raw=True, threads=T)
-        times = np.zeros(2)
-        res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times, raw=True,
-                                      threads=T)
-        if res is None:
-            raise SystemExit(f"cfg5 egress failed: errno {err}")
+        # three timed passes, the median reported: the leg is host-bound and a
+        # single pass varied 2x from box to box (profiles/README.md, r02_v25)
+        passes = []
+        for _ in range(3):
+            times = np.zeros(2)
+            res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times,
+                                          raw=True, threads=T)
+            if res is None:
+                raise SystemExit(f"cfg5 egress failed: errno {err}")
+            passes.append((float(times.sum()), times.copy()))
+            if len(passes) < 3:
+                del res
+        passes.sort(key=lambda p: p[0])
+        dt, times = passes[1]
         framed, f_off, f_len = res
-        dt = float(times.sum())
 
         def work(t, T=T):
             cuts = np.searchsorted(offs, np.linspace(0, nbytes, T + 1))
@@ -510,6 +518,7 @@ def bench_cfg5(args):
             if framed[int(f_off[i]):int(f_off[i]) + int(f_len[i])].tobytes() != want:
                 raise SystemExit(f"cfg5 egress mismatch at message {i}")
         out[f"loops_{T}"] = {"GiB_s": nbytes / dt / 2**30, "seconds": dt,
+                             "GiB_s_passes": [nbytes / p[0] / 2**30 for p in passes],
                              "setup_s": float(times[0]), "loop_s": float(times[1]),
                              "framed_bytes": int(f_len.sum()),
                              "cpu_port_GiB_s": nbytes / cpu_dt / 2**30, "cpu_threads": T}
