@@ -2152,7 +2152,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // predecessors' status words as k_decode_scan2 does, then each wave decodes
 // its ranges with decode_range, re-reading them (the tile was just read:
 // L2/MALL hits).  The last tile writes the result record, waits until every
-// tile is inclusive and every other block has drawn its final ticket, then
+// other block has drawn its final ticket (so every look-back is over), then
 // clears the status words, the ticket and the failure word.
 // At least 6 waves per SIMD (80 VGPRs; WHOLE took 96 and 5 waves): 1 GiB of
 // CRLF-76 under EXPECT_JUNK 998 -> 947 us, junk density 0.05 1045 -> 1026 us.
@@ -2311,20 +2311,21 @@ void k_decode_suffix(
                 const uint64_t V = Vb + s_excl + s_agg;
                 if (lane == 0) write_result(res, hres, V, hold);
                 find_tail_sextets(sm.tab, in, n, V, res, hres);
-                for (;;) {  // every tile inclusive -> every look-back is over
-                    bool all = true;
-                    for (uint32_t i = lane; i < ntiles; i += 64)
-                        all = all && (st_load(&w.fstatus[i]) >> 62) == 2;
-                    if (__all(all)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+                // Every other block has drawn its final ticket -> every
+                // look-back is over (a block draws its next ticket only after
+                // finishing its tile, look-back included), so the status words
+                // can be cleared and the ticket re-armed.  (This used to wait
+                // for every status word to read inclusive first: one dependent
+                // device-scope load per 64 tiles, ~170 round trips per GiB at
+                // the end of every call, and redundant with the ticket.)
                 if (lane == 0) {
-                    // every other block has drawn its final ticket -> re-arm
                     const uint32_t want = ntiles + gridDim.x - 1;
                     while (__hip_atomic_load(w.fticket, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT) != want)
                         __builtin_amdgcn_s_sleep(1);
+                }
+                for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+                if (lane == 0) {
                     __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (!WHOLE)
                         for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
