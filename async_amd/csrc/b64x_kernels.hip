@@ -905,8 +905,11 @@ struct DecodeWs {
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
-constexpr uint32_t kFusePer = 16;     // ranges per wave in the single-pass decode
-constexpr uint32_t kFuseLoad = 4;     // of them loaded at once for counting
+#ifndef B64X_FUSE_PER  // A/B builds only
+#define B64X_FUSE_PER 16
+#endif
+constexpr uint32_t kFusePer = B64X_FUSE_PER;  // ranges per wave in the single-pass decode
+constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
