@@ -910,6 +910,10 @@ constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 #endif
 constexpr uint32_t kFusePer = B64X_FUSE_PER;  // ranges per wave in the single-pass decode
 constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
+#ifndef B64X_FUSE_HOLD  // A/B builds only
+#define B64X_FUSE_HOLD 0
+#endif
+constexpr bool kFuseHold = B64X_FUSE_HOLD;
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
@@ -2229,6 +2233,10 @@ void k_decode_suffix(
         if (t >= ntiles) return;
         const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
         // counts; all of the wave's loads are issued before any is counted
+        // HOLD: the wave's ranges all fit one load group; its chunks stay in
+        // registers for the decode instead of being re-read (B64X_FUSE_HOLD)
+        constexpr bool kHold = kFuseHold && kFusePer <= kFuseLoad;
+        uint4 hc[kHold ? kFuseLoad : 1][2];
         for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
             uint4 c[kFuseLoad][2];
             uint32_t nin[kFuseLoad][2];
@@ -2258,6 +2266,13 @@ void k_decode_suffix(
                 }
                 cnt = wave_sum(cnt);
                 if (lane == 0) s_cnt[wv * kFusePer + j0 + jj] = cnt;
+            }
+            if constexpr (kHold) {
+#pragma unroll
+                for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+                    hc[jj][0] = c[jj][0];
+                    hc[jj][1] = c[jj][1];
+                }
             }
         }
         __syncthreads();
@@ -2295,6 +2310,29 @@ void k_decode_suffix(
         __syncthreads();
         uint64_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
         for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
+        if constexpr (kHold) {
+            // the wave's ranges from the chunks held since the count
+#pragma unroll
+            for (uint32_t j = 0; j < kFusePer; j++) {
+                const uint32_t r = rw + j;
+                if (r >= nranges) break;
+                const uint64_t rb = (uint64_t) r * R;
+                const uint64_t re = rb + R < n ? rb + R : n;
+                const bool first = r == r0, last = r + 1 == nranges;
+                const uint64_t start = first ? S : rb;
+                uint32_t nin[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                }
+                const bool la_ok = !last && re + lane < n;
+                const uint32_t la = la_ok ? base_in[re + lane] : 0u;
+                decode_range(sm, bq, base_in, n, start, re, first ? 0 : range_skip(B),
+                             base_out + (B + 3) / 4 * 3, hc[j], nin, la, la_ok, last, hold);
+                B += s_cnt[wv * kFusePer + j];
+            }
+        } else {
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
             const uint64_t rb = (uint64_t) r * R;
@@ -2308,6 +2346,7 @@ void k_decode_suffix(
             decode_range(sm, bq, base_in, n, start, re, first ? 0 : range_skip(B),
                          base_out + (B + 3) / 4 * 3, c, nin, la, la_ok, last, hold);
             B += s_cnt[wv * kFusePer + j];
+        }
         }
         if (t == ntiles - 1) {
             if (wv == 0) {
