@@ -868,6 +868,10 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //           ~(first failing slot) of k_decode_lines, published by each wave
 //           into word (block mod kFailWords) so that failing waves do not all
 //           read one line; 0 = none (cleared by k_decode_suffix)
+//   fail_any  nonzero when any failure word was published (set by the probe
+//           and by the first publisher into a word, which sees it zero;
+//           cleared by k_decode_suffix): the idle suffix kernel's one
+//           scalar load instead of a wave reading all 64 words per block
 //   model   the line model k_decode_probe found, for k_decode_lines and
 //           k_decode_suffix
 //   fticket, fstatus  k_decode_suffix's tile ticket and status words
@@ -892,6 +896,7 @@ static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of m
 
 struct DecodeWs {
     uint64_t *lfail;     // kFailWords words, kFailStride apart
+    uint64_t *fail_any;  // nonzero: some failure word was published (own line)
     LineModel *model;    // k_decode_lines' model, for k_decode_suffix
     uint64_t *fd;
     uint64_t *fd_cur;
@@ -920,7 +925,7 @@ constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsStatus = 64;                                        // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
 constexpr uint64_t kWsFail = kWsFStatus + kMaxRanges / kFuseTile * 8;     // lines failures
-constexpr uint64_t kWsScratch = kWsFail + kFailWords * kFailStride * 8;   // counts, bases
+constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 1) * kFailStride * 8;  // counts, bases
 
 // Layout: 64-byte header (fd, fd_cur, ticket, fticket, sfx_start, model), the
 // zero-between-calls regions at fixed offsets, then the scratch counts and
@@ -938,6 +943,7 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.status = (uint64_t *) (p + kWsStatus);
     w.fstatus = (uint64_t *) (p + kWsFStatus);
     w.lfail = (uint64_t *) (p + kWsFail);
+    w.fail_any = w.lfail + kFailWords * kFailStride;
     w.counts = (uint32_t *) (p + kWsScratch);
     w.bases = (uint64_t *) (p + kWsScratch + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     return w;
@@ -1724,6 +1730,7 @@ __global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__
         m.T = pj / 16;
         m.skip = 1;
         *ws_view(ws, nranges).lfail = ~(uint64_t) m.T;
+        *ws_view(ws, nranges).fail_any = 1;
     } else if (m.L == 0) {
         m.T = n32 / 16;
     } else {
@@ -1911,6 +1918,9 @@ void k_decode_lines(
         const unsigned long long cur =
             __hip_atomic_load(lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (key > cur) atomicMax(lf, key);
+        // the first publisher into a word sees it zero (at most a few racing
+        // ones do): they raise the summary the idle suffix kernel reads
+        if (cur == 0) *ws_view(ws, nranges).fail_any = 1;
     }
     if (T >= t0 + kLinesSlots || m.skip) return;
     // This wave owns slot T: the < 16 + s bytes after the last interior
@@ -2178,6 +2188,20 @@ void k_decode_suffix(
     DecodeWs w = ws_view(ws, nranges);
     uint64_t S = 0, Vb = 0;
     if (!WHOLE) {
+        if (scalar_load_u64(w.fail_any) == 0) {
+            // nothing failed (the common case; one scalar load per block):
+            // k_decode_lines took everything and its record is final.  The
+            // host mirror is written only now, so a completion never finds a
+            // consistent but provisional record there.
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                if (hres) {
+                    const b64x_dec_result r = *res;
+                    *hres = r;
+                }
+                *w.sfx_start = ~0ull;
+            }
+            return;
+        }
         // the first failing slot: the largest key over the failure words
         // (one wave reads them all, every block)
         uint64_t key = 0;
@@ -2371,6 +2395,7 @@ void k_decode_suffix(
                     __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (!WHOLE)
                         for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
+                    if (!WHOLE) *w.fail_any = 0;
                 }
             }
             return;  // this block draws no further ticket
