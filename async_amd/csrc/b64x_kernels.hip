@@ -3440,7 +3440,10 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
         static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
-        const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
+#ifndef B64X_SFX_OCC  // A/B builds only: blocks per CU of the suffix grid (0: occupancy)
+#define B64X_SFX_OCC 0
+#endif
+        const uint32_t sfx_grid = (uint32_t) d->cus * (B64X_SFX_OCC ? B64X_SFX_OCC : occ_sfx);
         if (flags & B64X_DEC_EXPECT_JUNK) {
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
