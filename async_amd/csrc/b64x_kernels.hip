@@ -4315,8 +4315,8 @@ uint64_t b64x__test_range_chunks(uint64_t chunks)
 
 const char *b64x_build_info(void)
 {
-    return "b64x abi=1 arch=gfx950 enc:quad12->16 lds-alphabet unroll=4; "
-           "dec:wave-range chunk=1024 lds-inverse-table 2-pass-fixup";
+    return "b64x abi=1 arch=gfx950 enc:quad12->16 bpermute-alphabet unroll=4; "
+           "dec:probe+line-model single pass (4 slots/lane) + exact suffix (look-back)";
 }
 
 const char *b64x_strerror(int err)
