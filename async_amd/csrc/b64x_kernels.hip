@@ -2683,7 +2683,10 @@ static_assert(sizeof(RowModel) == 48, "RowModel layout");
 // uses for its per-range counts (scratch between calls).
 DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + kWsScratch); }
 
-constexpr uint32_t kRowsU = 4;  // slots per lane of the row kernels
+#ifndef B64X_ROWS_U  // A/B builds only
+#define B64X_ROWS_U 4
+#endif
+constexpr uint32_t kRowsU = B64X_ROWS_U;  // slots per lane of the row kernels
 
 __global__ __launch_bounds__(kThreads) void k_rows_prep(
     uint64_t *__restrict__ outlen, uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len,
