@@ -765,7 +765,7 @@ DEV void map_chunk_lds(const uint8_t *tab, uint4 w, uint32_t nin, LaneChunk &lc)
 // only reach output bits past its floor(6j/8) counted bytes.  Per dword: the
 // four table values packed, the group by two v_dot4 of their low 6 bits, the
 // bit-7s gathered by a third (no 32-bit multiply: those issue at a quarter
-// of the VALU rate, and map_slot's two per dword made the MIME rows VALU-bound).
+// of the VALU rate, and the first form's two per dword made the MIME rows VALU-bound).
 DEV void map_row_slot(const uint8_t *tab, uint4 w, uint32_t G[4], uint32_t &im)
 {
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
