@@ -69,3 +69,25 @@ def exchange_totals(local_total: int, device=None) -> tuple[int, list[int]]:
     dist.all_gather_into_tensor(allt, mine)
     totals = [int(v) for v in allt.cpu().tolist()]
     return sum(totals[:rank]), totals
+
+
+def ranks_for(kernel_s: float, world: int, exchange_s: float, max_overhead: float = 0.1) -> int:
+    """How many of `world` ranks a batch should be sharded over (SURVEY.md
+    §8(e): shard "only when the batch is large enough to amortise").
+
+    `kernel_s` is the batch's kernel time on one GPU (it splits evenly:
+    the buffers are independent and resident per rank), `exchange_s` the
+    one collective's latency (all-gather of a few bytes; `bench.py` measures
+    it).  Each rank's share must keep the exchange within `max_overhead` of
+    its own kernel time, so n <= kernel_s * max_overhead / exchange_s.
+    Moving the buffers to the ranks first (root-scatter) never pays here:
+    the transform runs faster than xGMI moves its bytes (`bench.py`'s
+    root_scatter leg).
+    """
+    if world <= 1:
+        return 1
+    if exchange_s <= 0:  # a free exchange: every rank
+        return world
+    n = int(kernel_s * max_overhead / exchange_s)
+    return max(1, min(world, n))
+

@@ -255,6 +255,18 @@ def bench_batch(args, world, rank, b64):
     kern_ms = ev[0].elapsed_time(ev[2]) / K
     rank_frac = (2 * (nbuf * (L + Es))) / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
     per_rank = gather_floats([nbuf * L * K / mine / 2**30, rank_frac], world)
+    # the exchange step on its own (after the timed region): its latency
+    # decides how many ranks a batch of this size amortises (shard.ranks_for)
+    exchange_ms, advice = None, None
+    if world > 1:
+        ts = []
+        for _ in range(10):
+            sync_all(world)
+            t1 = time.perf_counter()
+            shard.exchange_totals(int(outlen.sum()), device=coll_device())
+            ts.append(time.perf_counter() - t1)
+        exchange_ms = max_over_ranks(statistics.median(ts), world) * 1e3
+        advice = shard.ranks_for(kern_ms * 1e-3 * world, world, exchange_ms * 1e-3)
     return {
         "workload": "cfg4: 1,048,576 x 1 KiB buffers split across ranks, strided "
                     "encode then decode, + allgather of per-rank output totals",
@@ -267,6 +279,8 @@ def bench_batch(args, world, rank, b64):
         "roofline_frac": rank_frac,
         "per_rank_GiB_s": [p[0] for p in per_rank],
         "per_rank_roofline_frac": [p[1] for p in per_rank],
+        "exchange_ms": exchange_ms,
+        "ranks_amortised": advice,
     }
 
 

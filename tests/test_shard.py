@@ -86,6 +86,18 @@ def test_gloo_exchange(world):
     assert whole == want
 
 
+def test_ranks_for_amortises_the_exchange():
+    # 1 GiB round trip on one MI355X ~0.8 ms; a 20 us exchange at 10 %
+    # overhead justifies 4 ranks, 8 only from 1.6 ms of work
+    assert shard.ranks_for(0.8e-3, 8, 20e-6) == 4
+    assert shard.ranks_for(1.6e-3, 8, 20e-6) == 8
+    assert shard.ranks_for(100e-3, 8, 20e-6) == 8      # never more than the world
+    assert shard.ranks_for(10e-6, 8, 20e-6) == 1       # tiny batches stay on one GPU
+    assert shard.ranks_for(0.8e-3, 1, 20e-6) == 1
+    assert shard.ranks_for(0.8e-3, 8, 0.0) == 8
+    assert shard.ranks_for(0.8e-3, 8, 20e-6, max_overhead=0.05) == 2
+
+
 def test_single_process_exchange():
     assert shard.exchange_totals(123) == (0, [123])
     assert torch.tensor([1]).sum() == 1
