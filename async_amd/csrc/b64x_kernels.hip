@@ -1548,6 +1548,9 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
 #ifndef B64X_LINES_U  // A/B builds only (scripts/ab_variants.sh)
 #define B64X_LINES_U 4
 #endif
+#ifndef B64X_LINES_NTL  // A/B builds only: non-temporal window loads on line-structured text
+#define B64X_LINES_NTL false
+#endif
 constexpr uint32_t kLinesU = B64X_LINES_U;          // slots per lane (2: +1-3 %, 8: +7 %)
 constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
 constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
@@ -1849,7 +1852,7 @@ void k_decode_lines(
             cc[u] = hs[u] ? L - col : 16u;
             oo[u] = pos & 3u;
             const uint8_t *ab = in + (pos & ~3u);
-            win[u] = load16_a4(ab);
+            win[u] = ld16<B64X_LINES_NTL>(ab);
             const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
             wx[u] = make_uint2(v.x, v.y);
         }
