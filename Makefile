@@ -24,16 +24,17 @@ HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC 
 CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
 
 LIB      = async_amd/libasync_b64.so
-# Stages + kernels only (no event loop/streams): the drop-in for a build of
-# the reference library, which supplies async_wound() and the streams.
+# Stages + kernels only (no event loop/streams/allocator): the drop-in for a
+# build of the reference library, which supplies async_wound(), the streams
+# and (through fsdyn) fsalloc()/fsfree().
 CORE     = async_amd/libasync_b64_core.so
 ORACLE   = oracle/liboracle.so
 HARNESS  = tests/csrc/libstage_harness.so
 OBJDIR   = build
 
 KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
-HOST_SRC   = async_amd/csrc/loop.c async_amd/csrc/streams.c async_amd/csrc/framing.c \
-             async_amd/csrc/b64_hub.c async_amd/csrc/b64_stages.c
+HOST_SRC   = async_amd/csrc/fsalloc.c async_amd/csrc/loop.c async_amd/csrc/streams.c \
+             async_amd/csrc/framing.c async_amd/csrc/b64_hub.c async_amd/csrc/b64_stages.c
 HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))

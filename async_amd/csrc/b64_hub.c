@@ -12,9 +12,19 @@
  * publishes the flag and writes the eventfd.  The registry that maps an
  * async_t to its hub is the only state shared between threads (loops on
  * different threads each get their own hub) and is mutex-protected.
+ *
+ * Life of a hub: the first stage of a loop that starts work acquires it;
+ * when the last one releases it, it is torn down at once (lanes waited
+ * for, arenas back to the pool, eventfd unregistered) unless the loop is
+ * inside one of its actions, which then tears it down on the way out.  Its
+ * memory comes from fsalloc() and goes through async_wound(): a flush or
+ * kick task already queued on the loop still finds it (and sees it dead),
+ * and a loop destroyed before those tasks run frees it all the same
+ * (destroy_async() frees wounded objects, ref src/async.c:140-162).
  */
 #define _GNU_SOURCE
 #include "b64_hub.h"
+#include "fsalloc.h"
 
 #include <errno.h>
 #include <pthread.h>
@@ -29,11 +39,13 @@ enum {
     HUB_LANES = 4,          /* batches in flight per loop */
     HUB_MAX_LIVE = HUB_LANES + 4, /* arenas a hub holds before idle
                                      stages are made to wait */
-    POOL_MAX = 128,         /* idle arenas kept process-wide for reuse (~41 MB
-                               pinned each; 16 loops on one GPU hold ~50 at
-                               once, and every arena freed and allocated again
-                               costs milliseconds of pinned-memory calls that
-                               stall the other loops) */
+    POOL_MAX = 128,         /* default of ASYNC_B64_POOL_MAX: idle arenas kept
+                               process-wide for reuse (~41 MB pinned each at
+                               the default ASYNC_B64_BATCH_BYTES; 16 loops on
+                               one GPU hold ~50 at once, and every arena freed
+                               and allocated again costs milliseconds of
+                               pinned-memory calls that stall the other
+                               loops) */
     HUB_JOBS = 1 << 16,     /* jobs per arena */
     HUB_DEPTH = 8,          /* reservations open at once (stages reading
                                through stages, see b64_hub_reserve) */
@@ -73,7 +85,10 @@ struct b64_hub {
     unsigned inflight;
     unsigned live;               /* arenas taken from the pool */
     size_t batch_bytes;
-    bool flush_scheduled, kick_scheduled, in_wake, doomed;
+    bool flush_scheduled, kick_scheduled; /* a task of ours is queued */
+    bool in_wake, in_kick;       /* inside hub_wake() / hub_kick() */
+    bool doomed;                 /* no users: torn down when not inside */
+    bool dead;                   /* torn down; memory awaits async_wound() */
     action_1 *wakes;             /* scratch for hub_wake() */
     size_t nwakes, wakes_cap;
     action_1 *waiters;           /* idle stages waiting for an arena */
@@ -103,6 +118,8 @@ static b64_hub *registry;
 static pthread_mutex_t pool_lock = PTHREAD_MUTEX_INITIALIZER;
 static b64_batch *pool;
 static unsigned npool;
+static unsigned pool_max = POOL_MAX;
+static pthread_once_t pool_once = PTHREAD_ONCE_INIT;
 
 static size_t env_bytes(const char *name, size_t dflt, size_t lo)
 {
@@ -112,6 +129,11 @@ static size_t env_bytes(const char *name, size_t dflt, size_t lo)
     char *end = NULL;
     unsigned long long x = strtoull(v, &end, 0);
     return (!end || *end || x < lo) ? dflt : (size_t) x;
+}
+
+static void pool_init(void)
+{
+    pool_max = (unsigned) env_bytes("ASYNC_B64_POOL_MAX", POOL_MAX, 0);
 }
 
 /* ---------------------------------------------------------------- batches */
@@ -164,8 +186,9 @@ static void batch_put(b64_batch *b)
     b->err = 0;
     b->hub = NULL;
     atomic_store_explicit(&b->done, 0, memory_order_relaxed);
+    pthread_once(&pool_once, pool_init);
     pthread_mutex_lock(&pool_lock);
-    if (npool < POOL_MAX) {
+    if (npool < pool_max) {
         b->next = pool;
         pool = b;
         npool++;
@@ -266,6 +289,10 @@ static void launch_ready(b64_hub *h)
                      : b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
                                               b->h_out, b->h_out_off, &b->abc, batch_done, b);
         if (rc) { /* report through the normal completion path */
+            /* work queued before the failure may still write into the
+             * arena: wait for it, so the arena is idle when it is recycled */
+            if (h->lanes[i])
+                (void) b64x_lane_wait(h->lanes[i]);
             b->err = rc;
             batch_done(b);
         }
@@ -282,22 +309,20 @@ static void launch_ready(b64_hub *h)
         h->tr.launch_s += mono_s() - t0;
 }
 
-static void hub_destroy(b64_hub *h);
+static void hub_teardown(b64_hub *h);
 
-/* A doomed hub goes once nothing scheduled on the loop refers to it. */
-static bool hub_idle(const b64_hub *h)
+/* A doomed hub is torn down as soon as none of its actions is running. */
+static void hub_maybe_teardown(b64_hub *h)
 {
-    return !h->in_wake && !h->flush_scheduled && !h->kick_scheduled;
+    if (h->doomed && !h->dead && !h->in_wake && !h->in_kick)
+        hub_teardown(h);
 }
 
 static void hub_flush(b64_hub *h)
 {
     h->flush_scheduled = false;
-    if (h->doomed) {
-        if (hub_idle(h))
-            hub_destroy(h);
+    if (h->dead || h->doomed)
         return;
-    }
     for (unsigned l = 0; l < HUB_DEPTH; l++)
         if (h->filling[l] && h->filling[l]->njobs && l >= h->depth)
             seal(h, l);
@@ -306,7 +331,7 @@ static void hub_flush(b64_hub *h)
 
 static void schedule_flush(b64_hub *h)
 {
-    if (h->flush_scheduled)
+    if (h->flush_scheduled || h->dead)
         return;
     h->flush_scheduled = true;
     async_execute(h->async, (action_1) { h, (act_1) hub_flush });
@@ -317,11 +342,8 @@ static void schedule_flush(b64_hub *h)
 static void hub_kick(b64_hub *h)
 {
     h->kick_scheduled = false;
-    if (h->doomed) {
-        if (hub_idle(h))
-            hub_destroy(h);
+    if (h->dead || h->doomed)
         return;
-    }
     /* Oldest first, and only until one of them still finds no room (it
      * re-queues itself): waking thousands of stages for one free arena
      * would cost a retry each. */
@@ -331,6 +353,7 @@ static void hub_kick(b64_hub *h)
     h->nwaiters = h->waiters_cap = 0;
     h->kicking = w;
     h->nkicking = n;
+    h->in_kick = true;
     size_t i = 0;
     while (i < n && !h->doomed) {
         action_1 a = w[i++];
@@ -342,7 +365,8 @@ static void hub_kick(b64_hub *h)
     }
     h->kicking = NULL;
     h->nkicking = 0;
-    for (; i < n; i++) { /* the rest keep their place */
+    h->in_kick = false;
+    for (; i < n && !h->doomed; i++) { /* the rest keep their place */
         if (!w[i].act)
             continue;
         if (h->nwaiters == h->waiters_cap) {
@@ -356,11 +380,12 @@ static void hub_kick(b64_hub *h)
         h->waiters[h->nwaiters++] = w[i];
     }
     free(w);
+    hub_maybe_teardown(h);
 }
 
 static void schedule_kick(b64_hub *h)
 {
-    if (h->kick_scheduled || h->doomed)
+    if (h->kick_scheduled || h->doomed || h->dead)
         return;
     h->kick_scheduled = true;
     async_execute(h->async, (action_1) { h, (act_1) hub_kick });
@@ -408,6 +433,8 @@ static void hub_wake(b64_hub *h)
      * write is a fresh edge; batch_done() publishes `done` before it
      * writes, so every batch whose write this read consumed is seen done
      * below. */
+    if (h->dead)
+        return;
     uint64_t v;
     while (read(h->efd, &v, sizeof v) == (ssize_t) sizeof v)
         ;
@@ -443,8 +470,7 @@ static void hub_wake(b64_hub *h)
         h->tr.t_last = mono_s();
         h->tr.wake_s += h->tr.t_last - t0;
     }
-    if (h->doomed && hub_idle(h))
-        hub_destroy(h);
+    hub_maybe_teardown(h);
 }
 
 /* ------------------------------------------------------------- lifecycle */
@@ -459,12 +485,7 @@ b64_hub *b64_hub_acquire(async_t *async)
             return h;
         }
     }
-    b64_hub *h = calloc(1, sizeof *h);
-    if (!h) {
-        pthread_mutex_unlock(&registry_lock);
-        errno = ENOMEM;
-        return NULL;
-    }
+    b64_hub *h = fscalloc(1, sizeof *h);
     h->async = async;
     h->batch_bytes = env_bytes("ASYNC_B64_BATCH_BYTES", (size_t) 16 << 20, 4096);
     h->tr.on = env_bytes("ASYNC_B64_HUB_TRACE", 0, 0) != 0;
@@ -474,7 +495,7 @@ b64_hub *b64_hub_acquire(async_t *async)
         int e = errno ? errno : EIO;
         if (h->efd >= 0)
             close(h->efd);
-        free(h);
+        fsfree(h);
         pthread_mutex_unlock(&registry_lock);
         errno = e;
         return NULL;
@@ -486,8 +507,9 @@ b64_hub *b64_hub_acquire(async_t *async)
     return h;
 }
 
-static void hub_destroy(b64_hub *h)
+static void hub_teardown(b64_hub *h)
 {
+    h->dead = true;
     if (h->tr.on)
         fprintf(stderr,
                 "b64_hub: batches %lu jobs %lu in %llu out %llu allocs %lu "
@@ -522,9 +544,12 @@ static void hub_destroy(b64_hub *h)
     }
     (void) async_unregister(h->async, h->efd);
     close(h->efd);
+    h->efd = -1;
     free(h->wakes);
     free(h->waiters);
-    free(h);
+    h->wakes = h->waiters = NULL;
+    h->nwakes = h->nwaiters = h->wakes_cap = h->waiters_cap = 0;
+    async_wound(h->async, h);
 }
 
 void b64_hub_release(b64_hub *h)
@@ -534,8 +559,7 @@ void b64_hub_release(b64_hub *h)
     pthread_mutex_lock(&registry_lock);
     h->doomed = true; /* no new stage may pick it up */
     pthread_mutex_unlock(&registry_lock);
-    if (hub_idle(h))
-        hub_destroy(h);
+    hub_maybe_teardown(h);
 }
 
 void b64_hub_forget(b64_hub *h, void *obj, bool waiting)

@@ -78,6 +78,7 @@
 #include "b64x.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
+#include "fsalloc.h"
 
 enum {
     NSLOTS = 4,   /* blocks in flight or staged per stage (read-ahead) */
@@ -516,10 +517,8 @@ static size_t serve_body(stage *st, uint8_t *dst, size_t n)
     uint8_t *spill = NULL;
     if (!dst) { /* a lending read without a fallback: the stage's own buffer */
         if (st->spill_cap < n) {
-            free(st->spill);
-            st->spill = malloc(n);
-            if (!st->spill)
-                abort(); /* like fsalloc: allocation failure is fatal */
+            fsfree(st->spill);
+            st->spill = fsalloc(n);
             st->spill_cap = n;
         }
         dst = spill = st->spill;
@@ -639,10 +638,14 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
     }
 }
 
+/* Ownership: the object came from fsalloc() and goes back
+ * through async_wound() -> fsfree() on a later loop turn, so posthumous
+ * callbacks (a hub wake already collected for this stage) find it valid;
+ * everything else the stage holds is given back here. */
 static void stage_close(stage *st)
 {
     st->lent = NULL;
-    free(st->spill);
+    fsfree(st->spill);
     st->spill = NULL;
     st->spill_cap = 0;
     stage_stop(st);
@@ -679,9 +682,7 @@ struct base64encoder {
 base64encoder_t *base64_encode(async_t *async, bytestream_1 stream, char pos62,
                                char pos63, bool pad, char padchar)
 {
-    base64encoder_t *e = malloc(sizeof *e);
-    if (!e)
-        abort();
+    base64encoder_t *e = fsalloc(sizeof *e); /* ref base64encoder.c:33 */
     b64x_alphabet abc = { pos62, pos63, padchar, pad };
     stage_init(&e->st, async, stream, DIR_ENCODE, abc);
     FSTRACE(ASYNC_BASE64ENCODER_CREATE, e->st.uid, e, async, stream.obj);
@@ -782,9 +783,7 @@ struct base64decoder {
 base64decoder_t *base64_decode(async_t *async, bytestream_1 stream, char pos62,
                                char pos63)
 {
-    base64decoder_t *d = malloc(sizeof *d);
-    if (!d)
-        abort();
+    base64decoder_t *d = fsalloc(sizeof *d); /* ref base64decoder.c:25 */
     b64x_alphabet abc = { pos62, pos63, (char) -1, false };
     stage_init(&d->st, async, stream, DIR_DECODE, abc);
     FSTRACE(ASYNC_BASE64DECODER_CREATE, d->st.uid, d, async, stream.obj);

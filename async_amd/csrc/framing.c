@@ -7,8 +7,9 @@
  *   queuestream (messages) -> base64_encode (GPU stage) -> chunk_encode
  *
  * Written from the behaviour the headers restate (ref src/queuestream.c,
- * src/chunkencoder.c); objects are freed through async_wound() like the
- * reference's, so callbacks arriving after close() find valid memory.
+ * src/chunkencoder.c); objects come from fsalloc() and are freed through
+ * async_wound() like the reference's (include/fsalloc.h), so callbacks
+ * arriving after close() find valid memory.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -20,14 +21,12 @@
 #include "b64_lend.h"
 #include "blobstream.h"
 #include "chunkencoder.h"
+#include "fsalloc.h"
 #include "queuestream.h"
 
 static void *xmalloc(size_t size)
 {
-    void *p = malloc(size ? size : 1);
-    if (!p)
-        abort(); /* fsalloc semantics: allocation failure is fatal */
-    return p;
+    return fsalloc(size);
 }
 
 /* ================================================================ queue */
@@ -146,7 +145,7 @@ static void queue_drop_first(queuestream_t *q)
     if (!q->first)
         q->last = NULL;
     bytestream_1_close(n->stream);
-    free(n);
+    fsfree(n);
 }
 
 ssize_t queuestream_read(queuestream_t *q, void *buf, size_t count)
@@ -359,7 +358,7 @@ void chunkencoder_close(chunkencoder_t *c)
 {
     c->data = NULL; /* the stage's close ends the loan */
     bytestream_1_close(c->up);
-    free(c->frame);
+    fsfree(c->frame);
     c->frame = NULL;
     async_wound(c->async, c);
     c->async = NULL;

@@ -13,8 +13,11 @@
  *    when tens of thousands of streams share a loop; task records are
  *    recycled through a free list;
  *  - async_wound() queues the object and schedules a task that frees the
- *    oldest wounded object, so a free happens only after every task that
- *    was already scheduled (ref src/async.c:386-392);
+ *    oldest wounded object with fsfree(), so a free happens only after
+ *    every task that was already scheduled (ref src/async.c:386-392);
+ *    destroy_async() frees the ones still queued (ref :140-162).  Every
+ *    object of the loop itself comes from fsalloc() (include/fsalloc.h),
+ *    so a counting allocator sees the loop's objects come and go;
  *  - at most kBurst due tasks run before the loop polls file descriptors
  *    (ref take_immediate_action, src/async.c:564-590, uses 20);
  *  - async_register() has the reference's contract (include/async.h,
@@ -39,6 +42,7 @@
 #include <unistd.h>
 
 #include "async.h"
+#include "fsalloc.h"
 
 enum { kBurst = 20, kMaxEvents = 16 };
 
@@ -60,6 +64,7 @@ struct wounded {
 
 struct fd_watch {
     int fd;
+    bool pending; /* an edge arrived after the loop was told to quit */
     action_1 action;
     struct fd_watch *next;
 };
@@ -73,6 +78,7 @@ struct async {
     size_t nfree;
     uint64_t seq;
     bool quit;
+    bool pending_scheduled; /* deliver_pending() is queued */
     struct wounded *wound_head, *wound_tail;
     struct fd_watch *watches;
 };
@@ -141,13 +147,11 @@ static void heap_remove(async_t *async, size_t i)
 
 async_t *make_async(void)
 {
-    async_t *async = calloc(1, sizeof *async);
-    if (!async)
-        return NULL;
+    async_t *async = fscalloc(1, sizeof *async);
     async->epfd = epoll_create1(EPOLL_CLOEXEC);
     if (async->epfd < 0) {
         int e = errno;
-        free(async);
+        fsfree(async);
         errno = e;
         return NULL;
     }
@@ -162,8 +166,8 @@ static void run_wound_task(async_t *async)
     async->wound_head = w->next;
     if (!async->wound_head)
         async->wound_tail = NULL;
-    free(w->object);
-    free(w);
+    fsfree(w->object);
+    fsfree(w);
 }
 
 void destroy_async(async_t *async)
@@ -171,27 +175,27 @@ void destroy_async(async_t *async)
     if (!async)
         return;
     for (size_t i = 0; i < async->nheap; i++)
-        free(async->heap[i]);
-    free(async->heap);
+        fsfree(async->heap[i]);
+    fsfree(async->heap);
     while (async->fifo_head) {
         async_timer_t *t = async->fifo_head;
         async->fifo_head = t->next;
-        free(t);
+        fsfree(t);
     }
     while (async->free_list) {
         async_timer_t *t = async->free_list;
         async->free_list = t->next;
-        free(t);
+        fsfree(t);
     }
     while (async->wound_head)
         run_wound_task(async);
     while (async->watches) {
         struct fd_watch *w = async->watches;
         async->watches = w->next;
-        free(w);
+        fsfree(w);
     }
     close(async->epfd);
-    free(async);
+    fsfree(async);
 }
 
 static async_timer_t *task_new(async_t *async)
@@ -202,10 +206,7 @@ static async_timer_t *task_new(async_t *async)
         async->nfree--;
         return t;
     }
-    t = malloc(sizeof *t);
-    if (!t)
-        abort(); /* like fsalloc: allocation failure is fatal */
-    return t;
+    return fsalloc(sizeof *t);
 }
 
 static void task_free(async_t *async, async_timer_t *t)
@@ -215,7 +216,7 @@ static void task_free(async_t *async, async_timer_t *t)
         async->free_list = t;
         async->nfree++;
     } else {
-        free(t);
+        fsfree(t);
     }
 }
 
@@ -236,9 +237,10 @@ async_timer_t *async_timer_start(async_t *async, uint64_t expires,
 {
     if (async->nheap == async->capheap) {
         size_t cap = async->capheap ? 2 * async->capheap : 64;
-        async_timer_t **h = realloc(async->heap, cap * sizeof *h);
-        if (!h)
-            abort(); /* like fsalloc: allocation failure is fatal */
+        async_timer_t **h = fsalloc(cap * sizeof *h);
+        if (async->nheap)
+            memcpy(h, async->heap, async->nheap * sizeof *h);
+        fsfree(async->heap);
         async->heap = h;
         async->capheap = cap;
     }
@@ -279,9 +281,7 @@ async_timer_t *async_execute(async_t *async, action_1 action)
 
 void async_wound(async_t *async, void *object)
 {
-    struct wounded *w = malloc(sizeof *w);
-    if (!w)
-        abort();
+    struct wounded *w = fsalloc(sizeof *w);
     w->object = object;
     w->next = NULL;
     if (async->wound_tail)
@@ -321,10 +321,9 @@ int async_register(async_t *async, int fd, action_1 action)
     ev.data.fd = fd;
     if (epoll_ctl(async->epfd, EPOLL_CTL_ADD, fd, &ev) < 0)
         return -1;
-    w = malloc(sizeof *w);
-    if (!w)
-        abort();
+    w = fsalloc(sizeof *w);
     w->fd = fd;
+    w->pending = false;
     w->action = action;
     w->next = async->watches;
     async->watches = w;
@@ -337,12 +336,33 @@ int async_unregister(async_t *async, int fd)
         if ((*p)->fd == fd) {
             struct fd_watch *w = *p;
             *p = w->next;
-            free(w);
+            fsfree(w);
             return epoll_ctl(async->epfd, EPOLL_CTL_DEL, fd, NULL);
         }
     }
     errno = ENOENT;
     return -1;
+}
+
+/* Edges that came in while the loop was quitting, one at a time (an
+ * action may unregister any watch, so the list is searched afresh). */
+static void deliver_pending(async_t *async)
+{
+    async->pending_scheduled = false;
+    for (;;) {
+        struct fd_watch *w = async->watches;
+        while (w && !w->pending)
+            w = w->next;
+        if (!w)
+            return;
+        if (async->quit) { /* an action quit again: next time round */
+            async->pending_scheduled = true;
+            async_execute(async, (action_1) { async, (act_1) deliver_pending });
+            return;
+        }
+        w->pending = false;
+        action_1_perf(w->action);
+    }
 }
 
 int async_loop(async_t *async)
@@ -385,10 +405,26 @@ int async_loop(async_t *async)
                 continue;
             return -1;
         }
-        for (int i = 0; i < n && !async->quit; i++) {
+        /* Every returned event is acted on: the registration is
+         * edge-triggered, so an edge dropped here would not be reported
+         * again.  Events that arrive after an action quit the loop are
+         * marked on their watch and delivered by a task when the loop runs
+         * again, unless the descriptor is unregistered first (the reference
+         * triggers each event as an immediate task and never drops one,
+         * src/async.c:300-330; an unregistered event is a zombie, :349-363). */
+        for (int i = 0; i < n; i++) {
             struct fd_watch *w = find_watch(async, evs[i].data.fd);
-            if (w)
+            if (!w)
+                continue;
+            if (!async->quit) {
                 action_1_perf(w->action);
+                continue;
+            }
+            w->pending = true;
+            if (!async->pending_scheduled) {
+                async->pending_scheduled = true;
+                async_execute(async, (action_1) { async, (act_1) deliver_pending });
+            }
         }
     }
     return 0;

@@ -7,9 +7,10 @@
  *   blobstream (memory source)                  ref src/blobstream.c
  *   nicestream (periodic EAGAIN injector)       ref src/nicestream.c:34-51
  *
- * Written from the interface contracts in the include/ headers; objects are freed
- * through async_wound() like the reference's, so a callback arriving
- * after close() still finds valid memory.
+ * Written from the interface contracts in the include/ headers; objects come
+ * from fsalloc() and are freed through async_wound() like the reference's
+ * (include/fsalloc.h), so a callback arriving after close() still finds
+ * valid memory and a counting allocator sees every object go.
  */
 #include <errno.h>
 #include <stdlib.h>
@@ -17,6 +18,7 @@
 
 #include "blobstream.h"
 #include "bytestream_1.h"
+#include "fsalloc.h"
 #include "nicestream.h"
 
 static void do_nothing(void *obj)
@@ -28,10 +30,7 @@ action_1 NULL_ACTION_1 = { NULL, do_nothing };
 
 static void *xcalloc(size_t size)
 {
-    void *p = calloc(1, size);
-    if (!p)
-        abort(); /* fsalloc semantics: allocation failure is fatal */
-    return p;
+    return fscalloc(1, size);
 }
 
 /* ---- bytestream_1_close_relaxed ----------------------------------- */
@@ -43,7 +42,7 @@ struct relaxed_close {
 static void relaxed_close_now(struct relaxed_close *rc)
 {
     bytestream_1 s = rc->stream;
-    free(rc);
+    fsfree(rc);
     bytestream_1_close(s);
 }
 
@@ -83,9 +82,7 @@ blobstream_t *open_blobstream(async_t *async, const void *blob, size_t count)
 
 blobstream_t *copy_blobstream(async_t *async, const void *blob, size_t count)
 {
-    void *copy = malloc(count ? count : 1);
-    if (!copy)
-        abort();
+    void *copy = fsalloc(count ? count : 1);
     if (count)
         memcpy(copy, blob, count);
     return new_blob(async, copy, count, copy, NULL_ACTION_1);
@@ -116,7 +113,7 @@ ssize_t blobstream_read(blobstream_t *b, void *buf, size_t count)
 void blobstream_close(blobstream_t *b)
 {
     action_1_perf(b->on_close);
-    free(b->owned);
+    fsfree(b->owned);
     b->owned = NULL;
     async_wound(b->async, b);
     b->async = NULL;

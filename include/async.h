@@ -15,9 +15,13 @@
  *   async_loop / async_quit_loop    ref include/async.h:191,223 (src/async.c:620)
  *   async_register / _unregister    ref include/async.h:249,277 (src/async.c:766)
  *
- * async_register() is level-style over epoll here: it is used for the
- * eventfd through which GPU completions re-enter the loop (SURVEY.md §3,
- * "Where a GPU would enter").
+ * async_register() has the reference's edge-triggered contract (below): it
+ * is used for the eventfd through which GPU completions re-enter the loop
+ * ("Where a GPU would enter").
+ *
+ * Objects: everything this loop allocates, and every object handed to
+ * async_wound(), comes from fsalloc() (include/fsalloc.h), as in the
+ * reference.
  */
 #ifndef ASYNC_AMD_ASYNC_H
 #define ASYNC_AMD_ASYNC_H
@@ -53,15 +57,22 @@ void async_timer_cancel(async_t *async, async_timer_t *timer);
 /* Run `action` from the loop at the first opportunity. */
 async_timer_t *async_execute(async_t *async, action_1 action);
 
-/* Free `object` (allocated with malloc) from the loop at the first
- * opportunity, after every task already scheduled has run. */
+/* fsfree() `object` (allocated with fsalloc()) from the loop at the first
+ * opportunity, after every task already scheduled has run; destroy_async()
+ * frees those still waiting. */
 void async_wound(async_t *async, void *object);
 
 /* Run until async_quit_loop(); 0 on quit, -1 + errno on error. */
 int async_loop(async_t *async);
 void async_quit_loop(async_t *async);
 
-/* Call `action` whenever `fd` becomes readable. */
+/* Watch `fd` edge-triggered (ref include/async.h:236-249): the descriptor
+ * is made non-blocking, and `action` is called when its state changes --
+ * it is guaranteed a call only after a read or write on `fd` has returned
+ * EAGAIN, so the action should drain it.  A registration may bring one
+ * spurious call.  An edge that arrives while the loop is quitting is kept
+ * and delivered when the loop runs again (unless `fd` is unregistered
+ * first). */
 int async_register(async_t *async, int fd, action_1 action);
 int async_unregister(async_t *async, int fd);
 

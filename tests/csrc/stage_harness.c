@@ -21,8 +21,52 @@
 #include "base64encoder.h"
 #include "blobstream.h"
 #include "chunkencoder.h"
+#include "fsalloc.h"
 #include "nicestream.h"
 #include "queuestream.h"
+
+/* ---- the reference runner's leak check: test/asynctest.c:108-147 ------ */
+
+/* Wired like the reference's main() (test/asynctest.c:276-278): every
+ * fsalloc()/fsfree() of the library (loop, streams, stages, hub) goes
+ * through test_realloc, which counts live objects and fills fresh ones with
+ * 0xa5; h_count_end() returns what is still outstanding (the reference's
+ * posttest_check fails a test on anything but 0). */
+static int outstanding_object_count;
+static fs_realloc_t reallocator;
+
+static void *test_realloc(void *ptr, size_t size)
+{
+    void *obj = reallocator(ptr, size);
+    if (ptr)
+        outstanding_object_count--;
+    if (obj) {
+        if (!ptr)
+            memset(obj, 0xa5, size);
+        outstanding_object_count++;
+    }
+    return obj;
+}
+
+static void test_reallocator_counter(int count)
+{
+    outstanding_object_count += count;
+}
+
+void h_count_begin(void)
+{
+    outstanding_object_count = 0;
+    reallocator = fs_get_reallocator();
+    fs_set_reallocator(test_realloc);
+    fs_set_reallocator_counter(test_reallocator_counter);
+}
+
+int h_count_end(void)
+{
+    fs_set_reallocator(reallocator);
+    fs_set_reallocator_counter(NULL);
+    return outstanding_object_count;
+}
 
 /* ---- counting source: test/asynctest-base64encoder.c:11-78 ------------ */
 
@@ -220,13 +264,13 @@ ssize_t h_reftest(size_t length, uint8_t *enc_out, size_t enc_cap,
     async_t *async = make_async();
     if (!async)
         return -1;
-    counting_source *src = calloc(1, sizeof *src);
+    counting_source *src = fscalloc(1, sizeof *src);
     src->async = async;
     src->size = length;
     nicestream_t *n1 = make_nice(async, (bytestream_1) { src, &cs_vt }, 113);
     base64encoder_t *enc = base64_encode(async, nicestream_as_bytestream_1(n1),
                                          '.', '_', true, '-');
-    tap_stream *tap = calloc(1, sizeof *tap);
+    tap_stream *tap = fscalloc(1, sizeof *tap);
     tap->async = async;
     tap->up = base64encoder_as_bytestream_1(enc);
     tap->copy = enc_out;

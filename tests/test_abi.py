@@ -37,7 +37,7 @@ def test_library_built_in_tree():
 def test_every_declared_symbol_is_exported():
     exported = _exported()
     headers = ["b64x.h", "base64encoder.h", "base64decoder.h", "async.h",
-               "bytestream_1.h", "blobstream.h", "nicestream.h"]
+               "bytestream_1.h", "blobstream.h", "nicestream.h", "fsalloc.h"]
     for h in headers:
         for name in _declared(h):
             assert name in exported, f"{h}: {name} not exported"
@@ -188,9 +188,14 @@ def test_core_library_dependencies():
     out = subprocess.run(["nm", "-D", "--undefined-only", core],
                          capture_output=True, text=True, check=True).stdout
     names = {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
-    ours = {n for n in names if n.startswith(("async_", "NULL_ACTION", "bytestream_"))}
+    ours = {n for n in names if n.startswith(("async_", "NULL_ACTION", "bytestream_", "fs"))}
     assert ours == {"async_wound", "async_execute", "async_register", "async_unregister",
-                    "NULL_ACTION_1"}
+                    "NULL_ACTION_1", "fsalloc", "fscalloc", "fsfree"}
+    # the allocator is the reference's (fsdyn's) in a reference build: the
+    # core library must not bring its own
+    defined = subprocess.run(["nm", "-D", "--defined-only", core],
+                             capture_output=True, text=True, check=True).stdout
+    assert not re.search(r"\bfs(alloc|calloc|free)\b", defined)
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     for n in ours:
         assert f"`{n}" in doc, n

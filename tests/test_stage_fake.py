@@ -184,3 +184,51 @@ def test_reference_topology_small_blocks(monkeypatch, cap):
     enc, dec = res
     assert enc == orc.encode(util.counting(100003).tobytes(), ".", "_", True, "-")
     assert dec == util.counting(100003).tobytes()
+
+
+# --- ownership: the reference runner's leak check (test/asynctest.c:108-147) --
+
+def test_leak_check_catches_an_outstanding_object():
+    """Negative control: an object still live when counting stops is seen."""
+    L = fake()
+    L.make_async.restype = ctypes.c_void_p
+    L.destroy_async.argtypes = [ctypes.c_void_p]
+    L.h_count_begin()
+    a = L.make_async()
+    left = L.h_count_end()
+    L.destroy_async(a)
+    assert left >= 1
+
+
+@pytest.mark.parametrize("cap", [None, "4096"])
+def test_reference_topology_leak_check(monkeypatch, cap):
+    """The reference test's topology (test/asynctest-base64encoder.c:123-151)
+    through the stages, with every allocation counted the way the
+    reference's runner counts them (fs_set_reallocator, test/asynctest.c:
+    276-278): after destroy_async() nothing is outstanding -- every stage,
+    hub and stream object was made by fsalloc() and freed by fsfree()
+    through async_wound(), the reference's ownership contract
+    (src/async.c:127-130, 386-392)."""
+    if cap:
+        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", cap)
+    L = fake()
+    L.fake_configure(21, 30, 0)
+    (res, err, _), left = util.counted(util.stage_reftest, 100003, lib=L)
+    assert err == 0 and res is not None
+    assert res[1] == util.counting(100003).tobytes()
+    assert left == 0
+
+
+def test_egress_and_ingress_stacks_leak_check():
+    """Many stacks on one loop (config 5's egress shape and the ingress
+    mirror), counted: nothing outstanding after the loop is destroyed."""
+    L = fake()
+    L.fake_configure(22, 30, 0)
+    lens = [int(x) for x in util.zipf_lengths(200, seed=0x33, rmax=256)]
+    payload = util.splitmix64(0x5EED, sum(lens))
+    (got, err), left = util.counted(util.egress_stacks, payload, lens, 1 << 20, 4096, lib=L)
+    assert err == 0 and left == 0
+    msgs = long_msgs(23, n=60)
+    (got, err), left = util.counted(util.ingress_stacks, msgs, 4096, lib=L)
+    assert err == 0 and left == 0
+    assert bad_streams(msgs, got) == []

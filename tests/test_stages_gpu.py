@@ -26,6 +26,19 @@ def test_reference_topology_on_gpu_stages():
     assert eagains > 0  # the nicestreams did push back
 
 
+def test_reference_topology_leak_check_on_gpu():
+    """The same test with the reference runner's counting allocator wired in
+    (test/asynctest.c:111-147, 276-278): after destroy_async() no object is
+    outstanding, so the reference's posttest_check would pass.  Stages and
+    hub come from fsalloc() and go back through async_wound() -> fsfree()."""
+    d = util.golden("digests.json")["G1"]
+    (res, err, _), left = util.counted(util.stage_reftest, 1000001)
+    assert err == 0 and res is not None
+    assert hashlib.sha256(res[0]).hexdigest() == d["out_sha256"]
+    assert res[1] == util.counting(1000001).tobytes()
+    assert left == 0
+
+
 @pytest.mark.parametrize("read_size", [1, 3, 4, 5, 200, 4096, 1 << 20])
 @pytest.mark.parametrize("burst", [0, 113])
 def test_encoder_stage_any_read_size(read_size, burst):

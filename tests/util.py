@@ -122,6 +122,10 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_egress_stacks_mt_dev.restype = ctypes.c_int
     L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
     L.h_ingress_stacks.restype = ctypes.c_int
+    L.h_count_begin.argtypes = []
+    L.h_count_begin.restype = None
+    L.h_count_end.argtypes = []
+    L.h_count_end.restype = ctypes.c_int
     L.h_prof_start.argtypes = [ctypes.c_int]
     L.h_prof_stop.argtypes = [ctypes.c_char_p]
     L.h_device_count.argtypes = []
@@ -176,6 +180,19 @@ def stage_reftest(length=1000001, lib=None):
                             dec.ctypes.data, dec.size, ctypes.byref(err), ctypes.byref(eag))
     return (None if n < 0 else (enc[: elen.value].tobytes(), dec[:n].tobytes())), \
         err.value, eag.value
+
+
+def counted(fn, *args, lib=None, **kw):
+    """Run fn(*args, lib=..., **kw) with the reference runner's counting
+    allocator wired in (test/asynctest.c:111-147, 276-278); returns
+    (fn's result, objects still outstanding afterwards)."""
+    L = _lib_or_default(lib)
+    L.h_count_begin()
+    try:
+        r = fn(*args, lib=L, **kw)
+    finally:
+        left = L.h_count_end()
+    return r, left
 
 
 def zipf_lengths(n_msgs=16384, seed=0x2F, rmax=16384, s=1.1) -> np.ndarray:
