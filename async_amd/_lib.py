@@ -45,17 +45,22 @@ class Alphabet(ctypes.Structure):
 
 
 class DecResult(ctypes.Structure):
-    """b64x_dec_result, 24 bytes, written by the device."""
+    """b64x_dec_result, 40 bytes, written by the device; nchars, seq and
+    flags name the call that wrote it (include/b64x.h)."""
 
     _fields_ = [
         ("out_len", ctypes.c_uint64),
         ("valid", ctypes.c_uint64),
         ("tail_n", ctypes.c_uint32),
         ("tail", ctypes.c_uint8 * 4),
+        ("nchars", ctypes.c_uint64),
+        ("seq", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
     ]
 
 
-assert ctypes.sizeof(DecResult) == 24
+assert ctypes.sizeof(DecResult) == 40
+RES_BYTES = ctypes.sizeof(DecResult)  # device buffers for one record
 
 _u64 = ctypes.c_uint64
 _u32 = ctypes.c_uint32
@@ -84,7 +89,7 @@ SIGNATURES = {
     "b64x_session_encode": (_int, [_vp, _u64, _ap, ctypes.POINTER(_u64)]),
     "b64x_session_decode": (_int, [_vp, _u64, _ap, ctypes.c_uint, ctypes.POINTER(DecResult)]),
     "b64x_session_encode_async": (_int, [_vp, _u64, _ap, _vp, _vp]),
-    "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp, _vp]),
+    "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp]),
     "b64x_session_result": (ctypes.POINTER(DecResult), [_vp]),
     "b64x_session_decode_result": (_int, [_vp, ctypes.POINTER(DecResult)]),
     "b64x_session_wait": (_int, [_vp]),

@@ -22,7 +22,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import B64xError, DecResult, alphabet  # noqa: F401
+from ._lib import RES_BYTES, B64xError, DecResult, alphabet  # noqa: F401
 
 HOLD_TAIL = 1  # B64X_DEC_HOLD_TAIL
 EXPECT_JUNK = 2  # B64X_DEC_EXPECT_JUNK
@@ -81,10 +81,10 @@ def encode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
 @dataclass
 class Decoded:
     out: torch.Tensor          # capacity-sized output buffer
-    result: torch.Tensor       # 24-byte b64x_dec_result on the device
+    result: torch.Tensor       # b64x_dec_result (RES_BYTES) on the device
 
     def info(self) -> DecResult:
-        host = self.result[:24].cpu().numpy()  # keep alive across the copy
+        host = self.result[:RES_BYTES].cpu().numpy()  # keep alive across the copy
         return DecResult.from_buffer_copy(host.tobytes())
 
     def bytes(self) -> torch.Tensor:
@@ -110,7 +110,7 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
     if out.numel() < cap:
         raise ValueError("output too small")
     if result is None:
-        result = torch.zeros(24, dtype=torch.uint8, device=x.device)
+        result = torch.zeros(RES_BYTES, dtype=torch.uint8, device=x.device)
     if workspace is None:  # must start zeroed; the library keeps it re-armed
         workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
     _lib.check("b64x_decode_dev", lib.b64x_decode_dev(

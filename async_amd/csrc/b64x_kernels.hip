@@ -1149,21 +1149,30 @@ DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, ui
     }
 }
 
-// The result record: `res` in device memory (read by the next chained
-// decode's k_spell_carry), and, when `hres` is set, the same record in
-// fine-grained host memory, written by this kernel instead of a D2H copy
-// queued behind it (see b64x_session_decode_async); the host checks every
-// field of it against the poison it wrote before the launch, so the order
-// of these stores does not matter.
-DEV void write_result(b64x_dec_result *res, b64x_dec_result *hres, uint64_t V, uint32_t hold)
+// The result record: `res` in device memory, and, when `hres` is set, the
+// same record in fine-grained host memory, written by this kernel instead
+// of a D2H copy queued behind it (see b64x_session_decode_async).  The
+// record names its call -- `n` characters, the hold flag and the call's
+// sequence number `seq` (drawn by the host, never 0) -- so the host's check
+// (b64x_result_check.h) rejects a record of an earlier call or a zeroed one
+// as well as poison; it checks every field, so the order of these stores
+// does not matter.
+DEV void write_result(b64x_dec_result *res, b64x_dec_result *hres, uint64_t V, uint32_t hold,
+                      uint64_t n, uint32_t seq)
 {
     const uint64_t out_len = hold ? V / 4 * 3 : V * 6 / 8;
     res->valid = V;
     res->tail_n = (uint32_t) (V & 3);
     res->out_len = out_len;
+    res->nchars = n;
+    res->seq = seq;
+    res->flags = hold ? 1u : 0u;
     if (hres) {
         hres->valid = V;
         hres->out_len = out_len;
+        hres->nchars = n;
+        hres->seq = seq;
+        hres->flags = hold ? 1u : 0u;
     }
 }
 
@@ -1223,7 +1232,8 @@ DEV uint64_t st_load(uint64_t *p)
 // ticket and re-arms the workspace (fd -> fd_cur).
 __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t R, uint32_t nranges,
-    DecAlpha a, void *ws, b64x_dec_result *res, b64x_dec_result *hres, uint32_t hold)
+    DecAlpha a, void *ws, b64x_dec_result *res, b64x_dec_result *hres, uint32_t hold,
+    uint32_t seq)
 {
     __shared__ uint8_t tab[256];
     __shared__ uint64_t wtot[kWavesPerBlock];
@@ -1238,7 +1248,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
         const uint64_t V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
         if (threadIdx.x == 0) {
             *w.fd_cur = 0;
-            write_result(res, hres, V, hold);
+            write_result(res, hres, V, hold, n, seq);
         }
         if (threadIdx.x < 64) find_tail_sextets(tab, in, n, V, res, hres);
         return;
@@ -1299,7 +1309,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     }
     if (t == ntiles - 1 && threadIdx.x < 64) {
         const uint64_t V = s_excl + agg;
-        if (lane == 0) write_result(res, hres, V, hold);
+        if (lane == 0) write_result(res, hres, V, hold, n, seq);
         find_tail_sextets(tab, in, n, V, res, hres);
         for (;;) {  // every tile inclusive -> every look-back is over
             bool all = true;
@@ -1770,7 +1780,7 @@ __global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
-    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res)
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, uint32_t seq)
 {
     __shared__ uint8_t tab[256];
     __shared__ uint8_t s_tail[64];
@@ -1972,6 +1982,9 @@ void k_decode_lines(
         r.valid = V;
         r.tail_n = rem;
         for (uint32_t j = 0; j < 4; j++) r.tail[j] = j < rem ? s_tail[4 * ng + j] : 0;
+        r.nchars = n;
+        r.seq = seq;
+        r.flags = hold ? 1u : 0u;
         *res = r;  // provisional: k_decode_suffix mirrors it to the host or replaces it
     }
 }
@@ -2195,7 +2208,8 @@ template <bool WHOLE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
 void k_decode_suffix(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
-    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres)
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
+    uint32_t seq)
 {
     constexpr uint64_t R = 2 * kChunk;
     DecodeWs w = ws_view(ws, nranges);
@@ -2388,7 +2402,7 @@ void k_decode_suffix(
         if (t == ntiles - 1) {
             if (wv == 0) {
                 const uint64_t V = Vb + s_excl + s_agg;
-                if (lane == 0) write_result(res, hres, V, hold);
+                if (lane == 0) write_result(res, hres, V, hold, n, seq);
                 find_tail_sextets(sm.tab, in, n, V, res, hres);
                 // Every other block has drawn its final ticket -> every
                 // look-back is over (a block draws its next ticket only after
@@ -3067,7 +3081,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
 __global__ __launch_bounds__(kThreads) void k_batch_finish(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
     const uint8_t *__restrict__ flags, const uint64_t *__restrict__ vcount, uint32_t njobs,
-    uint64_t big, DecAlpha a, b64x_dec_result *__restrict__ hres)
+    uint64_t big, DecAlpha a, b64x_dec_result *__restrict__ hres, uint32_t seq)
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
@@ -3100,6 +3114,9 @@ __global__ __launch_bounds__(kThreads) void k_batch_finish(
             r->valid = V;
             r->out_len = hold ? V / 4 * 3 : V * 6 / 8;
             r->tail_n = (uint32_t) (V & 3);
+            r->nchars = n;
+            r->seq = seq;
+            r->flags = hold ? 1u : 0u;
         }
     }
 }
@@ -3408,11 +3425,26 @@ static void *library_workspace(void *stream, int *err)
     return ws;
 }
 
-__global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres)
+__global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres,
+                                                    uint32_t hold, uint32_t seq)
 {
     if (threadIdx.x != 0) return;
-    *res = b64x_dec_result{};
-    if (hres) *hres = b64x_dec_result{};
+    b64x_dec_result r{};
+    r.seq = seq;
+    r.flags = hold ? 1u : 0u;
+    *res = r;
+    if (hres) *hres = r;
+}
+
+// Sequence numbers of decode calls and batches: nonzero, process-wide.
+static uint32_t next_seq()
+{
+    static std::atomic<uint32_t> g_seq{0};
+    uint32_t v;
+    do {
+        v = g_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+    } while (v == 0);
+    return v;
 }
 
 // b64x_decode_dev, plus an optional host mirror of the result record that
@@ -3420,7 +3452,7 @@ __global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_d
 static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
                            b64x_dec_result *d_res, b64x_dec_result *h_res,
                            const b64x_alphabet *abc, unsigned flags, void *d_workspace,
-                           void *stream)
+                           void *stream, uint32_t seq)
 {
     if (!d_res) return -EINVAL;
     if (flags & ~(unsigned) (B64X_DEC_HOLD_TAIL | B64X_DEC_EXPECT_JUNK)) return -EINVAL;
@@ -3429,7 +3461,8 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     if (!d) return -ENODEV;
     hipStream_t s = (hipStream_t) stream;
     if (nchars == 0) {
-        hipLaunchKernelGGL(k_result_zero, dim3(1), dim3(64), 0, s, d_res, h_res);
+        hipLaunchKernelGGL(k_result_zero, dim3(1), dim3(64), 0, s, d_res, h_res,
+                           flags & B64X_DEC_HOLD_TAIL, seq);
         return launch_status();
     }
     int err = 0;
@@ -3453,7 +3486,7 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         if (flags & B64X_DEC_EXPECT_JUNK) {
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res);
+                               hold, d_res, h_res, seq);
             return launch_status();
         }
         hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(64), 0, s, (const uint8_t *) d_in, nchars,
@@ -3462,11 +3495,11 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
         hipLaunchKernelGGL(k_decode_lines, dim3((uint32_t) ((waves + kWavesPerBlock - 1) / kWavesPerBlock)),
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
-                           p.nranges, a, ws, hold, d_res);
+                           p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
         hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                           hold, d_res, h_res);
+                           hold, d_res, h_res, seq);
         return launch_status();
     }
     // Larger inputs (ranges longer than 2,048 characters): pass 1, the scan,
@@ -3476,7 +3509,7 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     if ((err = launch_status())) return err;
     hipLaunchKernelGGL(k_decode_scan2, dim3((p.nranges + kScanTile - 1) / kScanTile),
                        dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, p.R, p.nranges, a,
-                       ws, d_res, h_res, hold);
+                       ws, d_res, h_res, hold, seq);
     if ((err = launch_status())) return err;
     // grid-stride over the ranges with exactly the resident blocks (a second
     // partial round of blocks would trail the rest)
@@ -3493,7 +3526,7 @@ int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     unsigned flags, void *d_workspace, void *stream)
 {
     return decode_dev_impl(d_in, nchars, d_out, d_res, nullptr, abc, flags, d_workspace,
-                           stream);
+                           stream, next_seq());
 }
 
 // rv: d_outlen receives alphabet counts V (the hub's jobs) instead of bytes.
@@ -3625,15 +3658,15 @@ int b64x_fill_splitmix64(void *d_out, uint64_t n, uint64_t seed, void *stream)
 struct b64x_session {
     int device;
     hipStream_t stream;
-    hipEvent_t decoded;  // recorded after each decode's kernels
     uint64_t cap;
     uint8_t *h_in, *h_out;
     uint8_t *h_base;     // h_in - kSessionHead (pinned, for in-place decodes)
     uint8_t *d_base;     // d_in - kSessionHead
     uint64_t last_len;   // characters of the last decode (0: none yet)
     bool dec_staged;     // the last decode found junk throughout: stage the next
-    uint64_t res_len;    // characters and flags of the last decode, for the
-    unsigned res_flags;  // result check (b64x_session_decode_result)
+    uint64_t res_len;    // characters, flags and sequence number of the last
+    unsigned res_flags;  // decode, for the result check
+    uint32_t res_seq;    // (b64x_session_decode_result)
     uint8_t *d_in, *d_out;
     void *d_ws;
     b64x_dec_result *d_res, *h_res;
@@ -3655,35 +3688,13 @@ struct b64x_session {
 // b64x_result_check.h, shared with the CPU stage tests.
 static std::atomic<uint64_t> g_early_session{0}, g_early_lane{0};
 
-// Device headroom in front of d_in: a chained decode writes the carried
-// sextets (re-spelled as characters, right-aligned, padded on the left with
-// a character the alphabet skips) into the last kCarryHead bytes of it.
+// Device headroom in front of d_in (kept for the decode kernels' vector
+// loads, which may start below an unaligned input).
 constexpr uint64_t kSessionHead = 256;
-constexpr uint32_t kCarryHead = 16;
 // Pinned slack after host_in: the decode kernels' last vector loads may
 // reach past the input, harmless in a page-rounded hipMalloc, not assumed
 // of host memory read in place.
 constexpr uint64_t kSessionTail = 64;
-
-// One wave: writes the kCarryHead-byte prefix for a decode chained after
-// the HOLD_TAIL decode whose result is *prev (ref base64decoder.c:64-76 --
-// the reference keeps those bits in decoder->bits across reads).
-__global__ void __launch_bounds__(64)
-k_spell_carry(const b64x_dec_result *__restrict__ prev, uint8_t *__restrict__ head,
-              char pos62, char pos63, uint8_t skip)
-{
-    const uint32_t i = threadIdx.x;
-    if (i >= kCarryHead) return;
-    const uint32_t n = prev->tail_n < 4 ? prev->tail_n : 0;
-    const uint32_t first = kCarryHead - n;
-    uint8_t c = skip;
-    if (i >= first) {
-        const uint32_t v = prev->tail[i - first] & 63;
-        c = v < 26 ? 'A' + v : v < 52 ? 'a' + (v - 26) : v < 62 ? '0' + (v - 52)
-          : (uint8_t) (v == 62 ? pos62 : pos63);
-    }
-    head[i] = c;
-}
 
 static uint64_t session_out_cap(uint64_t cap)
 {
@@ -3716,15 +3727,13 @@ b64x_session *b64x_session_open(uint64_t capacity)
     if (!s) return nullptr;
     s->cap = capacity;
     (void) hipGetDevice(&s->device);
-    // Decodes may carry kCarryHead extra characters in front of host_in.
-    const uint64_t ocap = session_out_cap(capacity + kCarryHead);
-    const uint64_t wsz = b64x_decode_workspace_size(capacity + kCarryHead);
+    const uint64_t ocap = session_out_cap(capacity);
+    const uint64_t wsz = b64x_decode_workspace_size(capacity);
     bool ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
               hipHostMalloc((void **) &s->h_base, kSessionHead + capacity + kSessionTail,
                             kSessionHostFlags) == hipSuccess &&
               hipHostMalloc((void **) &s->h_out, ocap, kSessionHostFlags) == hipSuccess &&
               hipHostMalloc((void **) &s->h_res, sizeof(b64x_dec_result), kSessionHostFlags) == hipSuccess &&
-              hipEventCreateWithFlags(&s->decoded, hipEventDisableTiming) == hipSuccess &&
               hipMalloc((void **) &s->d_base, kSessionHead + capacity) == hipSuccess &&
               hipMalloc((void **) &s->d_out, ocap) == hipSuccess &&
               hipMalloc((void **) &s->d_res, sizeof(b64x_dec_result)) == hipSuccess &&
@@ -3751,7 +3760,6 @@ void b64x_session_close(b64x_session *s)
     if (s->h_out) (void) hipHostFree(s->h_out);
     if (s->h_res) (void) hipHostFree(s->h_res);
     if (s->d_base) (void) hipFree(s->d_base);
-    if (s->decoded) (void) hipEventDestroy(s->decoded);
     if (s->d_out) (void) hipFree(s->d_out);
     if (s->d_res) (void) hipFree(s->d_res);
     if (s->d_ws) (void) hipFree(s->d_ws);
@@ -3826,7 +3834,7 @@ int b64x_session_decode(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
     if (!s || n > s->cap || !res) return -EINVAL;
     memset(res, 0, sizeof(*res));
     int err;
-    if ((err = b64x_session_decode_async(s, n, abc, flags, nullptr, nullptr, nullptr))) return err;
+    if ((err = b64x_session_decode_async(s, n, abc, flags, nullptr, nullptr))) return err;
     if ((err = b64x_session_wait(s))) return err;
     return b64x_session_decode_result(s, res);
 }
@@ -3866,17 +3874,6 @@ int b64x_session_encode_async(b64x_session *s, uint64_t n, const b64x_alphabet *
     return 0;
 }
 
-// A character the decoder skips under this alphabet (ref map(),
-// base64decoder.c:38-48: not alphanumeric, not pos62/pos63).
-static uint8_t skip_char(const b64x_alphabet *abc)
-{
-    const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
-    const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
-    for (char c : {'\n', '\r', ' '})
-        if (c != p62 && c != p63) return (uint8_t) c;
-    return '\n';  // unreachable: two characters cannot shadow three
-}
-
 // A session's decode reads host_in and writes host_out in place over PCIe
 // too, unless its last decode found junk throughout (MIME line breaks):
 // pass 2 re-reads the input and pass-1 output where junk is, which in place
@@ -3884,81 +3881,54 @@ static uint8_t skip_char(const b64x_alphabet *abc)
 // CRLF-76 ones 21.6 staged against 17.7 in place (scripts/bench_zero_copy.py).
 // The result of the last decode is consulted only once the session's stream
 // has drained, so the policy never waits and never reads a result in flight.
-// A chained decode reads in place only when its carry is already known to be
-// empty (carry_from's stream has drained): the spelled carry head's skip
-// characters displace every range, so pass 2 rewrites the whole block, which
-// in place re-reads all of it over PCIe (32 MiB chained blocks: 13.8 GiB/s in
-// place against 16-36 staged, profiles/r01_host_pipeline_v9.jsonl).  With
-// the carry known empty there is no head at all.
 // ASYNC_B64_ZERO_COPY=0 stages every decode as well.
-constexpr uint64_t kZeroCopyJunk = 64;  // skipped characters beyond the carry head
+constexpr uint64_t kZeroCopyJunk = 80;  // skipped characters that make the next decode staged
 
 static bool decode_in_place(b64x_session *s)
 {
     if (!zero_copy_sessions()) return false;
     b64x_dec_result r;
     if (s->last_len && hipStreamQuery(s->stream) == hipSuccess &&
-        b64x_result_ok(s->h_res, s->res_len, s->res_flags, &r)) {
+        b64x_result_ok(s->h_res, s->res_len, s->res_flags, s->res_seq, &r)) {
         const uint64_t junk = s->last_len - (r.valid < s->last_len ? r.valid : s->last_len);
-        s->dec_staged = junk > kCarryHead + kZeroCopyJunk;
+        s->dec_staged = junk > kZeroCopyJunk;
         s->last_len = 0;
     }
     return !s->dec_staged;
 }
 
+// Round 1 chained a stream's blocks over sessions on the device (a carry
+// spelled by a kernel on the previous session's stream, a cross-stream
+// event, the record copied D2H behind the kernels), and a block was once in
+// a while served as empty from a well-formed "nothing decoded" record.  That
+// chaining is gone: a session decode is H2D (or in place),
+// the kernels and the completion, all on the session's own stream, and the
+// record the kernels write into host memory names this call (n, flags and
+// a fresh sequence number), so no earlier or zero-filled record passes the
+// check.
 int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
-                              unsigned flags, const b64x_session *carry_from,
-                              b64x_done_fn done, void *arg)
+                              unsigned flags, b64x_done_fn done, void *arg)
 {
-    if (!s || n > s->cap || carry_from == s) return -EINVAL;
-    if (carry_from && carry_from->device != s->device) return -EINVAL;
+    if (!s || n > s->cap) return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(s->device)))) return err;
-    b64x_dec_result cr;
-    if (carry_from && hipStreamQuery(carry_from->stream) == hipSuccess &&
-        b64x_result_ok(carry_from->h_res, carry_from->res_len, carry_from->res_flags, &cr) &&
-        cr.tail_n == 0)
-        carry_from = nullptr;  // finished, and nothing to carry
-    const bool in_place = decode_in_place(s) && !carry_from;
+    const bool in_place = decode_in_place(s);
     uint8_t *in = in_place ? s->h_in : s->d_in;
     uint8_t *out = in_place ? s->h_out : s->d_out;
-    const uint8_t *src = in;
-    uint64_t len = n;
     if (n && !in_place &&
         (err = hip_err(hipMemcpyAsync(s->d_in, s->h_in, n, hipMemcpyHostToDevice, s->stream))))
         return err;
-    if (carry_from) {
-        // The carry is spelled on carry_from's stream, right after the decode
-        // that produced it, so carry_from's next decode (which overwrites its
-        // result) is ordered after the read by stream order; this session
-        // waits for the spelling.  (Spelled on this stream instead, behind an
-        // event, the read could lose the race against carry_from's next
-        // decode when many streams share the hardware queues.)  The prefix
-        // it writes lies in front of the input (device or pinned host
-        // headroom), so it overlaps the H2D above.
-        const char p62 = abc && abc->pos62 != (char) -1 ? abc->pos62 : '+';
-        const char p63 = abc && abc->pos63 != (char) -1 ? abc->pos63 : '/';
-        if ((err = hip_err(hipSetDevice(carry_from->device)))) return err;
-        hipLaunchKernelGGL(k_spell_carry, dim3(1), dim3(64), 0, carry_from->stream,
-                           carry_from->d_res, in - kCarryHead, p62, p63, skip_char(abc));
-        if ((err = launch_status())) return err;
-        if ((err = hip_err(hipEventRecord(carry_from->decoded, carry_from->stream)))) return err;
-        if ((err = hip_err(hipSetDevice(s->device)))) return err;
-        if ((err = hip_err(hipStreamWaitEvent(s->stream, carry_from->decoded, 0)))) return err;
-        src -= kCarryHead;
-        len += kCarryHead;
-    }
     b64x_poison_result(s->h_res);
-    s->res_len = len;
+    s->res_len = n;
     s->res_flags = flags;
-    if ((err = decode_dev_impl(src, len, out, s->d_res, s->h_res, abc, flags, s->d_ws,
-                               s->stream)))
+    s->res_seq = next_seq();
+    if ((err = decode_dev_impl(in, n, out, s->d_res, s->h_res, abc, flags, s->d_ws, s->stream,
+                               s->res_seq)))
         return err;
-    if ((err = hip_err(hipEventRecord(s->decoded, s->stream)))) return err;
-    s->last_len = len;
+    s->last_len = n;
     // The output length is device-determined: copy the capacity bound.
-    if (len && !in_place &&
-        (err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(len),
+    if (n && !in_place &&
+        (err = hip_err(hipMemcpyAsync(s->h_out, s->d_out, b64x_decoded_cap(n),
                                       hipMemcpyDeviceToHost, s->stream))))
         return err;
     if (done) return hip_err(hipLaunchHostFunc(s->stream, done, arg));
@@ -3973,11 +3943,11 @@ const b64x_dec_result *b64x_session_result(const b64x_session *s)
 int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res)
 {
     if (!s || !res) return -EINVAL;
-    if (b64x_result_ok(s->h_res, s->res_len, s->res_flags, res)) return 0;
+    if (b64x_result_ok(s->h_res, s->res_len, s->res_flags, s->res_seq, res)) return 0;
     g_early_session.fetch_add(1, std::memory_order_relaxed);
     int err = b64x_session_wait(s);
     if (err) return err;
-    const bool ok = b64x_result_ok(s->h_res, s->res_len, s->res_flags, res);
+    const bool ok = b64x_result_ok(s->h_res, s->res_len, s->res_flags, s->res_seq, res);
     return ok ? 0 : -EIO;
 }
 
@@ -4030,6 +4000,7 @@ struct b64x_lane {
     uint64_t in_cap, offs_cap, flags_cap;  // bytes allocated
     b64x_dec_result *d_res;  // big decode jobs: the pipeline's record ...
     void *d_ws;              // ... and workspace (allocated at the first)
+    uint32_t dseq;           // the last decode batch's sequence number
 };
 
 b64x_lane *b64x_lane_open(void)
@@ -4186,6 +4157,7 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     if (njobs) {
         const uint64_t words = (uint64_t) njobs + 1;
         for (uint32_t j = 0; j < njobs; j++) b64x_poison_result(h_res + j);
+        l->dseq = next_seq();
         if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, words))) return err;
         if ((err = lane_grow(l, (void **) &l->d_flags, &l->flags_cap, njobs))) return err;
         if ((err = hip_err(hipMemcpyAsync(l->d_flags, h_flags, njobs, hipMemcpyHostToDevice,
@@ -4209,13 +4181,20 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                                            (uint64_t) d->cus * 8);
             hipLaunchKernelGGL(k_batch_finish, dim3(grid), dim3(kThreads), 0, l->stream, src,
                                d_in_off, (const uint8_t *) l->d_flags,
-                               (const uint64_t *) d_vcount, njobs, L.big, dec_alpha(abc), h_res);
+                               (const uint64_t *) d_vcount, njobs, L.big, dec_alpha(abc), h_res,
+                               l->dseq);
             if ((err = launch_status())) return err;
         }
         if (nbig && !l->d_ws) {
             const uint64_t wsz = b64x_decode_workspace_size(0);
-            if (hipMalloc(&l->d_res, sizeof *l->d_res) != hipSuccess) return -ENOMEM;
-            if (hipMalloc(&l->d_ws, wsz) != hipSuccess) return -ENOMEM;
+            if (!l->d_res && hipMalloc(&l->d_res, sizeof *l->d_res) != hipSuccess) {
+                l->d_res = nullptr;
+                return -ENOMEM;
+            }
+            if (hipMalloc(&l->d_ws, wsz) != hipSuccess) {
+                l->d_ws = nullptr;
+                return -ENOMEM;
+            }
             if ((err = hip_err(hipMemsetAsync(l->d_ws, 0, wsz, l->stream)))) return err;
         }
         for (uint32_t j = 0; nbig && j < njobs; j++) {
@@ -4223,7 +4202,7 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
             if (n < kBigJob) continue;
             if ((err = decode_dev_impl(l->d_in + h_in_off[j], n, h_out + h_out_off[j], l->d_res,
                                        h_res + j, abc, h_flags[j] & 1 ? B64X_DEC_HOLD_TAIL : 0,
-                                       l->d_ws, l->stream)))
+                                       l->d_ws, l->stream, l->dseq)))
                 return err;
         }
     }
@@ -4238,10 +4217,11 @@ int b64x_lane_wait(b64x_lane *l)
 }
 
 static bool jobs_ok(const uint64_t *h_in_off, const uint8_t *h_flags,
-                    const b64x_dec_result *h_res, uint32_t njobs)
+                    const b64x_dec_result *h_res, uint32_t njobs, uint32_t seq)
 {
     for (uint32_t j = 0; j < njobs; j++)
-        if (!b64x_result_ok(h_res + j, h_in_off[j + 1] - h_in_off[j], h_flags[j] & 1, nullptr))
+        if (!b64x_result_ok(h_res + j, h_in_off[j + 1] - h_in_off[j], h_flags[j] & 1, seq,
+                            nullptr))
             return false;
     return true;
 }
@@ -4250,11 +4230,11 @@ int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t
                            const b64x_dec_result *h_res, uint32_t njobs)
 {
     if (!l || (njobs && (!h_in_off || !h_flags || !h_res))) return -EINVAL;
-    if (jobs_ok(h_in_off, h_flags, h_res, njobs)) return 0;
+    if (jobs_ok(h_in_off, h_flags, h_res, njobs, l->dseq)) return 0;
     g_early_lane.fetch_add(1, std::memory_order_relaxed);
     int err = b64x_lane_wait(l);
     if (err) return err;
-    return jobs_ok(h_in_off, h_flags, h_res, njobs) ? 0 : -EIO;
+    return jobs_ok(h_in_off, h_flags, h_res, njobs, l->dseq) ? 0 : -EIO;
 }
 
 #ifdef B64X_TEST_HOOKS
@@ -4321,7 +4301,7 @@ uint64_t b64x__test_range_chunks(uint64_t chunks)
 
 const char *b64x_build_info(void)
 {
-    return "b64x abi=1 arch=gfx950 enc:quad12->16 bpermute-alphabet unroll=4; "
+    return "b64x abi=2 arch=gfx950 enc:quad12->16 bpermute-alphabet unroll=4; "
            "dec:probe+line-model single pass (4 slots/lane) + exact suffix (look-back)";
 }
 

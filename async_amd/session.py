@@ -9,9 +9,9 @@ scripts/bench_host_pipeline.py, which measures the PCIe-inclusive rate.
     s.host_in[:n] = data
     s.encode_async(n); s.wait(); chars = s.host_out[:encoded_len(n)]
 
-Chained decoding (``decode_async(..., carry_from=other)``) prepends on the
-device the sextets the other session's last HOLD_TAIL decode held back, so
-a stream of blocks can be queued without a host round trip per block.
+A stream decoded in blocks uses HOLD_TAIL for every block but the last and
+spells the record's held-back sextets (``result().tail``) in front of the
+next block, as the bytestream_1 decoder stage does.
 """
 from __future__ import annotations
 
@@ -92,12 +92,10 @@ class Session:
                    self._L.b64x_session_encode_async(self._h, n, ctypes.byref(_abc(abc)),
                                                      None, None))
 
-    def decode_async(self, n: int, abc=None, flags: int = 0,
-                     carry_from: "Session | None" = None) -> None:
-        prev = carry_from.handle if carry_from is not None else None
+    def decode_async(self, n: int, abc=None, flags: int = 0) -> None:
         _lib.check("b64x_session_decode_async",
                    self._L.b64x_session_decode_async(self._h, n, ctypes.byref(_abc(abc)),
-                                                     flags, prev, None, None))
+                                                     flags, None, None))
 
     def wait(self) -> None:
         _lib.check("b64x_session_wait", self._L.b64x_session_wait(self._h))

@@ -153,7 +153,7 @@ def bench_single(args, world, rank, b64):
     enc = torch.empty(E, dtype=torch.uint8, device="cuda")
     dec = torch.empty(b64.decoded_cap(E), dtype=torch.uint8, device="cuda")
     ws = torch.zeros(b64.workspace_size(E), dtype=torch.uint8, device="cuda")
-    res = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
     def step():
@@ -319,7 +319,7 @@ def bench_host_inclusive(args, b64):
     streams = [torch.cuda.Stream() for _ in range(k)]
     dev_in = [torch.empty(eblk + slack, dtype=torch.uint8, device="cuda") for _ in range(k)]
     dev_out = [torch.empty(eblk + slack, dtype=torch.uint8, device="cuda") for _ in range(k)]
-    res = [torch.zeros(24, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    res = [torch.zeros(_lib.RES_BYTES, dtype=torch.uint8, device="cuda") for _ in range(k)]
     ws = [torch.zeros(b64.workspace_size(eblk), dtype=torch.uint8, device="cuda")
           for _ in range(k)]
     a = _lib.alphabet()
@@ -414,7 +414,7 @@ def bench_mime(args, b64, steps=10):
     text = crlf76(b64.encode(x))
     out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device="cuda")
     ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device="cuda")
-    res = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
     def timed(fn):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define B64X_ABI_VERSION 1
+#define B64X_ABI_VERSION 2
 
 /* Alphabet descriptor.  (char) -1 selects the reference's defaults,
  * exactly like base64_encode()/base64_decode() (ref
@@ -55,12 +55,19 @@ typedef struct b64x_alphabet {
     bool pad;
 } b64x_alphabet;
 
-/* Per-call decode result, written by the device. */
+/* Per-call decode result, written by the device.  A record names the call
+ * that wrote it: `nchars` and `flags` echo the call's arguments and `seq` is
+ * a nonzero number the library draws for every decode call (or batch), so
+ * a record left over from an earlier call, or a zero-filled one, is never
+ * taken for this call's (b64x_session_decode_result, b64x_lane_decode_check). */
 typedef struct b64x_dec_result {
     uint64_t out_len;  /* bytes written to the output */
     uint64_t valid;    /* alphabet characters seen (V) */
     uint32_t tail_n;   /* V mod 4 */
-    uint8_t tail[4];   /* the last tail_n sextet values (0..63) */
+    uint8_t tail[4];   /* the last tail_n sextet values (0..63); the rest 0 */
+    uint64_t nchars;   /* characters this decode covered */
+    uint32_t seq;      /* the call's sequence number, never 0 */
+    uint32_t flags;    /* the call's B64X_DEC_HOLD_TAIL bit */
 } b64x_dec_result;
 
 /* Decode flags. */
@@ -180,28 +187,25 @@ typedef void (*b64x_done_fn)(void *arg);
 int b64x_session_encode_async(b64x_session *s, uint64_t n,
                               const b64x_alphabet *abc, b64x_done_fn done,
                               void *arg);
-/* carry_from (NULL = none): another session on the same device whose last
- * call was a decode with B64X_DEC_HOLD_TAIL.  The sextets it held back are
- * prepended on the device, so a stream of blocks can be queued before the
- * previous block's result reaches the host: a one-wave kernel on
- * carry_from's stream spells them in front of this session's input, and
- * this session waits for it with a HIP event.  carry_from's next call is
- * ordered after that read by its own stream order, so any number of
- * sessions can be chained round-robin.
- * n == 0 with carry_from flushes the carried sextets alone. */
+/* A caller that decodes one stream in several blocks uses
+ * B64X_DEC_HOLD_TAIL and spells the record's held-back sextets in front of
+ * its next block itself (ABI version 1's device-side chaining of sessions,
+ * `carry_from`, is gone: DESIGN.md §8, "Round 1's decoder-ingress block
+ * loss"). */
 int b64x_session_decode_async(b64x_session *s, uint64_t n,
                               const b64x_alphabet *abc, unsigned flags,
-                              const b64x_session *carry_from,
                               b64x_done_fn done, void *arg);
 /* The decode result of the last completed call (host memory; the kernels
  * write it there themselves).  Raw view: prefer the checked form below. */
 const b64x_dec_result *b64x_session_result(const b64x_session *s);
 /* Checked copy of the last decode's result, to be called once its `done`
  * has run (or after b64x_session_wait).  The record is poisoned before each
- * launch; one that is still poisoned or inconsistent (valid > characters,
- * tail_n != valid mod 4, out_len not the flags' function of valid) is
- * counted (b64x_diag_counters), the session's stream is waited for and the
- * record is checked again.  0, or -EIO if it is still wrong. */
+ * launch; one that is still poisoned, names another call (seq, nchars or
+ * flags differ) or is inconsistent (valid > characters, tail_n != valid
+ * mod 4, a held-back sextet >= 64 or a nonzero unused tail byte, out_len
+ * not the flags' function of valid) is counted (b64x_diag_counters), the
+ * session's stream is waited for and the record is checked again.  0, or
+ * -EIO if it is still wrong. */
 int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res);
 /* Wait for everything queued on the session. */
 int b64x_session_wait(b64x_session *s);

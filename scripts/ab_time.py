@@ -31,7 +31,7 @@ def child(lib, steps):
     dirty = crlf76(enc)
     junk = sprinkle(enc, 0.05)
     out = torch.empty(b64.decoded_cap(junk.numel()), dtype=torch.uint8, device="cuda")
-    rr = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    rr = torch.zeros(_lib.RES_BYTES, dtype=torch.uint8, device="cuda")
     ws = torch.zeros(b64.workspace_size(junk.numel()), dtype=torch.uint8, device="cuda")
     res = {}
 

@@ -44,14 +44,13 @@ def run_resident(src: np.ndarray, block: int, k: int, op: str, total: int):
     already holds its block (as if upstream had read into it); results stay
     in pinned host_out.  Returns seconds for `total` input units."""
     sess = [Session(block) for _ in range(k)]
-    step = block // 3 * 3 if op == "encode" else block
+    step = block // 3 * 3 if op == "encode" else block // 4 * 4
     try:
         for s in sess:
             s.host_in[:step] = src[:step]
             s.encode(step) if op == "encode" else s.decode(step)
         nblk = (total + step - 1) // step
         t0 = time.perf_counter()
-        prev = None
         for i in range(nblk):
             s = sess[i % k]
             if i >= k:
@@ -59,11 +58,8 @@ def run_resident(src: np.ndarray, block: int, k: int, op: str, total: int):
             n = min(step, total - i * step)
             if op == "encode":
                 s.encode_async(n)
-            elif op == "decode_blocks":  # whole groups, clean: blocks need no carry
+            else:  # whole groups of clean text: blocks need no carry
                 s.decode_async(n, None, 0)
-            else:
-                s.decode_async(n, None, HOLD_TAIL if i + 1 < nblk else 0, carry_from=prev)
-            prev = s
         for s in sess:
             s.wait()
         return time.perf_counter() - t0
@@ -104,7 +100,7 @@ def pcie_calibration(nbytes: int):
 def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
     """Stream src through k sessions; returns (seconds, out_len)."""
     sess = [Session(block) for _ in range(k)]
-    step = block // 3 * 3 if op == "encode" else block
+    step = block // 3 * 3 if op == "encode" else block // 4 * 4
     try:
         # warm up every session once (allocations, code objects)
         for s in sess:
@@ -115,7 +111,6 @@ def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
                 s.decode(step)
         live = []  # (session, out_len or None)
         opos = 0
-        prev = None
         t0 = time.perf_counter()
         pos, i = 0, 0
         while pos < len(src) or live:
@@ -128,10 +123,11 @@ def run_sessions(src: np.ndarray, block: int, k: int, op: str, out: np.ndarray):
                     s.encode_async(n)
                     m = (n + 2) // 3 * 4 if last else n // 3 * 4
                 else:
-                    s.decode_async(n, None, 0 if last else HOLD_TAIL, carry_from=prev)
+                    # blocks are whole 4-character groups of clean text, so no
+                    # block holds a carry for the next one
+                    s.decode_async(n, None, 0)
                     m = None
                 live.append((s, m))
-                prev = s
                 pos += n
                 i += 1
                 continue

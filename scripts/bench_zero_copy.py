@@ -76,7 +76,7 @@ for mib in (4, 32, 256):
         h_out = torch.empty(cap, dtype=torch.uint8).pin_memory()
         d_in = torch.empty(m, dtype=torch.uint8, device="cuda")
         d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
-        res = torch.zeros(24, dtype=torch.uint8, device="cuda")
+        res = torch.zeros(_lib.RES_BYTES, dtype=torch.uint8, device="cuda")
         ws = torch.zeros(b64.workspace_size(m), dtype=torch.uint8, device="cuda")
 
         def dec(src, dst):

@@ -24,7 +24,13 @@
  *  - raw mode stands for the round-1 stage: b64x_session_decode_result and
  *    b64x_lane_decode_check return what is there without checking (and
  *    nothing is poisoned), so an early job's block is read as the previous
- *    call's record.
+ *    call's record;
+ *  - "zero" mode: an early job publishes an all-zero record before its
+ *    callback (what round 1's stage once served: a well-formed "nothing
+ *    decoded" record, profiles/r02_diag_notes.md), and the real one later;
+ *  - "torn" mode: an early job publishes its record's every field but the
+ *    held-back sextets tail[] before its callback (a record
+ *    whose tail_n landed before its tail bytes).
  *
  * b64x_session_decode_result / b64x_lane_decode_check otherwise run the
  * library's own check (async_amd/csrc/b64x_result_check.h).
@@ -78,6 +84,18 @@ static bool stopping;
 static uint64_t rng_state = 1;
 static unsigned early_pct;
 static bool raw_mode;
+enum { MODE_CHECKED = 0, MODE_RAW = 1, MODE_ZERO = 2, MODE_TORN = 3 };
+static int fake_mode;
+static atomic_uint g_seq;
+
+static uint32_t next_seq(void)
+{
+    uint32_t v;
+    do
+        v = atomic_fetch_add(&g_seq, 1) + 1;
+    while (v == 0);
+    return v;
+}
 static atomic_ulong n_early, n_jobs;
 
 static uint64_t rnd(void) /* splitmix64, under mu */
@@ -86,6 +104,30 @@ static uint64_t rnd(void) /* splitmix64, under mu */
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+/* What an early job shows before its callback in zero / torn mode. */
+static void publish_early_record(b64x_dec_result *dst, const b64x_dec_result *r)
+{
+    if (fake_mode == MODE_ZERO) {
+        memset(dst, 0, sizeof *dst);
+    } else if (fake_mode == MODE_TORN) {
+        volatile b64x_dec_result *v = dst;
+        v->out_len = r->out_len;
+        v->valid = r->valid;
+        v->tail_n = r->tail_n;
+        v->nchars = r->nchars;
+        v->seq = r->seq;
+        v->flags = r->flags; /* tail[] left as it was */
+    }
+}
+
+static void publish_early(fjob *j)
+{
+    if (j->res_dst)
+        publish_early_record(j->res_dst, &j->res);
+    for (uint32_t k = 0; j->recs_dst && k < j->njobs; k++)
+        publish_early_record(j->recs_dst + k, j->recs + k);
 }
 
 static void publish(fjob *j)
@@ -159,6 +201,7 @@ static void *worker(void *unused)
         if (early) {
             atomic_fetch_add(&n_early, 1);
             j->called = true;
+            publish_early(j);
             if (j->done)
                 j->done(j->arg); /* callback first: the round-1 hazard */
             pthread_mutex_lock(&mu);
@@ -234,9 +277,10 @@ static void submit(fjob *j)
     pthread_mutex_unlock(&mu);
 }
 
-/* Test control: seed, % of early jobs, raw (round-1) reads.  Waits for the
- * device to go idle first. */
-void fake_configure(uint64_t seed, unsigned pct, int raw)
+/* Test control: seed, % of early jobs, mode (0 checked, 1 raw round-1
+ * reads, 2 zero records, 3 torn tails).  Waits for the device to go idle
+ * first. */
+void fake_configure(uint64_t seed, unsigned pct, int mode)
 {
     pthread_mutex_lock(&mu);
     while (queue_head || busy)
@@ -249,7 +293,8 @@ void fake_configure(uint64_t seed, unsigned pct, int raw)
     }
     rng_state = seed ? seed : 1;
     early_pct = pct;
-    raw_mode = raw != 0;
+    raw_mode = mode == MODE_RAW;
+    fake_mode = mode;
     pthread_mutex_unlock(&mu);
 }
 
@@ -306,9 +351,8 @@ static const char *kStd = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0
 
 /* Decode `pre` sextets then chars[0..n): whole groups (hold) or
  * floor(6V/8) bytes; returns the record. */
-static b64x_dec_result decode_bits(const uint8_t *pre, unsigned npre, const uint8_t *chars,
-                                   size_t n, const b64x_alphabet *abc, bool hold,
-                                   uint8_t *out)
+static b64x_dec_result decode_bits(const uint8_t *chars, size_t n, const b64x_alphabet *abc,
+                                   bool hold, uint32_t seq, uint8_t *out)
 {
     int8_t t[256];
     dec_table(abc, t);
@@ -316,8 +360,8 @@ static b64x_dec_result decode_bits(const uint8_t *pre, unsigned npre, const uint
     memset(&r, 0, sizeof r);
     uint64_t V = 0, bits = 0, nb = 0, olen = 0;
     uint8_t last[4] = {0, 0, 0, 0};
-    for (size_t i = 0; i < npre + n; i++) {
-        int v = i < npre ? pre[i] : t[chars[i - npre]];
+    for (size_t i = 0; i < n; i++) {
+        int v = t[chars[i]];
         if (v < 0)
             continue;
         last[V & 3] = (uint8_t) v;
@@ -334,6 +378,9 @@ static b64x_dec_result decode_bits(const uint8_t *pre, unsigned npre, const uint
     r.out_len = hold ? V / 4 * 3 : V * 6 / 8;
     for (uint32_t k = 0; k < r.tail_n; k++)
         r.tail[k] = last[(V - r.tail_n + k) & 3];
+    r.nchars = n;
+    r.seq = seq;
+    r.flags = hold ? 1u : 0u;
     (void) olen; /* the first out_len bytes are the stream's; the rest is scratch */
     return r;
 }
@@ -342,9 +389,9 @@ struct b64x_session {
     uint64_t cap;
     uint8_t *h_in, *h_out;
     b64x_dec_result h_res;   /* the host-visible record */
-    b64x_dec_result d_res;   /* the "device" record: what chaining reads */
     uint64_t res_len;
     unsigned res_flags;
+    uint32_t res_seq;
 };
 
 static b64x_session *spool[64];
@@ -417,27 +464,21 @@ int b64x_session_wait(b64x_session *s)
 }
 
 int b64x_session_decode_async(b64x_session *s, uint64_t n, const b64x_alphabet *abc,
-                              unsigned flags, const b64x_session *carry_from,
-                              b64x_done_fn done, void *arg)
+                              unsigned flags, b64x_done_fn done, void *arg)
 {
-    if (!s || n > s->cap || carry_from == s)
+    if (!s || n > s->cap)
         return -EINVAL;
     fjob *j = calloc(1, sizeof *j);
     j->owner = s;
     j->out_src = malloc(b64x_decoded_cap(n + 4) + 16);
-    uint8_t pre[4];
-    unsigned npre = 0;
-    if (carry_from) /* the device-side record of its last decode */
-        for (; npre < carry_from->d_res.tail_n && npre < 3; npre++)
-            pre[npre] = carry_from->d_res.tail[npre];
-    j->res = decode_bits(pre, npre, s->h_in, n, abc, flags & B64X_DEC_HOLD_TAIL, j->out_src);
-    s->d_res = j->res;
+    s->res_seq = next_seq();
+    j->res = decode_bits(s->h_in, n, abc, flags & B64X_DEC_HOLD_TAIL, s->res_seq, j->out_src);
     j->out_n = j->res.out_len;
     j->out_dst = s->h_out;
     j->res_dst = &s->h_res;
     j->done = done;
     j->arg = arg;
-    s->res_len = n + npre;
+    s->res_len = n;
     s->res_flags = flags;
     pthread_mutex_lock(&mu);
     flush_parked(s); /* the previous launch lands before the poison */
@@ -470,16 +511,17 @@ int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res)
         *res = *(volatile b64x_dec_result *) &s->h_res;
         return 0;
     }
-    if (b64x_result_ok(&s->h_res, s->res_len, s->res_flags, res))
+    if (b64x_result_ok(&s->h_res, s->res_len, s->res_flags, s->res_seq, res))
         return 0;
     atomic_fetch_add(&g_early_session, 1);
     owner_wait(s);
-    return b64x_result_ok(&s->h_res, s->res_len, s->res_flags, res) ? 0 : -EIO;
+    return b64x_result_ok(&s->h_res, s->res_len, s->res_flags, s->res_seq, res) ? 0 : -EIO;
 }
 
 struct b64x_lane {
     uint64_t stamp; /* the "host memory" stamp, published with a batch */
     uint64_t seq;   /* the last encode batch queued */
+    uint32_t dseq;  /* the last decode batch's sequence number */
 };
 
 b64x_lane *b64x_lane_acquire(void)
@@ -545,10 +587,11 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     size_t total = njobs ? h_out_off[njobs] : 0;
     j->out_src = malloc(total + 16);
     j->recs = calloc(njobs ? njobs : 1, sizeof *j->recs);
+    l->dseq = next_seq();
     for (uint32_t k = 0; k < njobs; k++) {
         size_t n = h_in_off[k + 1] - h_in_off[k];
-        j->recs[k] = decode_bits(NULL, 0, h_in + h_in_off[k], n, abc,
-                                 h_flags[k] & B64X_DEC_HOLD_TAIL, j->out_src + h_out_off[k]);
+        j->recs[k] = decode_bits(h_in + h_in_off[k], n, abc, h_flags[k] & B64X_DEC_HOLD_TAIL,
+                                 l->dseq, j->out_src + h_out_off[k]);
     }
     j->out_dst = h_out;
     j->out_n = total;
@@ -568,15 +611,27 @@ int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t
 {
     bool ok = true;
     for (uint32_t k = 0; k < njobs && ok && !raw_mode; k++)
-        ok = b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], NULL);
+        ok = b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], l->dseq, NULL);
     if (ok)
         return 0;
     atomic_fetch_add(&g_early_lane, 1);
     owner_wait(l);
     for (uint32_t k = 0; k < njobs; k++)
-        if (!b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], NULL))
+        if (!b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], l->dseq, NULL))
             return -EIO;
     return 0;
+}
+
+/* The product's record check on a caller's record (tests/test_stage_fake.py
+ * checks what it accepts and rejects). */
+int fake_result_ok(const b64x_dec_result *r, uint64_t len, unsigned flags, uint32_t seq)
+{
+    return b64x_result_ok(r, len, flags, seq, NULL);
+}
+
+void fake_poison(b64x_dec_result *r)
+{
+    b64x_poison_result(r);
 }
 
 /* The harness's multi-GPU driver asks the HIP runtime for devices. */

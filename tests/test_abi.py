@@ -199,3 +199,54 @@ def test_core_library_dependencies():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     for n in ours:
         assert f"`{n}" in doc, n
+
+
+def test_edges_arriving_after_quit_are_kept():
+    """Two descriptors become readable in the same poll; the action of the
+    first one quits the loop.  The second edge is not dropped (an
+    edge-triggered registration would never report it again): it is
+    delivered when the loop runs again, as the reference's loop delivers
+    every triggered event (src/async.c:300-330)."""
+    L = _lib.load()
+
+    class Action(ctypes.Structure):
+        _fields_ = [("obj", ctypes.c_void_p), ("act", ctypes.c_void_p)]
+
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    L.make_async.restype = ctypes.c_void_p
+    L.async_now.argtypes = [ctypes.c_void_p]
+    L.async_now.restype = ctypes.c_uint64
+    L.async_register.argtypes = [ctypes.c_void_p, ctypes.c_int, Action]
+    L.async_unregister.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.async_timer_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, Action]
+    L.async_timer_start.restype = ctypes.c_void_p
+    L.async_loop.argtypes = [ctypes.c_void_p]
+    L.async_quit_loop.argtypes = [ctypes.c_void_p]
+    L.destroy_async.argtypes = [ctypes.c_void_p]
+    async_ = L.make_async()
+    calls = []
+    on_fd = CB(lambda obj: (calls.append(obj), L.async_quit_loop(async_)))
+    on_quit = CB(lambda obj: L.async_quit_loop(async_))
+    quit_addr = ctypes.cast(on_quit, ctypes.c_void_p).value
+    fd_addr = ctypes.cast(on_fd, ctypes.c_void_p).value
+    p1, p2 = os.pipe(), os.pipe()
+    try:
+        assert L.async_register(async_, p1[0], Action(1, fd_addr)) == 0
+        assert L.async_register(async_, p2[0], Action(2, fd_addr)) == 0
+        L.async_timer_start(async_, L.async_now(async_) + 30 * 1000000, Action(None, quit_addr))
+        assert L.async_loop(async_) == 0   # spurious registration calls, if any
+        calls.clear()
+        os.write(p1[1], b"x")
+        os.write(p2[1], b"y")
+        assert L.async_loop(async_) == 0   # the first action quits
+        assert len(calls) == 1
+        L.async_timer_start(async_, L.async_now(async_) + 30 * 1000000, Action(None, quit_addr))
+        assert L.async_loop(async_) == 0
+        assert sorted(calls) == [1, 2]
+        assert L.async_unregister(async_, p1[0]) == 0
+        assert L.async_unregister(async_, p2[0]) == 0
+    finally:
+        for a, b in (p1, p2):
+            os.close(a)
+            os.close(b)
+        L.destroy_async(async_)

@@ -31,9 +31,18 @@ def genc(data, pos62=-1, pos63=-1, pad=True, padchar=-1) -> bytes:
     return b64.encode(dev(data), abc=(pos62, pos63, pad, padchar)).cpu().numpy().tobytes()
 
 
+def _named(info, n, hold):
+    """The device record names its call (include/b64x.h b64x_dec_result)."""
+    assert info.nchars == n and info.seq != 0 and info.flags == int(hold), \
+        (info.nchars, n, info.seq, info.flags)
+    for k in range(4):
+        assert (info.tail[k] < 64) if k < info.tail_n else info.tail[k] == 0
+    return info
+
+
 def gdec(chars, pos62=-1, pos63=-1, hold=False):
     d = b64.decode(dev(chars), abc=(pos62, pos63, True, -1), hold_tail=hold)
-    return d.bytes().cpu().numpy().tobytes(), d.info()
+    return d.bytes().cpu().numpy().tobytes(), _named(d.info(), len(chars), hold)
 
 
 def test_device_and_library():
@@ -400,7 +409,7 @@ def test_library_workspace_per_stream():
         dirty = _junk(rng, chars, 0.01 * (k + 1))
         x = dev(dirty)
         out = torch.empty(b64.decoded_cap(len(dirty)), dtype=torch.uint8, device=DEV)
-        res = torch.zeros(24, dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
         jobs.append((x, out, res, raw))
     a = b64._abc(None)
     torch.cuda.synchronize()
@@ -558,7 +567,7 @@ def test_decode_long_ranges_vs_oracle(chunks):
     def hdec(chars: bytes, hold: bool):
         x = dev(chars)
         out = torch.empty(max(b64.decoded_cap(len(chars)), 1), dtype=torch.uint8, device=DEV)
-        res = torch.zeros(24, dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
         ws = torch.zeros(b64.workspace_size(len(chars)), dtype=torch.uint8, device=DEV)
         a = _lib.alphabet()
         _lib.check("b64x_decode_dev", L.b64x_decode_dev(
@@ -591,7 +600,7 @@ def test_decode_long_ranges_vs_oracle(chunks):
 def gdec_j(chars, pos62=-1, pos63=-1, hold=False):
     d = b64.decode(dev(chars), abc=(pos62, pos63, True, -1), hold_tail=hold,
                    expect_junk=True)
-    return d.bytes().cpu().numpy().tobytes(), d.info()
+    return d.bytes().cpu().numpy().tobytes(), _named(d.info(), len(chars), hold)
 
 
 @pytest.mark.parametrize("density", [0.0, 1e-3, 0.05, 0.5])

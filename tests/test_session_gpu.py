@@ -1,7 +1,8 @@
 """Host-memory sessions (include/b64x.h b64x_session_*) and the pipelined
-stages built on them: asynchronous calls,
-device-chained decode carries, and stages forced through many small
-blocks so every carry length crosses a block seam."""
+stages: asynchronous calls, decode carries kept by
+the caller (HOLD_TAIL records, spelled in front of the next block), and
+stages forced through many small blocks so every carry length crosses a
+block seam."""
 import numpy as np
 import pytest
 
@@ -19,33 +20,41 @@ def _dirty(rng, n, pad=True, abc=(-1, -1)):
     return sep.join(chars[i:i + 76] for i in range(0, len(chars), 76))
 
 
+def _spell(tail, abc):
+    """Held-back sextets as alphabet characters (what the stage does,
+    async_amd/csrc/b64_stages.c spell_sextet)."""
+    p62 = "+" if abc[0] == -1 else abc[0]
+    p63 = "/" if abc[1] == -1 else abc[1]
+    std = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789"
+    return "".join(std[v] if v < 62 else (p62 if v == 62 else p63) for v in tail).encode()
+
+
 def _chained_decode(blocks, abc=(-1, -1), cap=None, drain=False):
-    """Decode `blocks` through two alternating sessions, queueing each block
-    before the previous one's result is back on the host (drain=True: after
-    it, so the library sees the carry on the host)."""
-    cap = cap or max(64, max((len(b) for b in blocks), default=0))
+    """Decode `blocks` as one stream through two alternating sessions: every
+    block but the last with HOLD_TAIL, its held-back sextets spelled in
+    front of the next block on the host (the stage's carry).  A block is
+    launched once the previous one's record is back; the session it goes to
+    may still be busy with the block before (drain=True waits for that one
+    first, so the in-place / staged choice sees every result)."""
+    cap = (cap or max(64, max((len(b) for b in blocks), default=0))) + 4
     out = []
+    head = b""
     with Session(cap) as a, Session(cap) as b:
         ss = (a, b)
-        pending = []
-        prev = None
         for i, blk in enumerate(blocks + [b""]):
             s = ss[i % 2]
-            if pending and pending[0] is s:  # refilling s: wait for its last call
-                s.wait()
-                out.append(bytes(s.host_out[:s.result().out_len]))
-                pending.pop(0)
-            s.host_in[:len(blk)] = np.frombuffer(blk, np.uint8)
+            other = ss[(i + 1) % 2]
+            if drain:
+                other.wait()
+            data = head + blk
+            s.host_in[:len(data)] = np.frombuffer(data, np.uint8)
             last = i == len(blocks)
-            if drain and prev is not None:
-                prev.wait()
-            s.decode_async(len(blk), abc + (True, -1), 0 if last else HOLD_TAIL,
-                           carry_from=prev)
-            pending.append(s)
-            prev = s
-        for s in pending:
+            s.decode_async(len(data), abc + (True, -1), 0 if last else HOLD_TAIL)
             s.wait()
-            out.append(bytes(s.host_out[:s.result().out_len]))
+            r = s.result()
+            assert r.nchars == len(data) and r.seq != 0
+            out.append(bytes(s.host_out[:r.out_len]))
+            head = _spell(list(r.tail)[:r.tail_n], abc)
     return b"".join(out)
 
 
@@ -144,8 +153,8 @@ def test_reference_topology_small_slots(monkeypatch):
 def test_chained_decode_in_place_and_staged_blocks():
     """Clean blocks decode in place over PCIe; a session whose last block
     held junk throughout stages its next one (b64x_session_decode_async).
-    Clean and MIME blocks alternate in one chain, so both forms, and carries
-    spelled into host or device headroom, meet at the seams."""
+    Clean and MIME blocks alternate in one chain, so both forms meet at the
+    seams, with their carries."""
     rng = np.random.default_rng(21)
     chars = orc.encode(rng.integers(0, 256, 300000, dtype=np.uint8).tobytes(), pad=False)
     blocks = []
@@ -156,8 +165,8 @@ def test_chained_decode_in_place_and_staged_blocks():
         blocks.append(blk)
     stream = b"".join(blocks)
     assert _chained_decode(blocks) == orc.decode(stream)
-    # Drained chains: empty carries read in place with no carry head, the
-    # rest stage behind a spelled head; ragged cuts give every tail_n.
+    # Drained: every result is seen by the in-place / staged choice; ragged
+    # cuts give every tail_n.
     assert _chained_decode(blocks, drain=True) == orc.decode(stream)
     cuts = np.sort(rng.integers(0, len(stream) + 1, 30))
     ragged = [stream[i:j] for i, j in zip([0, *cuts], [*cuts, len(stream)])]

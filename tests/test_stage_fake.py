@@ -87,6 +87,63 @@ def test_long_decoder_streams_adversarial_orders(small_blocks, seed, pct):
         assert early == batches and counters(L)[1] - e0[1] == batches
 
 
+@pytest.mark.parametrize("mode,seed", [(2, 31), (3, 32)])
+def test_zero_and_torn_records_are_rejected(small_blocks, mode, seed):
+    """Early callbacks that find a well-formed all-zero record (mode 2: what
+    round 1's stage served as an empty block, profiles/r02_diag_notes.md) or
+    a record whose tail bytes have not landed (mode 3): the record names its
+    call (seq, nchars, flags) and its unused tail bytes are checked, so
+    every such batch is caught, waited for and read again -- no stream loses
+    or corrupts a block."""
+    L = fake()
+    L.fake_configure(seed, 100, mode)
+    try:
+        e0 = counters(L)
+        j0 = stats(L)
+        msgs = long_msgs(seed)
+        got, err = util.ingress_stacks(msgs, 4096, lib=L)
+        assert err == 0
+        assert bad_streams(msgs, got) == []
+        batches, early = (a - b for a, b in zip(stats(L), j0))
+        assert early == batches and counters(L)[1] - e0[1] == batches
+    finally:
+        L.fake_configure(1, 0, 0)
+
+
+def test_record_check_names_the_call():
+    """b64x_result_check.h: only this call's finished record passes."""
+    L = fake()
+    from async_amd._lib import DecResult
+    L.fake_result_ok.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_uint32]
+    L.fake_poison.argtypes = [ctypes.c_void_p]
+
+    def rec(valid=10, hold=True, nchars=12, seq=7, tail=None, tail_n=None):
+        r = DecResult()
+        r.valid, r.nchars, r.seq, r.flags = valid, nchars, seq, int(hold)
+        r.tail_n = valid & 3 if tail_n is None else tail_n
+        r.out_len = valid // 4 * 3 if hold else valid * 6 // 8
+        t = [5, 9, 0, 0][:r.tail_n] + [0] * (4 - r.tail_n) if tail is None else tail
+        for k in range(4):
+            r.tail[k] = t[k]
+        return r
+
+    ok = lambda r, n=12, f=1, q=7: L.fake_result_ok(ctypes.addressof(r), n, f, q)  # noqa: E731
+    assert ok(rec())
+    assert ok(rec(valid=11, hold=False), f=0)
+    assert not ok(rec(seq=6))                     # an earlier call's record
+    assert not ok(rec(), q=0)                     # seq 0 is never drawn
+    assert not ok(rec(nchars=13))                 # another length
+    assert not ok(rec(hold=False))                # another flag
+    assert not ok(rec(tail=[5, 64, 0, 0]))        # a held-back byte that is no sextet
+    assert not ok(rec(tail=[5, 9, 1, 0]))         # a stray byte past tail_n
+    assert not ok(rec(valid=13))                  # more sextets than characters
+    zero = DecResult()
+    assert not ok(zero, 0, 0, 7) and not ok(zero)
+    p = rec()
+    L.fake_poison(ctypes.addressof(p))
+    assert not ok(p)
+
+
 def test_round1_raw_read_loses_blocks(small_blocks):
     """The same interleavings with the records read unchecked (round 1):
     blocks are lost -- the test above would have failed before the fix."""
