@@ -87,6 +87,7 @@ SIGNATURES = {
     "b64x_session_host_in": (_vp, [_vp]),
     "b64x_session_host_out": (_vp, [_vp]),
     "b64x_session_encode": (_int, [_vp, _u64, _ap, ctypes.POINTER(_u64)]),
+    "b64x_release_stream": (None, [_vp]),
     "b64x_session_decode": (_int, [_vp, _u64, _ap, ctypes.c_uint, ctypes.POINTER(DecResult)]),
     "b64x_session_encode_async": (_int, [_vp, _u64, _ap, _vp, _vp]),
     "b64x_session_decode_async": (_int, [_vp, _u64, _ap, ctypes.c_uint, _vp, _vp]),

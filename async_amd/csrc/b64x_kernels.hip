@@ -48,7 +48,6 @@
 #include <string.h>
 
 #include <atomic>
-#include <map>
 #include <mutex>
 #include <utility>
 
@@ -3186,8 +3185,19 @@ std::mutex g_mu;
 DeviceInfo g_info[kMaxDevices];
 bool g_info_done[kMaxDevices];
 // Library-owned decode workspaces, one per (device, stream): a workspace
-// carries state from pass 1 to pass 2, so streams must not share one.
-std::map<std::pair<int, void *>, void *> g_ws;
+// carries state from one kernel of a decode to the next, so streams must
+// not share one.  At most kWsCache of them are kept (about 12.7 MiB of HBM
+// each); the least recently used goes when another stream needs one, or
+// when its stream is released (b64x_release_stream).
+struct WsEntry {
+    int dev;
+    void *stream;
+    void *ws;
+    uint64_t used;  // last use (g_ws_tick)
+};
+constexpr int kWsCache = 8;
+WsEntry g_ws[kWsCache];
+uint64_t g_ws_tick;
 
 const DeviceInfo *device_info()
 {
@@ -3401,6 +3411,23 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
     return launch_status();
 }
 
+// Free a cached workspace.  Work still queued on its stream may use it, and
+// the stream itself may have been destroyed since (its handle is then not
+// to be used): wait for the whole device, then free.  Eviction is rare (a
+// ninth stream decoding with a library-owned workspace).  Called with g_mu
+// held.
+static void ws_drop(WsEntry &e)
+{
+    if (!e.ws) return;
+    int prev = 0;
+    (void) hipGetDevice(&prev);
+    (void) hipSetDevice(e.dev);
+    (void) hipDeviceSynchronize();
+    (void) hipFree(e.ws);
+    (void) hipSetDevice(prev);
+    e = WsEntry{};
+}
+
 static void *library_workspace(void *stream, int *err)
 {
     int dev = 0;
@@ -3409,20 +3436,45 @@ static void *library_workspace(void *stream, int *err)
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(g_mu);
-    void *&ws = g_ws[{dev, stream}];
-    if (!ws) {
-        void *p = nullptr;
-        hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
-        if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
-        if (e != hipSuccess) {
-            if (p) (void) hipFree(p);
-            *err = hip_err(e);
-            return nullptr;
+    int victim = -1;
+    for (int i = 0; i < kWsCache; i++) {
+        WsEntry &e = g_ws[i];
+        if (e.ws && e.dev == dev && e.stream == stream) {
+            e.used = ++g_ws_tick;
+            *err = 0;
+            return e.ws;
         }
-        ws = p;
     }
+    for (int i = 0; i < kWsCache && victim < 0; i++)
+        if (!g_ws[i].ws) victim = i;
+    if (victim < 0) {
+        victim = 0;
+        for (int i = 1; i < kWsCache; i++)
+            if (g_ws[i].used < g_ws[victim].used) victim = i;
+    }
+    // A new stream: the least recently used entry (or a free one) goes.
+    ws_drop(g_ws[victim]);
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
+    if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
+    if (e != hipSuccess) {
+        if (p) (void) hipFree(p);
+        *err = hip_err(e);
+        return nullptr;
+    }
+    g_ws[victim] = WsEntry{dev, stream, p, ++g_ws_tick};
     *err = 0;
-    return ws;
+    return p;
+}
+
+void b64x_release_stream(void *stream)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (int i = 0; i < kWsCache; i++)
+        if (g_ws[i].ws && g_ws[i].dev == dev && g_ws[i].stream == stream)
+            ws_drop(g_ws[i]);
 }
 
 __global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres,
@@ -4287,6 +4339,68 @@ int b64x__test_copy_mode(const void *src, void *dst, uint64_t n, void *stream, i
 int b64x__test_copy(const void *src, void *dst, uint64_t n, void *stream)
 {
     return b64x__test_copy_mode(src, dst, n, stream, 0);
+}
+
+// Test builds only: copies with a kernel's own read/write mix, for the copy
+// ceiling of each leg (bench.py): every lane loads IN bytes (dwordx3 or
+// dwordx4, non-temporal) and stores OUT bytes, U of them in flight --
+// encode's 12 -> 16 (3 : 4) and decode's 16 -> 12 (4 : 3), no arithmetic
+// beyond one XOR that makes the stored dwords depend on the loaded ones.
+// `units` lane-steps; one block of TH lanes takes TH * U of them.
+extern "C++" {
+template <int U, int TH, int IN, int OUT>
+__global__ __launch_bounds__(TH) void k_test_mix(const uint8_t *__restrict__ in,
+                                                 uint8_t *__restrict__ out)
+{
+    const uint64_t u0 = (uint64_t) blockIdx.x * TH * U + threadIdx.x;
+    uint32_t v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint8_t *p = in + (u0 + (uint64_t) u * TH) * IN;
+        if (IN == 16) {
+            const uint4 w = ld16<true>(p);
+            v[u][0] = w.x, v[u][1] = w.y, v[u][2] = w.z, v[u][3] = w.w;
+        } else {
+            const u32x3a4 w = ld12<true>(p);
+            v[u][0] = w.x, v[u][1] = w.y, v[u][2] = w.z, v[u][3] = w.x ^ w.z;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        uint8_t *q = out + (u0 + (uint64_t) u * TH) * OUT;
+        if (OUT == 16)
+            store16<true>(q, uint4{v[u][0], v[u][1], v[u][2], v[u][3]});
+        else
+            __builtin_nontemporal_store(u32x3a4{v[u][0], v[u][1] ^ v[u][3], v[u][2]},
+                                        (u32x3a4 *) q);
+    }
+}
+
+template <int U, int TH, int IN, int OUT>
+static int test_mix(const void *src, void *dst, uint64_t units, void *stream)
+{
+    const uint64_t per = (uint64_t) TH * U;
+    if (units % per || ((((uintptr_t) src) | ((uintptr_t) dst)) & 15)) return -EINVAL;
+    hipLaunchKernelGGL((k_test_mix<U, TH, IN, OUT>), dim3((uint32_t) (units / per)), dim3(TH),
+                       0, (hipStream_t) stream, (const uint8_t *) src, (uint8_t *) dst);
+    return launch_status();
+}
+}  // extern "C++"
+
+// mix 0: encode's 12 -> 16, mix 1: decode's 16 -> 12; shape 0..2: U = 1, 2, 4
+// (TH = 256).  `units` must be a multiple of 256 * U.
+int b64x__test_copy_mix(const void *src, void *dst, uint64_t units, void *stream, int mix,
+                        int shape)
+{
+    switch (mix * 3 + shape) {
+    case 0: return test_mix<1, 256, 12, 16>(src, dst, units, stream);
+    case 1: return test_mix<2, 256, 12, 16>(src, dst, units, stream);
+    case 2: return test_mix<4, 256, 12, 16>(src, dst, units, stream);
+    case 3: return test_mix<1, 256, 16, 12>(src, dst, units, stream);
+    case 4: return test_mix<2, 256, 16, 12>(src, dst, units, stream);
+    case 5: return test_mix<4, 256, 16, 12>(src, dst, units, stream);
+    default: return -EINVAL;
+    }
 }
 
 // Test builds only: decode ranges of `chunks` chunks (0 = the default);

@@ -201,18 +201,27 @@ def bench_single(args, world, rank, b64):
             "enc_ms_min": min(enc_ms), "dec_ms_min": min(dec_ms)}
 
 
-def bench_batch(args, world, rank, b64):
-    """BASELINE config 4: 1 M x 1 KiB, sharded across ranks by index."""
+def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
+    """A uniform batch of independent buffers (BASELINE config 4: 1 M x
+    1 KiB; config 3: 65,536 x 4 KiB), split across the ranks by index range
+    (strong scaling: the batch is fixed, each rank owns 1/N of it), strided
+    encode + decode, plus the one exchange step (all-gather of per-rank
+    output totals).  Buffer i holds bytes [i L, (i+1) L) of the splitmix64
+    (0x5EED) stream; buffer 0's characters are checked against the G4
+    digest prefix recorded from the reference and every
+    buffer round-trips bit-exactly before timing."""
+    import hashlib
+
     from async_amd import shard
 
-    total_buf, L = 1 << 20, 1024
     lo, nbuf = shard.by_index(total_buf, world, rank)
     Es = b64.encoded_len(L)
     # decode rows: 12 bytes per 16-character slot (>= capacity; the row kernel
     # writes whole slots, so consecutive rows form one contiguous byte stream)
     cap = 12 * ((Es + 15) // 16)
-    x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
-    b64.fill_splitmix64(x, 0x5EED + lo)
+    x = torch.empty((lo + nbuf) * L, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    x = x[lo * L:].clone()  # this rank's share of the one stream
     enc = torch.empty(nbuf * Es, dtype=torch.uint8, device="cuda")
     dec = torch.empty(nbuf * cap, dtype=torch.uint8, device="cuda")
     outlen = torch.zeros(nbuf, dtype=torch.int64, device="cuda")
@@ -229,7 +238,15 @@ def bench_batch(args, world, rank, b64):
     ok = bool((outlen == L).all()) and bool(torch.equal(dec.view(nbuf, cap)[:, :L],
                                                         x.view(nbuf, L)))
     if not ok:
-        raise SystemExit(f"rank {rank}: batch round trip mismatch")
+        raise SystemExit(f"rank {rank}: {name} batch round trip mismatch")
+    g4 = None
+    if lo == 0:
+        want = _golden_digest(f"G4_{L}")
+        if want is not None:
+            got = hashlib.sha256(enc[:Es].cpu().numpy().tobytes()).hexdigest()
+            g4 = got.startswith(want)
+            if not g4:
+                raise SystemExit(f"{name}: buffer 0 does not match the G4_{L} digest")
     # warm the exchange path too (first reduction / collective launches load
     # their code objects and set up communicators)
     for _ in range(2):
@@ -252,9 +269,12 @@ def bench_batch(args, world, rank, b64):
     mine = time.perf_counter() - t0
     wall = max_over_ranks(mine, world)
     assert int(totals.sum()) == total_buf * L
-    kern_ms = ev[0].elapsed_time(ev[2]) / K
-    rank_frac = (2 * (nbuf * (L + Es))) / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
-    per_rank = gather_floats([nbuf * L * K / mine / 2**30, rank_frac], world)
+    enc_ms = ev[0].elapsed_time(ev[1]) / K
+    dec_ms = ev[1].elapsed_time(ev[2]) / K
+    kern_ms = enc_ms + dec_ms
+    alg = nbuf * (L + Es)  # per leg: read + written
+    rank_frac = 2 * alg / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
+    per_rank = gather_floats([nbuf * L * K / mine / 2**30, rank_frac, enc_ms, dec_ms], world)
     # the exchange step on its own (after the timed region): its latency
     # decides how many ranks a batch of this size amortises (shard.ranks_for)
     exchange_ms, advice = None, None
@@ -268,20 +288,36 @@ def bench_batch(args, world, rank, b64):
         exchange_ms = max_over_ranks(statistics.median(ts), world) * 1e3
         advice = shard.ranks_for(kern_ms * 1e-3 * world, world, exchange_ms * 1e-3)
     return {
-        "workload": "cfg4: 1,048,576 x 1 KiB buffers split across ranks, strided "
+        "workload": f"{name}: {total_buf:,} x {L} B buffers split across ranks, strided "
                     "encode then decode, + allgather of per-rank output totals",
+        "scaling": "strong",
         "buffers_per_rank": nbuf,
         "value": total_buf * L * K / wall / 2**30,
         "unit": "GiB/s",
         "ms_per_step": wall / K * 1e3,
-        "encode_kernel_ms": ev[0].elapsed_time(ev[1]) / K,
-        "decode_kernel_ms": ev[1].elapsed_time(ev[2]) / K,
+        "encode_kernel_ms": enc_ms,
+        "decode_kernel_ms": dec_ms,
+        "encode_roofline_frac": alg / (enc_ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+        "decode_roofline_frac": alg / (dec_ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
         "roofline_frac": rank_frac,
+        "g4_digest_ok": g4,
         "per_rank_GiB_s": [p[0] for p in per_rank],
         "per_rank_roofline_frac": [p[1] for p in per_rank],
+        "per_rank_kernel_ms": [[p[2], p[3]] for p in per_rank],
         "exchange_ms": exchange_ms,
         "ranks_amortised": advice,
     }
+
+
+def _golden_digest(key: str):
+    """A digest prefix from tests/golden/digests.json (recorded from the
+    reference); None when the file is absent."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+            d = json.load(f)[key]
+    except (OSError, KeyError, ValueError):
+        return None
+    return d.get("out_sha256_prefix") or d.get("out_sha256")
 
 
 def bench_host_inclusive(args, b64):
@@ -471,116 +507,170 @@ def bench_mime(args, b64, steps=10):
     return {"cfg2_crlf76": single, "cfg4_crlf76": batch, "unit": "ms, GiB/s payload"}
 
 
-def bench_cfg5(args):
-    """BASELINE config 5 on this GPU: 16,384 Zipf messages (64 B - 1 MiB,
-    SURVEY.md §8(d)), each its own queuestream -> GPU base64encoder stage ->
+def bench_cfg5(args, world=1, rank=0):
+    """BASELINE config 5: 16,384 Zipf messages (64 B - 1 MiB, SURVEY.md
+    §8(d)), each its own queuestream -> GPU base64encoder stage ->
     chunkencoder(1 MiB) stack of the product's C API, drained 10,240 bytes
     per read (the reference's tcp_connection.c:22 pull size); host memory in,
     framed host memory out, so the rate includes every pinned copy and PCIe
     crossing.  T event loops (threads, one batching hub each) share the
-    messages; T = 1 and 16 (the box's CPU share).  Beside it, the oracle's
-    restatement of the same stack on the same thread counts, whose outputs
-    check a sample of the GPU stacks' (cpu_baseline's checker role)."""
+    messages.
+
+    One GPU: T = 1 and 16 (the box's CPU share), with the oracle's
+    restatement of the same stack timed beside it on the same thread counts
+    (whose outputs check a sample of the GPU stacks': cpu_baseline's checker
+    role).  N GPUs: each rank takes its byte-balanced share of the messages
+    (shard.by_bytes) on its own GPU, every loop of the rank on that GPU, 16
+    loops per rank; the aggregate is all messages' bytes over the slowest
+    rank's time (median of three passes, each started from a barrier); a
+    sample of each rank's messages is checked against the oracle."""
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
 
+    from async_amd import shard
     from oracle import pyoracle as orc
     from tests import util
 
     lens = util.zipf_lengths()
-    payload = util.splitmix64(0x5EED, int(lens.sum()))
+    nbytes_all = int(lens.sum())
+    offs_all = np.concatenate([[0], np.cumsum(lens)])
+    bounds = shard.by_bytes(lens.tolist(), world)
+    b0, b1 = bounds[rank], bounds[rank + 1]
+    payload = util.splitmix64(0x5EED, int(offs_all[b1]))[int(offs_all[b0]):]
+    lens = lens[b0:b1]
     nbytes = int(lens.sum())
     offs = np.concatenate([[0], np.cumsum(lens)])
-    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
-    out = {"workload": f"cfg5: {lens.size} Zipf messages, {nbytes} bytes, "
+    device = torch.cuda.current_device()
+    util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240, device=device)  # warm-up
+    out = {"workload": f"cfg5: {offs_all.size - 1} Zipf messages, {nbytes_all} bytes, "
                        "queuestream -> encoder -> chunkencoder(1 MiB), 10,240-byte reads",
            "unit": "GiB/s of payload, host memory to host memory"}
-    sample = list(range(0, lens.size, lens.size // 64))
-    for T in (1, min(16, args.cpu_threads)):
+    if world > 1:
+        out["shards"] = {"by": "shard.by_bytes", "messages_per_rank":
+                         [bounds[i + 1] - bounds[i] for i in range(world)]}
+    sample = list(range(0, lens.size, max(1, lens.size // 64)))
+    loop_counts = (1, min(16, args.cpu_threads)) if world == 1 else (min(16, args.cpu_threads),)
+    for T in loop_counts:
         # one untimed pass first: T loops' hubs, lanes (HIP streams) and pinned
         # arenas come from process-wide pools, filled on first use
-        util.egress_stacks(payload, lens, 1 << 20, 10240, raw=True, threads=T)
+        util.egress_stacks(payload, lens, 1 << 20, 10240, raw=True, threads=T, device=device)
         # three timed passes, the median reported: the leg is host-bound and a
         # single pass varied 2x from box to box (profiles/README.md, r02_v25)
         passes = []
         for _ in range(3):
             times = np.zeros(2)
+            sync_all(world)
+            t0 = time.perf_counter()
             res, err = util.egress_stacks(payload, lens, 1 << 20, 10240, times=times,
-                                          raw=True, threads=T)
+                                          raw=True, threads=T, device=device)
+            mine = time.perf_counter() - t0
             if res is None:
-                raise SystemExit(f"cfg5 egress failed: errno {err}")
-            passes.append((float(times.sum()), times.copy()))
+                raise SystemExit(f"cfg5 egress failed on rank {rank}: errno {err}")
+            wall = max_over_ranks(mine, world)
+            passes.append((wall, times.copy()))
             if len(passes) < 3:
                 del res
-        passes.sort(key=lambda p: p[0])
-        dt, times = passes[1]
+        order = sorted(range(3), key=lambda i: passes[i][0])
+        dt, times = passes[order[1]]
         framed, f_off, f_len = res
-
-        def work(t, T=T):
-            cuts = np.searchsorted(offs, np.linspace(0, nbytes, T + 1))
-            for i in range(cuts[t], cuts[t + 1]):
-                orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
-                                   read_size=10240)
-        t0 = time.perf_counter()
-        with ThreadPoolExecutor(T) as ex:
-            list(ex.map(work, range(T)))
-        cpu_dt = time.perf_counter() - t0
         for i in sample:
             want = orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
                                       read_size=10240)
             if framed[int(f_off[i]):int(f_off[i]) + int(f_len[i])].tobytes() != want:
-                raise SystemExit(f"cfg5 egress mismatch at message {i}")
-        out[f"loops_{T}"] = {"GiB_s": nbytes / dt / 2**30, "seconds": dt,
-                             "GiB_s_passes": [nbytes / p[0] / 2**30 for p in passes],
-                             "setup_s": float(times[0]), "loop_s": float(times[1]),
-                             "framed_bytes": int(f_len.sum()),
-                             "cpu_port_GiB_s": nbytes / cpu_dt / 2**30, "cpu_threads": T}
+                raise SystemExit(f"cfg5 egress mismatch at message {b0 + i}")
+        leg = {"GiB_s": nbytes_all / dt / 2**30, "seconds": dt,
+               "GiB_s_passes": [nbytes_all / p[0] / 2**30 for p in passes],
+               "setup_s": float(times[0]), "loop_s": float(times[1]),
+               "loops_per_gpu": T, "n_gpus": world}
+        if world == 1:
+            def work(t, T=T):
+                cuts = np.searchsorted(offs, np.linspace(0, nbytes, T + 1))
+                for i in range(cuts[t], cuts[t + 1]):
+                    orc.chunked_encode(payload[offs[i]:offs[i + 1]], max_chunk=1 << 20,
+                                       read_size=10240)
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(T) as ex:
+                list(ex.map(work, range(T)))
+            cpu_dt = time.perf_counter() - t0
+            leg.update({"framed_bytes": int(f_len.sum()),
+                        "cpu_port_GiB_s": nbytes / cpu_dt / 2**30, "cpu_threads": T})
+        else:
+            leg["framed_bytes"] = int(sum(v[0] for v in gather_floats([float(f_len.sum())],
+                                                                        world)))
+        out[f"loops_{T}"] = leg
         del framed, res
     return out
 
 
-def copy_ceiling(nbytes: int, steps: int = 20) -> dict | None:
+def copy_ceilings(N: int, E: int, steps: int = 20) -> dict | None:
     """The measured copy bandwidth SURVEY.md 8(d) asks the roofline to be
-    read against: a copy moving the same bytes as one launch of the path
-    (nbytes read + written in total) with the kernels' own access shape --
-    16-byte non-temporal loads and stores, 4 per lane in flight, a
-    non-persistent grid (k_test_copy in the test-hooks build of the kernels,
-    tests/csrc/libb64x_hooks.so; HIP's blit copy reaches only ~5.1 TB/s) --
-    median of `steps` runs after 3 warm-ups, HIP events on torch's stream."""
+    read against, per leg: the best of several copy kernels moving the same
+    bytes as one launch of the leg (test-hooks build of the kernels,
+    tests/csrc/libb64x_hooks.so; HIP's blit copy reaches only ~5.1 TB/s):
+      - plain 16-byte non-temporal copies (half the bytes read, half
+        written) in the sweep's shapes (1, 4 lanes' loads in flight; 256-
+        and 1024-thread blocks; profiles/r02_copy_sweep.jsonl);
+      - copies with the leg's own read/write mix: encode reads 12 bytes per
+        lane and writes 16 (3 : 4), decode reads 16 and writes 12 (4 : 3),
+        1, 2 or 4 in flight per lane.
+    Each candidate: median of `steps` runs after 3 warm-ups, HIP events on
+    torch's stream; the ceiling is the fastest candidate (GB/s of read +
+    written bytes)."""
     import ctypes
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "csrc",
-                        "libb64x_hooks.so")
+    path = os.path.join(ROOT, "tests", "csrc", "libb64x_hooks.so")
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
-    lib.b64x__test_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                    ctypes.c_void_p]
-    lib.b64x__test_copy.restype = ctypes.c_int
-    per = 256 * 4 * 16
-    half = nbytes // 2 // per * per
-    src = torch.empty(half, dtype=torch.uint8, device="cuda")
+    for fn in (lib.b64x__test_copy_mode,):
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                       ctypes.c_int]
+        fn.restype = ctypes.c_int
+    lib.b64x__test_copy_mix.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.b64x__test_copy_mix.restype = ctypes.c_int
+    stream = torch.cuda.current_stream().cuda_stream
+    src = torch.empty(max(N, E) + 4096, dtype=torch.uint8, device="cuda")
     dst = torch.empty_like(src)
     src.fill_(7)
-    stream = torch.cuda.current_stream().cuda_stream
-    ts = []
-    for i in range(steps + 3):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        rc = lib.b64x__test_copy(src.data_ptr(), dst.data_ptr(), half, stream)
-        b.record()
-        b.synchronize()
-        if rc:
-            raise RuntimeError(f"b64x__test_copy: {rc}")
-        if i >= 3:
-            ts.append(a.elapsed_time(b))
-    ok = bool(torch.equal(dst[:: 1 << 20], src[:: 1 << 20]))
-    ms = sorted(ts)[len(ts) // 2]
+
+    def timed(launch):
+        ts = []
+        for i in range(steps + 3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            rc = launch()
+            b.record()
+            b.synchronize()
+            if rc:
+                raise RuntimeError(f"test copy: {rc}")
+            if i >= 3:
+                ts.append(a.elapsed_time(b))
+        return sorted(ts)[len(ts) // 2]
+
+    plain = {}
+    half = (N + E) // 2 // (1024 * 4 * 16) * (1024 * 4 * 16)
+    for mode, shape in ((0, "U4 TH256"), (1, "U1 TH256"), (8, "U1 TH1024")):
+        ms = timed(lambda: lib.b64x__test_copy_mode(src.data_ptr(), dst.data_ptr(), half,
+                                                    stream, mode))
+        plain[shape] = 2 * half / (ms * 1e-3) / 1e9
+    ok = bool((dst[:half:1 << 16] == 7).all())  # the copies did move the bytes
+    out = {"plain_GBps": plain, "checked": ok}
+    for leg, mix, ib, ob, n_in in (("encode", 0, 12, 16, N), ("decode", 1, 16, 12, E)):
+        best = max(plain.values())
+        how = "plain " + max(plain, key=plain.get)
+        for shape, U in enumerate((1, 2, 4)):
+            units = n_in // ib // (256 * U) * (256 * U)
+            ms = timed(lambda: lib.b64x__test_copy_mix(src.data_ptr(), dst.data_ptr(), units,
+                                                       stream, mix, shape))
+            gbps = units * (ib + ob) / (ms * 1e-3) / 1e9
+            if gbps > best:
+                best, how = gbps, f"mix {ib}->{ob} U{U} TH256"
+        out[leg] = {"GBps": best, "best": how}
     del src, dst
-    return {"GBps": 2 * half / (ms * 1e-3) / 1e9, "ms": ms, "bytes_moved": 2 * half,
-            "checked": ok,
-            "how": "k_test_copy (tests/csrc/libb64x_hooks.so): 16-B nt loads/stores, 4 per "
-                   f"lane, median of {steps} after 3 warm-ups"}
+    out["how"] = ("fastest of plain 16-B nt copies (sweep shapes) and copies with the leg's "
+                  f"read/write mix, median of {steps} after 3 warm-ups")
+    return out
 
 
 def bench_root_scatter(world, rank, nbytes=1 << 30, steps=3):
@@ -687,6 +777,35 @@ def cpu_baseline(args, b64):
     }
 
 
+def dry_run_plans(world: int, rank: int) -> dict:
+    """What the scaled legs do across ranks, without a GPU: config 4's and
+    config 3's index shares and the one exchange (the all-gather of per-rank
+    output totals, each rank contributing what its share would decode to),
+    and config 5's byte-balanced message shares."""
+    from async_amd import shard
+    from tests import util
+
+    curve = {"leg": "batch_cfg4", "scaling": "strong", "n_gpus": world}
+    for name, total_buf, L in (("cfg4", 1 << 20, 1024), ("cfg3", 1 << 16, 4096)):
+        lo, nbuf = shard.by_index(total_buf, world, rank)
+        off, totals = shard.exchange_totals(nbuf * L, device=coll_device())
+        if sum(totals) != total_buf * L or off != lo * L:
+            raise SystemExit(f"{name}: exchange gave {totals}, offset {off}")
+        shares = [int(v[0]) for v in gather_floats([float(nbuf)], world)]
+        if name == "cfg4":
+            curve.update({"buffers_per_rank": shares, "output_offsets_ok": True})
+        else:
+            curve["cfg3_buffers_per_rank"] = shares
+    lens = util.zipf_lengths()
+    bounds = shard.by_bytes(lens.tolist(), world)
+    per_rank_bytes = [int(lens[bounds[i]:bounds[i + 1]].sum()) for i in range(world)]
+    return {"scaling_curve": curve,
+            "cfg5_egress": {"shards": {"by": "shard.by_bytes",
+                                       "messages_per_rank": [bounds[i + 1] - bounds[i]
+                                                             for i in range(world)],
+                                       "bytes_per_rank": per_rank_bytes}}}
+
+
 def launch_ranks(args) -> int:
     """--gpus N > 1 without a launcher: start one rank per GPU under
     torch.distributed.run as a child process (nothing here has touched the
@@ -731,15 +850,17 @@ def main():
                   f"--gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
     if args.dry_run:
-        # the launch and the process group only (CPU tests, gloo): no GPU work
+        # the launch, the process group and the multi-rank plans of the
+        # scaled legs, with their collectives (CPU tests, gloo): no GPU work
         ranks = gather_floats([float(rank)], world)
         scatter = bench_root_scatter(world, rank, nbytes=1 << 20, steps=2)
+        plan = dry_run_plans(world, rank)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world,
                               "process_group": {"backend": dist.get_backend() if world > 1
                                                 else None, "world_size": world},
                               "ranks_seen": [int(r[0]) for r in ranks],
-                              "root_scatter": scatter}), flush=True)
+                              "root_scatter": scatter, **plan}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -747,8 +868,10 @@ def main():
 
     b64.device_check()
     r = bench_single(args, world, rank, b64)
-    ceiling = copy_ceiling(r["N"] + r["E"]) if rank == 0 else None
+    ceiling = copy_ceilings(r["N"], r["E"]) if rank == 0 else None
     batch = None if args.no_batch else bench_batch(args, world, rank, b64)
+    batch3 = None if args.no_batch else bench_batch(args, world, rank, b64, 1 << 16, 4096,
+                                                    "cfg3")
     scatter = bench_root_scatter(world, rank)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -760,8 +883,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_mime and args.size == 1 << 30:
         mime = bench_mime(args, b64)
     cfg5 = None
-    if rank == 0 and world == 1 and not args.no_cfg5 and not args.no_cpu:
-        cfg5 = bench_cfg5(args)
+    if not args.no_cfg5 and (world > 1 or not args.no_cpu):
+        cfg5 = bench_cfg5(args, world, rank)
 
     if rank == 0:
         N, E, K = r["N"], r["E"], r["K"]
@@ -809,14 +932,29 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "copy_ceiling_GBps": ceiling["GBps"] if ceiling else None,
-                "frac_of_copy": achieved / ceiling["GBps"] if ceiling else None,
+                "copy_ceiling_GBps": ceiling[dom]["GBps"] if ceiling else None,
+                "frac_of_copy": achieved / ceiling[dom]["GBps"] if ceiling else None,
+                "frac_of_copy_per_leg": {
+                    "encode": per_launch / (r["enc_ms"] * 1e-3) / 1e9 / ceiling["encode"]["GBps"],
+                    "decode": per_launch / (r["dec_ms"] * 1e-3) / 1e9 / ceiling["decode"]["GBps"],
+                } if ceiling else None,
                 "copy_ceiling": ceiling,
                 # the committed PMC summary is for the 1 GiB workload
                 "traffic": load_traffic(knames) if N == 1 << 30 else None,
             },
+            # the north star's 1 -> 2 -> 4 -> 8 curve: config 4's fixed batch of
+            # 1 M buffers, strong-scaled over the ranks (batch_cfg4); `value`
+            # above is config 2, one buffer per rank (weak)
+            "scaling_curve": {
+                "leg": "batch_cfg4", "scaling": "strong", "n_gpus": world,
+                "GiB_s": batch["value"] if batch else None,
+                "per_rank_kernel_ms": batch["per_rank_kernel_ms"] if batch else None,
+                "exchange_ms": batch["exchange_ms"] if batch else None,
+                "ranks_amortised": batch["ranks_amortised"] if batch else None,
+            },
             "cpu_baseline": cpu,
             "batch_cfg4": batch,
+            "batch_cfg3": batch3,
             "host_inclusive": host,
             "root_scatter": scatter,
             "mime_decode": mime,

@@ -111,10 +111,16 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * zero-filled before its first use (each call leaves it ready for the
  * next; one workspace per stream), or NULL to use a library-owned one
  * per (device, stream) (allocated on the first such call for that stream:
- * that call is not capture-safe). */
+ * that call is not capture-safe).  The library keeps at most 8 such
+ * workspaces (about 12.7 MiB of HBM each): a call on a ninth stream waits
+ * for the least recently used one's stream and frees its workspace. */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);
+/* Free the library-owned decode workspace of `stream` on the current device,
+ * if it has one (after waiting for the device); call it before destroying a
+ * stream that decoded with d_workspace == NULL. */
+void b64x_release_stream(void *stream);
 
 /* ---- batches of independent buffers ----------------------------------- */
 

@@ -617,11 +617,37 @@ int h_egress_stacks_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
                                   padchar, out, out_off, out_len, err_out, times, nthreads, 1);
 }
 
+static int egress_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg, size_t max_chunk,
+                     size_t read_size, char pos62, char pos63, int pad, char padchar,
+                     uint8_t *out, const uint64_t *out_off, uint64_t *out_len, int *err_out,
+                     double *times, size_t nthreads, int ndevices, int device);
+
 int h_egress_stacks_mt_dev(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
                            size_t max_chunk, size_t read_size, char pos62, char pos63,
                            int pad, char padchar, uint8_t *out, const uint64_t *out_off,
                            uint64_t *out_len, int *err_out, double *times,
                            size_t nthreads, int ndevices)
+{
+    return egress_mt(in, in_off, nmsg, max_chunk, read_size, pos62, pos63, pad, padchar, out,
+                     out_off, out_len, err_out, times, nthreads, ndevices, -1);
+}
+
+/* Every loop on GPU `device` (a rank of a multi-GPU run: threads start on
+ * device 0, whatever the process's main thread selected). */
+int h_egress_stacks_mt_on(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
+                          size_t max_chunk, size_t read_size, char pos62, char pos63,
+                          int pad, char padchar, uint8_t *out, const uint64_t *out_off,
+                          uint64_t *out_len, int *err_out, double *times, size_t nthreads,
+                          int device)
+{
+    return egress_mt(in, in_off, nmsg, max_chunk, read_size, pos62, pos63, pad, padchar, out,
+                     out_off, out_len, err_out, times, nthreads, 1, device);
+}
+
+static int egress_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg, size_t max_chunk,
+                     size_t read_size, char pos62, char pos63, int pad, char padchar,
+                     uint8_t *out, const uint64_t *out_off, uint64_t *out_len, int *err_out,
+                     double *times, size_t nthreads, int ndevices, int device)
 {
     if (nthreads < 1)
         nthreads = 1;
@@ -645,6 +671,8 @@ int h_egress_stacks_mt_dev(const uint8_t *in, const uint64_t *in_off, size_t nms
         if (ndevices > 1) {  /* loop t on GPU t mod ndevices (mod what exists) */
             const int have = h_device_count();
             sh[t].device = have > 0 ? (int) (t % (size_t) ndevices) % have : 0;
+        } else if (device >= 0) {
+            sh[t].device = device;
         }
         first = last;
     }

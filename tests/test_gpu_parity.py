@@ -760,3 +760,42 @@ def test_strided_mime_rows_vs_oracle(n, L, sep):
         want = orc.decode(r + b"\n" * (stride - len(r)))
         assert ol[i] == len(want), i
         assert dh[i * cap:i * cap + ol[i]].tobytes() == want, i
+
+
+def test_library_workspace_is_bounded():
+    """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
+    library workspaces (~12.7 MiB of HBM each), not one per stream forever;
+    b64x_release_stream frees a stream's one; every result stays exact."""
+    import ctypes
+
+    from async_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(31)
+    raw = rng.integers(0, 256, 30000, dtype=np.uint8)
+    text = dev(b"\r\n".join(orc.encode(raw)[i:i + 76] for i in range(0, 40000, 76)))
+    a = b64._abc(None)
+    ws_bytes = b64.workspace_size(0)
+
+    def run(st):
+        out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+        rc = lib.b64x_decode_dev(ctypes.c_void_p(text.data_ptr()), text.numel(),
+                                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                 ctypes.byref(a), 0, None, ctypes.c_void_p(st.cuda_stream))
+        assert rc == 0
+        st.synchronize()
+        assert np.array_equal(out[:raw.size].cpu().numpy(), raw)
+
+    keep = [torch.cuda.Stream() for _ in range(100)]
+    run(keep[0])  # first use of the path (code objects, one workspace)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for st in keep[1:]:
+        run(st)
+    torch.cuda.synchronize()
+    grew = free0 - torch.cuda.mem_get_info()[0]
+    assert grew < 8 * ws_bytes + (64 << 20), grew  # unbounded: 99 x 12.7 MiB
+    for st in keep:
+        lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
+    run(keep[5])  # a released stream gets a fresh workspace
+    lib.b64x_release_stream(ctypes.c_void_p(keep[5].cuda_stream))

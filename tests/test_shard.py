@@ -12,6 +12,7 @@ import torch.multiprocessing as mp
 
 from async_amd import shard
 from oracle import pyoracle as orc
+from tests import util
 
 
 def test_by_index_covers_everything():
@@ -132,6 +133,16 @@ def test_bench_self_launches_ranks():
     assert lines[0]["ranks_seen"] == [0, 1]
     sc = lines[0]["root_scatter"]  # the scatter leg runs over the same group
     assert "error" not in sc and sc["ms"] > 0
+    # the scaled legs' multi-rank plans: config 4 strong-scaled over the
+    # ranks (the north star's curve) with its exchange, config 5's shares
+    curve = lines[0]["scaling_curve"]
+    assert curve["leg"] == "batch_cfg4" and curve["scaling"] == "strong"
+    assert curve["buffers_per_rank"] == [1 << 19, 1 << 19] and curve["output_offsets_ok"]
+    assert curve["cfg3_buffers_per_rank"] == [1 << 15, 1 << 15]
+    c5 = lines[0]["cfg5_egress"]["shards"]
+    assert sum(c5["messages_per_rank"]) == 16384
+    b = c5["bytes_per_rank"]
+    assert abs(b[0] - b[1]) <= (1 << 20) and sum(b) == int(util.zipf_lengths().sum())
 
 
 def test_bench_refuses_a_mismatched_world():

@@ -119,6 +119,7 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_egress_stacks_mt.argtypes = L.h_egress_stacks.argtypes + [sz]
     L.h_egress_stacks_mt.restype = ctypes.c_int
     L.h_egress_stacks_mt_dev.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
+    L.h_egress_stacks_mt_on.argtypes = L.h_egress_stacks.argtypes + [sz, ctypes.c_int]
     L.h_egress_stacks_mt_dev.restype = ctypes.c_int
     L.h_ingress_stacks.argtypes = [vp, vp, sz, sz, ch, ch, vp, vp, vp, ip, vp]
     L.h_ingress_stacks.restype = ctypes.c_int
@@ -254,9 +255,10 @@ def device_count() -> int:
 
 def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos62=-1,
                   pos63=-1, pad=True, padchar=-1, times=None, raw=False, threads=1,
-                  devices=1, lib=None):
+                  devices=1, device=None, lib=None):
     """Run len(lens) GPU egress stacks on `threads` loops (loop t on GPU
-    t mod `devices` when devices > 1); returns
+    t mod `devices` when devices > 1, every loop on GPU `device` when it is
+    given); returns
     (list of framed bytes | None, errno).  `times` (a float64[2] array)
     receives the C-side setup and loop seconds; raw=True returns
     (out, out_off, out_len) instead of a list."""
@@ -275,7 +277,9 @@ def egress_stacks(payload: np.ndarray, lens, max_chunk: int, read_size: int, pos
     args = (src.ctypes.data, in_off.ctypes.data, lens.size, max_chunk, read_size, cch(pos62),
             cch(pos63), int(bool(pad)), cch(padchar), out.ctypes.data, out_off.ctypes.data,
             out_len.ctypes.data, ctypes.byref(err), tp)
-    if devices > 1:
+    if device is not None:
+        rc = _lib_or_default(lib).h_egress_stacks_mt_on(*args, max(threads, 1), int(device))
+    elif devices > 1:
         rc = _lib_or_default(lib).h_egress_stacks_mt_dev(*args, max(threads, 1), devices)
     elif threads > 1:
         rc = _lib_or_default(lib).h_egress_stacks_mt(*args, threads)
