@@ -2692,60 +2692,29 @@ struct RowModel {
     uint32_t F;             // model positions per row
     uint32_t m, k;          // i / L == (i * m) >> (31 + k)
     uint32_t mL;            // ceil(2^32 / L): i / L == umulhi(i, mL) for i < 2^24
+    uint32_t j0;            // alphabet characters in a passing row's last slot (row 0's);
+                            // kNoRowShape: no row passes (every row is decoded exactly)
+    uint32_t rcpS;          // ceil(2^20 / S) when rel / S == umul24(rel, rcpS) >> 20 for every
+                            // slot offset of a block (and, for line-structured rows,
+                            // 16 S <= 4,096: the 20-bit line division), else 0
+    uint64_t len0;          // output bytes of a passing row: floor(6 (16 (S - 1) + j0) / 8)
 };
-static_assert(sizeof(RowModel) == 48, "RowModel layout");
+static_assert(sizeof(RowModel) == 64, "RowModel layout");
+constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the model, in the region pass 1
-// uses for its per-range counts (scratch between calls).
+// uses for its per-range counts (scratch between calls), and after it the
+// rows' failure bitmap: bit b set when row b must be decoded exactly.
 DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + kWsScratch); }
+DEV unsigned long long *row_fail(void *ws)
+{
+    return (unsigned long long *) ((uint8_t *) ws + kWsScratch + sizeof(RowModel));
+}
 
 #ifndef B64X_ROWS_U  // A/B builds only
 #define B64X_ROWS_U 4
 #endif
 constexpr uint32_t kRowsU = B64X_ROWS_U;  // slots per lane of the row kernels
-
-__global__ __launch_bounds__(kThreads) void k_rows_prep(
-    uint64_t *__restrict__ outlen, uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len,
-    uint64_t in_stride, DecAlpha a, void *ws)
-{
-    for (uint64_t i = (uint64_t) blockIdx.x * kThreads + threadIdx.x; i < nbuf;
-         i += (uint64_t) gridDim.x * kThreads)
-        outlen[i] = 0;
-    if (blockIdx.x != 0) return;
-    __shared__ uint8_t tab[256];
-    build_dec_table(tab, a);
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    const LineModel lm = probe_lines(tab, in, len);
-    if (threadIdx.x != 0) return;
-    RowModel r{};
-    const uint32_t L = lm.L, s = lm.s, P = L + s;
-    if (L) {
-        const uint32_t F = len / P * L + (len % P < L ? len % P : L);
-        const uint32_t S = (F + 15) / 16;
-        const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
-        const uint64_t e = (uint64_t) magic * S - (1ull << 32);
-        const uint64_t relmax = S + (uint64_t) kRowsU * kThreads;
-        // (rows of at least 32 bytes: a window never reads more than 24
-        // bytes past a row start beyond the next row's)
-        if (S >= 2 && len >= 32 && relmax * e < (1ull << 32) &&
-            (relmax / S + 1) * in_stride < (1ull << 40)) {
-            r.L = L;
-            r.s = s;
-            r.P = P;
-            r.rcp = ((1u << 20) + L - 1) / L;
-            r.S = S;
-            r.magic = magic;
-            r.m64 = ~0ull / S + 1;
-            r.F = F;
-            r.k = 32 - __builtin_clz(L - 1);
-            r.m = (uint32_t) ((((uint64_t) 1 << (31 + r.k)) + L - 1) / L);
-            // exact for i < 16 S <= 2^24: i (mL L - 2^32) < 2^24 * 252 < 2^32
-            r.mL = (uint32_t) ((0xFFFFFFFFull + L) / L);
-        }
-    }
-    *row_model(ws) = r;
-}
 
 // One slot of a line-structured row: its 16 model characters from the
 // window at its span, checked strictly (interior) or by the prefix rule
@@ -2778,33 +2747,137 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
     return shape && !sep_alpha;
 }
 
+// Rows with room (out_stride >= 12 S), one pass over the row slots, the
+// lengths written afterwards (k_rows_finish):
+//   k_rows_prep   zeroes the failure bitmap and, in one wave, probes the line
+//                 model from row 0 and decodes row 0's last slot: its
+//                 alphabet count j0 is the shape every passing row's last slot
+//                 must have, so a passing row's length is known in advance;
+//   k_decode_rows_lines  checks and decodes every slot, marking a row that
+//                 does not pass (one atomicOr of its bit, by the first failing
+//                 lane of the row in the wave; no per-row atomics otherwise);
+//   k_rows_finish writes every row's length with coalesced stores and decodes
+//                 the marked rows exactly.
+// (Round 2 zeroed outlen[] and took every row's length by an atomicMax from
+// the lane of its last slot: 1 M scattered 8-byte atomics per batch of 1 M
+// rows, 1.09x the output's write traffic, profiles/r02_pmc_rows32_crlf76.json.)
+__global__ __launch_bounds__(kThreads) void k_rows_prep(
+    uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len, uint64_t in_stride, uint32_t S,
+    DecAlpha a, void *ws)
+{
+    unsigned long long *bm = row_fail(ws);
+    const uint32_t nw = (nbuf + 63) / 64;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < nw; i += gridDim.x * kThreads)
+        bm[i] = 0;
+    if (blockIdx.x != 0) return;
+    __shared__ uint8_t tab[256];
+    build_dec_table(tab, a);
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const LineModel lm = probe_lines(tab, in, len);
+    RowModel r{};
+    const uint32_t L = lm.L, s = lm.s, P = L + s;
+    if (L) {
+        const uint32_t F = len / P * L + (len % P < L ? len % P : L);
+        const uint32_t Sm = (F + 15) / 16;
+        const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + Sm) / Sm);
+        const uint64_t e = (uint64_t) magic * Sm - (1ull << 32);
+        const uint64_t relmax = Sm + (uint64_t) kRowsU * kThreads;
+        // (rows of at least 32 bytes: a window never reads more than 24
+        // bytes past a row start beyond the next row's)
+        if (Sm >= 2 && len >= 32 && relmax * e < (1ull << 32) &&
+            (relmax / Sm + 1) * in_stride < (1ull << 40)) {
+            r.L = L;
+            r.s = s;
+            r.P = P;
+            r.rcp = ((1u << 20) + L - 1) / L;
+            r.S = Sm;
+            r.magic = magic;
+            r.m64 = ~0ull / Sm + 1;
+            r.F = F;
+            r.k = 32 - __builtin_clz(L - 1);
+            r.m = (uint32_t) ((((uint64_t) 1 << (31 + r.k)) + L - 1) / L);
+            // exact for i < 16 S <= 2^24: i (mL L - 2^32) < 2^24 * 252 < 2^32
+            r.mL = (uint32_t) ((0xFFFFFFFFull + L) / L);
+        }
+    }
+    // row 0's last slot: the shape of every passing row's
+    uint32_t j0 = kNoRowShape;
+    const uint32_t Sr = r.L ? r.S : S;
+    if (r.L) {
+        const uint32_t i = 16 * (Sr - 1), k = r.F - i;
+        const uint32_t dl = i / L, col = i - dl * L, pos = dl * P + col;
+        const uint8_t *ab = in + (pos & ~3u);
+        const uint8_t *end = in + len;
+        const uint4 w = load_win16(ab, end);
+        const uint2 x = load_win8(ab + 16, end);
+        const uint32_t w6[6] = {w.x, w.y, w.z, w.w, x.x, x.y};
+        uint32_t G[4], j;
+        if (row_lines_slot(tab, r, w6, pos & 3u, col, true, k, len - pos, G, &j)) j0 = j;
+    } else {
+        const uint32_t nlast = len - 16 * (Sr - 1);
+        const uint4 w = load_chars(in + 16 * (Sr - 1), nlast);
+        uint32_t G[4], A[4], k = 16;
+        map_fast_acc(tab, w, G, A);
+        if (row_last_slot(tab, w, A, G, nlast, k)) j0 = k;
+    }
+    r.j0 = j0;
+    r.len0 = j0 == kNoRowShape ? 0 : (16ull * (Sr - 1) + j0) * 6 / 8;
+    // the 24-bit slot mapping: rel < S + U x 256 for every lane slot of a
+    // block; rel / S exact as (rel * rcpS) >> 20 iff rel (rcpS S - 2^20) < 2^20
+    const uint32_t rS = ((1u << 20) + Sr - 1) / Sr;
+    const uint64_t relmax = Sr + (uint64_t) kRowsU * kThreads;
+    if ((!r.L || 16ull * Sr <= 4096) && relmax * ((uint64_t) rS * Sr - (1u << 20)) < (1u << 20))
+        r.rcpS = rS;
+    if (threadIdx.x == 0) *row_model(ws) = r;
+}
+
 // The row kernel.  Clean rows (the model's L = 0): the block's first slot
 // gives its row b0 and slot q0 once, each lane's slot is a 32-bit offset
 // from there split with a 32-bit multiply-high (magic = ceil(2^32/S), exact
 // in range -- the launcher checks); lane slots load 16 characters and store
-// 12 bytes unconditionally (the last slot of a row over-writes past out_len
-// inside its own row; its length follows the prefix rule, row_last_slot).
-// Blocks that touch the last row ("tail", block-uniform) read page-safely
-// and store only decoded bytes, so one launch covers the batch.  Lengths and
-// marks go through atomicMax on the zeroed outlen[] as in k_decode_slots.
-// Line-structured rows: the same shape with the model's S, magic and m64,
-// and each slot's span (row_lines_slot).
+// 12 bytes unconditionally (the last slot of a row over-writes past its
+// length inside its own row).  Line-structured rows: the same shape with the
+// model's S and each slot's span (row_lines_slot); when the model allows
+// (rcpS), the slot mapping and the line division are 24-bit products, as in
+// k_decode_lines (a 32-bit multiply issues at a quarter of the VALU rate).
+// A slot passes when it is all alphabet (interior) or when its alphabet
+// characters are a prefix as long as row 0's last slot's (the last; j0, the
+// prep's) -- then the row's length is the prep's len0.  The first failing
+// lane of a row in the wave sets the row's bit for the exact decode
+// (k_rows_finish); nothing else is written per row.  Blocks that touch the
+// last row ("tail", block-uniform) read page-safely and store only decoded
+// bytes, so one launch covers the batch.
 #ifndef B64X_ROWS_WPE  // A/B builds only: minimum waves per SIMD
 #define B64X_ROWS_WPE 1
 #endif
+
+// Mark the rows of this u-step's failing lanes: the first failing lane of
+// each row among the wave's lanes (rows are contiguous runs of lanes: lane
+// l's slot q = l - (its row's first lane)).  Wave-uniform call.
+DEV void mark_failed_rows(unsigned long long *bm, uint64_t junk, uint32_t q, uint64_t row)
+{
+    const uint32_t ln = lane_id();
+    const uint32_t rs = q < ln ? ln - q : 0u;
+    const uint64_t row_junk = junk & (~0ull << rs);
+    if ((junk >> ln) & 1 && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln)
+        atomicOr(bm + (row >> 6), 1ull << (row & 63));
+}
+
 template <int U, bool O32>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
 void k_decode_rows_lines(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
-    uint8_t *__restrict__ out, uint64_t out_stride,
-    unsigned long long *__restrict__ outlen, uint32_t S, uint32_t magic, uint64_t m64,
+    uint8_t *__restrict__ out, uint64_t out_stride, uint32_t S, uint32_t magic, uint64_t m64,
     uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws)
 {
     __shared__ uint8_t tab[256];
     const uint64_t *rmw = (const uint64_t *) row_model(ws);
-    const uint64_t r0 = scalar_load_u64(rmw);
+    const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
+    unsigned long long *bm = row_fail(ws);
     build_dec_table(tab, a);
     __syncthreads();
+    const uint32_t j0 = (uint32_t) r6, rcpS = (uint32_t) (r6 >> 32);
     if ((uint32_t) r0 != 0) {
         RowModel rm;
         const uint64_t r1 = scalar_load_u64(rmw + 1), r2 = scalar_load_u64(rmw + 2),
@@ -2830,8 +2903,94 @@ void k_decode_rows_lines(
         const uint32_t q0 = (uint32_t) (s0 - b0 * Sm);
         const uint8_t *ib = in + b0 * in_stride;
         uint8_t *ob = out + b0 * out_stride;
-        unsigned long long *olb = outlen + b0;
         const bool tail = s0 + U * kThreads > tail_m;
+        if (O32 && !tail && rcpS && (rm.L & 3) == 0) {
+            // The hot path of MIME-formatted rows (L % 4 == 0: RFC 2045's 76,
+            // PEM's 64, so a line end is a dword boundary of a slot and the
+            // merge a dword select): 24-bit slot mapping, the line division by
+            // the model's 20-bit reciprocal, unguarded window loads,
+            // non-temporal stores.  A row's last slot sits at the same place
+            // in every row, so its rule is wave-uniform constants: CARE_g /
+            // EXP_g, the bit-7 masks of its k model positions and of those
+            // that must be outside the alphabet (the ones from j0 on), and
+            // the separator bytes its span must end with.
+            const uint32_t kq = rm.F - 16 * (Sm - 1);  // model positions of a last slot
+            const uint32_t iL = 16 * (Sm - 1), dL = iL / rm.L, colL = iL - dL * rm.L;
+            const uint32_t cL = rm.L - colL < 16 ? rm.L - colL : 16u;
+            const uint32_t spanL = len - (dL * rm.P + colL);
+            const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
+                                 : (spanL - cL < rm.s ? spanL - cL : rm.s);
+            uint32_t CARE[4], EXP[4];
+#pragma unroll
+            for (uint32_t g = 0; g < 4; g++) {
+                CARE[g] = EXP[g] = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    const uint32_t c = 4 * g + b;
+                    if (c < kq) CARE[g] |= 0x80u << (8 * b);
+                    if (c < kq && c >= j0) EXP[g] |= 0x80u << (8 * b);
+                }
+            }
+            if (j0 == kNoRowShape) EXP[0] |= 1;  // no last slot passes
+            const uint32_t need_s = sep_need(rm.s), need_L = sep_need(nsepL);
+            uint32_t bl[U], qq[U], oo[U], cc[U];
+            uint4 win[U];
+            uint2 wx[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rel = q0 + u * kThreads + threadIdx.x;
+                bl[u] = __umul24(rel, rcpS) >> 20;
+                qq[u] = rel - __umul24(bl[u], Sm);
+                const uint32_t i = 16 * qq[u];
+                const uint32_t dl = __umul24(i, rm.rcp) >> 20;
+                const uint32_t col = i - __umul24(dl, rm.L);
+                const uint32_t pos = __umul24(dl, rm.P) + col;
+                oo[u] = pos & 3u;
+                cc[u] = col;
+                const uint8_t *ab = ib + (__umul24(bl[u], (uint32_t) in_stride) + (pos & ~3u));
+                win[u] = load16_a4(ab);
+                const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+                wx[u] = make_uint2(v.x, v.y);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t q = qq[u];
+                const bool last = q == Sm - 1;
+                const uint32_t col = cc[u];
+                const bool hs = rm.L - col <= 16;
+                const uint32_t c = hs ? rm.L - col : 16u;
+                const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+                uint32_t sep;
+                const uint4 d = slot_chars4(w6, oo[u], c >> 2, rm.s, &sep);
+                const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+                uint32_t G[4], bad = 0;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const uint32_t P = (uint32_t) tab[dw[g] & 0xFFu] |
+                                       ((uint32_t) tab[(dw[g] >> 8) & 0xFFu] << 8) |
+                                       ((uint32_t) tab[(dw[g] >> 16) & 0xFFu] << 16) |
+                                       ((uint32_t) tab[dw[g] >> 24] << 24);
+                    const uint32_t Pz = P & 0x3F3F3F3Fu;
+                    G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
+                           __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
+                    // interior: no byte outside the alphabet; last: exactly
+                    // the EXP ones among the CARE ones
+                    const uint32_t care = last ? CARE[g] : 0x80808080u;
+                    const uint32_t exp = last ? EXP[g] : 0u;
+                    bad |= (P & care) ^ exp;
+                }
+                // the separator bytes of a line that ends in the span
+                const uint32_t need = last ? need_L : hs ? need_s : 0u;
+                bad |= (sep_nonalpha(tab, sep) & need) ^ need;
+                uint32_t o0, o1, o2;
+                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+                uint8_t *dst = ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u));
+                __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+                const uint64_t junk = __ballot(bad != 0);
+                if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
+            }
+            return;
+        }
         const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
         uint32_t bl[U], qq[U], oo[U], cl[U], pp[U];
         uint4 win[U];
@@ -2871,12 +3030,12 @@ void k_decode_rows_lines(
             const uint32_t pos = pp[u];
             const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
             uint32_t G[4], j;
-            const bool ok = row_lines_slot(tab, rm, w6, oo[u], cl[u], last, k, len - pos, G, &j);
+            bool ok = row_lines_slot(tab, rm, w6, oo[u], cl[u], last, k, len - pos, G, &j);
+            ok = ok && (!last || j == j0);
             uint32_t o0, o1, o2;
             groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
             uint8_t *dst = O32 ? ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u))
                                : ob + (uint64_t) bl[u] * out_stride + 12 * q;
-            unsigned long long *ol = olb + bl[u];
             const bool live = !tail || s0 + u * kThreads + threadIdx.x < ns_m;
             if (!tail) {
                 __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
@@ -2884,16 +3043,7 @@ void k_decode_rows_lines(
                 store_bytes12(dst, o0, o1, o2, last ? 3 * (j >> 2) + ((6 * (j & 3)) >> 3) : 12u);
             }
             const uint64_t junk = __ballot(live && !ok);
-            const uint32_t ln = lane_id();
-            const uint32_t rs = q < ln ? ln - q : 0u;
-            const uint64_t row_junk = junk & (~0ull << rs);
-            const bool marker = live && !ok && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln;
-            if (!live) {
-            } else if (!ok) {
-                if (marker) atomicMax(ol, (unsigned long long) kNeedsExact);
-            } else if (last) {
-                atomicMax(ol, (unsigned long long) ((16ull * q + j) * 6 / 8));
-            }
+            if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
         }
         return;
     }
@@ -2903,38 +3053,43 @@ void k_decode_rows_lines(
     const uint32_t q0 = (uint32_t) (s0 - b0 * S);
     const uint8_t *ib = in + b0 * in_stride;
     uint8_t *ob = out + b0 * out_stride;
-    unsigned long long *olb = outlen + b0;
     const uint32_t nlast = len - 16 * (S - 1);  // characters in a row's last slot
     uint32_t bl[U], qq[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t rel = q0 + u * kThreads + threadIdx.x;
-        bl[u] = __umulhi(rel, magic);
-        qq[u] = rel - bl[u] * S;
+        if (rcpS) {
+            bl[u] = __umul24(rel, rcpS) >> 20;
+            qq[u] = rel - __umul24(bl[u], S);
+        } else {
+            bl[u] = __umulhi(rel, magic);
+            qq[u] = rel - bl[u] * S;
+        }
     }
     if (s0 + U * kThreads > tail_slot) {
         // tail block: page-safe loads, decoded bytes only
         for (int u = 0; u < U; u++) {
             const uint64_t t = s0 + u * kThreads + threadIdx.x;
             const uint32_t q = qq[u];
-            if (t >= nslots) continue;
+            const bool live = t < nslots;
             const bool last = q == S - 1;
-            const uint4 wv = load_chars(ib + (uint64_t) bl[u] * in_stride + 16 * q,
-                                        last ? nlast : 16u);
+            bool ok = true;
             uint32_t G[4], A[4], k = 16;
-            map_fast_acc(tab, wv, G, A);
-            bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
-            if (last) ok = row_last_slot(tab, wv, A, G, nlast, k);
-            unsigned long long *ol = olb + bl[u];
-            if (!ok) {
-                atomicMax(ol, (unsigned long long) kNeedsExact);
-                continue;
+            if (live) {
+                const uint4 wv = load_chars(ib + (uint64_t) bl[u] * in_stride + 16 * q,
+                                            last ? nlast : 16u);
+                map_fast_acc(tab, wv, G, A);
+                ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
+                if (last) ok = row_last_slot(tab, wv, A, G, nlast, k) && k == j0;
+                if (ok) {
+                    uint32_t o0, o1, o2;
+                    groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+                    store_bytes12(ob + (uint64_t) bl[u] * out_stride + 12 * q, o0, o1, o2,
+                                  3 * (k >> 2) + ((6 * (k & 3)) >> 3));
+                }
             }
-            uint32_t o0, o1, o2;
-            groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-            store_bytes12(ob + (uint64_t) bl[u] * out_stride + 12 * q, o0, o1, o2,
-                          3 * (k >> 2) + ((6 * (k & 3)) >> 3));
-            if (last) atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
+            const uint64_t junk = __ballot(live && !ok);
+            if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
         }
         return;
     }
@@ -2951,24 +3106,14 @@ void k_decode_rows_lines(
         map_fast_acc(tab, w[u], G, A);
         uint32_t k = 16;
         bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
-        if (last) ok = row_last_slot(tab, w[u], A, G, nlast, k);
+        if (last) ok = row_last_slot(tab, w[u], A, G, nlast, k) && k == j0;
         uint32_t o0, o1, o2;
         groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
         uint8_t *dst = O32 ? ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u))
                            : ob + (uint64_t) bl[u] * out_stride + 12 * q;
         __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
-        unsigned long long *ol = olb + bl[u];
-        // only the first junk slot of each row in the wave marks it
         const uint64_t junk = __ballot(!ok);
-        const uint32_t ln = lane_id();
-        const uint32_t rs = q < ln ? ln - q : 0u;
-        const uint64_t row_junk = junk & (~0ull << rs);
-        const bool marker = !ok && (uint32_t) __ffsll((unsigned long long) row_junk) - 1 == ln;
-        if (!ok) {
-            if (marker) atomicMax(ol, (unsigned long long) kNeedsExact);
-        } else if (last) {
-            atomicMax(ol, (unsigned long long) ((16ull * q + k) * 6 / 8));
-        }
+        if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
     }
 }
 
@@ -3065,6 +3210,42 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
             buf_first_chunks(in + beg, len, c);
             const uint64_t V = decode_buf_bits(sm, sm.bits[wv], in + beg, len, out + obeg, c);
             if (lane == 0) outlen[b] = RV ? V : V * 6 / 8;
+        }
+    }
+}
+
+// Row lengths after k_decode_rows_lines: one wave per 64 rows (one bitmap
+// word, read through the scalar cache), every unmarked row's length (the
+// prep's len0) by one coalesced store per lane, then the marked rows decoded
+// exactly one after another with pass 2d's bit-stream machinery (as
+// k_decode_batch_fix2 does).
+__global__ __launch_bounds__(kThreads) void k_rows_finish(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
+    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a, void *ws)
+{
+    __shared__ P2dSmem sm;
+    const uint64_t len0 = scalar_load_u64((const uint64_t *) row_model(ws) + 7);
+    const unsigned long long *bm = row_fail(ws);
+    build_dec_table(sm.tab, a);
+    build_compact_sel(sm.sel);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
+    for (uint64_t g = (uint64_t) blockIdx.x * kWavesPerBlock + wv; g * 64 < nbuf; g += nw) {
+        const uint64_t base = g * 64;
+        uint64_t m = scalar_load_u64((const uint64_t *) bm + g);
+        const uint64_t b = base + lane;
+        if (b < nbuf && !((m >> lane) & 1)) outlen[b] = len0;
+        while (m) {
+            const uint32_t r = (uint32_t) (base + __ffsll((unsigned long long) m) - 1);
+            m &= m - 1;
+            uint64_t beg, len, obeg;
+            batch_buf(L, r, beg, len, obeg);
+            uint4 c[2];
+            buf_first_chunks(in + beg, len, c);
+            const uint64_t V = decode_buf_bits(sm, sm.bits[wv], in + beg, len, out + obeg, c);
+            if (lane == 0) outlen[r] = V * 6 / 8;
         }
     }
 }
@@ -3630,23 +3811,27 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     bool done = false;
     int err = 0;
     if (rows && S < (1u << 20)) {
-        // rows with room, one launch after the prep (k_rows_prep zeroes
-        // outlen[] and probes the line model from row 0; k_decode_rows_lines
-        // takes clean rows by k_decode_rows2's path and MIME-formatted rows by
-        // the model)
+        // rows with room: k_rows_prep (the failure bitmap, the line model
+        // and the shape of row 0's last slot), k_decode_rows_lines (clean
+        // rows by k_decode_rows2's path, MIME-formatted rows by the model),
+        // k_rows_finish (every row's length; the marked rows exactly)
         constexpr uint32_t U = kRowsU;
         const uint32_t magic = (uint32_t) ((0xFFFFFFFFull + S) / S);
         const uint64_t e = (uint64_t) magic * S - (1ull << 32);
         const uint64_t relmax = S + (uint64_t) U * kThreads;
         void *ws = nullptr;
+        const uint64_t bitmap = ((uint64_t) nbuf + 63) / 64 * 8 + sizeof(RowModel);
         if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40) &&
+            bitmap <= b64x_decode_workspace_size(0) - kWsScratch &&
             (ws = library_workspace(stream, &err))) {
             const uint64_t m64 = ~0ull / S + 1;
             const uint64_t per = (uint64_t) U * kThreads;
             const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
-            hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nbuf + kThreads - 1) / kThreads, (uint64_t) d->cus * 4)),
-                               dim3(kThreads), 0, s, d_outlen, nbuf, (const uint8_t *) d_in,
-                               (uint32_t) len, in_stride, a, ws);
+            const uint64_t nwords = ((uint64_t) nbuf + 63) / 64;
+            hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nwords + kThreads - 1) / kThreads,
+                                                          (uint64_t) d->cus)),
+                               dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in, (uint32_t) len,
+                               in_stride, (uint32_t) S, a, ws);
             if ((err = launch_status())) return err;
             const dim3 g((uint32_t) ((slots + per - 1) / per));
             // 32-bit offsets within a block's rows (relmax / S + 1 rows at most)
@@ -3656,10 +3841,13 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             hipLaunchKernelGGL((o32 ? k_decode_rows_lines<U, true> : k_decode_rows_lines<U, false>),
                                g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, (uint32_t) len, (uint8_t *) d_out,
-                               out_stride, (unsigned long long *) d_outlen, (uint32_t) S, magic, m64,
-                               slots, tail_slot, a, nbuf, ws);
+                               out_stride, (uint32_t) S, magic, m64, slots, tail_slot, a, nbuf, ws);
             if ((err = launch_status())) return err;
-            done = true;
+            const uint32_t fg = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) /
+                                         (64 * kWavesPerBlock), (uint64_t) d->cus * 8);
+            hipLaunchKernelGGL(k_rows_finish, dim3(fg), dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a, ws);
+            return launch_status();
         } else if (err) {
             return err;
         }
