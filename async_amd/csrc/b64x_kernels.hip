@@ -1727,6 +1727,28 @@ DEV uint32_t sep_need(uint32_t n)
     return n >= 4 ? 0x01010101u : 0x01010101u & ((1u << (8 * n)) - 1u);
 }
 
+// The table values of x's four bytes, packed (byte k: the value of byte k),
+// with two v_perm pairs and one merge instead of three shifts and ors.
+DEV uint32_t tab_pack4(const uint8_t *tab, uint32_t x)
+{
+    const uint32_t t0 = tab[x & 0xFFu], t1 = tab[(x >> 8) & 0xFFu];
+    const uint32_t t2 = tab[(x >> 16) & 0xFFu], t3 = tab[x >> 24];
+    const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0400u);  // t0 t1 0 0
+    const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x0c0c0400u);  // t2 t3 0 0
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);                // t0 t1 t2 t3
+}
+
+// Separator bytes of a uniform count s (1..4) outside the alphabet: only
+// the s lookups that matter (s is wave-uniform, so the tests are scalar).
+DEV bool sep_ok_s(const uint8_t *tab, uint32_t sep, uint32_t s)
+{
+    uint32_t acc = tab[sep & 0xFFu];
+    if (s > 1) acc &= tab[(sep >> 8) & 0xFFu];
+    if (s > 2) acc &= tab[(sep >> 16) & 0xFFu];
+    if (s > 3) acc &= tab[sep >> 24];
+    return (acc & 0x80u) != 0;
+}
+
 // One wave: the model, the stream's interior slot count T and the division
 // constants into the workspace, for k_decode_lines (every block reads them
 // with one scalar load instead of probing -- 175 K probes of the same 256
@@ -2698,8 +2720,13 @@ struct RowModel {
                             // slot offset of a block (and, for line-structured rows,
                             // 16 S <= 4,096: the 20-bit line division), else 0
     uint64_t len0;          // output bytes of a passing row: floor(6 (16 (S - 1) + j0) / 8)
+    uint32_t Sx;            // slots per row of the line-structured hot path: S, or
+                            // out_stride / 12 when that is whole (slots from S on store
+                            // only filler, so consecutive rows' writes are contiguous)
+    uint32_t pad;
+    uint64_t m64x;          // ceil(2^64 / Sx)
 };
-static_assert(sizeof(RowModel) == 64, "RowModel layout");
+static_assert(sizeof(RowModel) == 80, "RowModel layout");
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the model, in the region pass 1
@@ -2763,7 +2790,7 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
 // rows, 1.09x the output's write traffic, profiles/r02_pmc_rows32_crlf76.json.)
 __global__ __launch_bounds__(kThreads) void k_rows_prep(
     uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len, uint64_t in_stride, uint32_t S,
-    DecAlpha a, void *ws)
+    uint64_t out_stride, DecAlpha a, void *ws)
 {
     unsigned long long *bm = row_fail(ws);
     const uint32_t nw = (nbuf + 63) / 64;
@@ -2823,11 +2850,23 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
     }
     r.j0 = j0;
     r.len0 = j0 == kNoRowShape ? 0 : (16ull * (Sr - 1) + j0) * 6 / 8;
-    // the 24-bit slot mapping: rel < S + U x 256 for every lane slot of a
-    // block; rel / S exact as (rel * rcpS) >> 20 iff rel (rcpS S - 2^20) < 2^20
-    const uint32_t rS = ((1u << 20) + Sr - 1) / Sr;
-    const uint64_t relmax = Sr + (uint64_t) kRowsU * kThreads;
-    if ((!r.L || 16ull * Sr <= 4096) && relmax * ((uint64_t) rS * Sr - (1u << 20)) < (1u << 20))
+    // Line-structured rows use fewer slots per row (the model's S) than the
+    // characters would (the launcher's S); when the output stride is whole
+    // slots, the hot path takes that many per row (at most the launcher's)
+    // and fills the slack, so no row leaves a hole between its bytes and the
+    // next row's (a hole makes every row's last line a partial write).
+#ifndef B64X_ROWS_SLACK  // A/B builds only: fill each row's slack (0: leave holes)
+#define B64X_ROWS_SLACK 1
+#endif
+    r.Sx = B64X_ROWS_SLACK && r.L && out_stride % 12 == 0
+               ? (out_stride / 12 < S ? (uint32_t) (out_stride / 12) : S) : Sr;
+    const uint32_t Sq = r.L ? r.Sx : Sr;
+    r.m64x = ~0ull / r.Sx + 1;
+    // the 24-bit slot mapping: rel < Sq + U x 256 for every lane slot of a
+    // block; rel / Sq exact as (rel * rcpS) >> 20 iff rel (rcpS Sq - 2^20) < 2^20
+    const uint32_t rS = ((1u << 20) + Sq - 1) / Sq;
+    const uint64_t relmax = Sq + (uint64_t) kRowsU * kThreads;
+    if ((!r.L || 16ull * Sr <= 4096) && relmax * ((uint64_t) rS * Sq - (1u << 20)) < (1u << 20))
         r.rcpS = rS;
     if (threadIdx.x == 0) *row_model(ws) = r;
 }
@@ -2895,44 +2934,45 @@ void k_decode_rows_lines(
         rm.k = (uint32_t) r5;
         rm.mL = (uint32_t) (r5 >> 32);
         const uint32_t Sm = rm.S;
-        const uint64_t ns_m = (uint64_t) Sm * nbuf;
-        const uint64_t tail_m = (uint64_t) Sm * (nbuf - 1);
         const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
-        if (s0 >= ns_m) return;
-        const uint64_t b0 = __umul64hi(s0, rm.m64);
-        const uint32_t q0 = (uint32_t) (s0 - b0 * Sm);
-        const uint8_t *ib = in + b0 * in_stride;
-        uint8_t *ob = out + b0 * out_stride;
-        const bool tail = s0 + U * kThreads > tail_m;
-        if (O32 && !tail && rcpS && (rm.L & 3) == 0) {
+        const uint32_t Sx = (uint32_t) scalar_load_u64(rmw + 8);
+        if (O32 && rcpS && (rm.L & 3) == 0) {
+            if (s0 >= (uint64_t) Sx * nbuf) return;
+            // blocks that touch the last row: page-safe loads, no slack
+            // filler (the last row's capacity may end before out_stride),
+            // decoded bytes only
+            const bool tail = s0 + U * kThreads > (uint64_t) Sx * (nbuf - 1);
+            const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
+            const uint32_t nb_last = j0 == kNoRowShape ? 0u : 3 * (j0 >> 2) + ((6 * (j0 & 3)) >> 3);
+            const uint64_t b0 = __umul64hi(s0, scalar_load_u64(rmw + 9));
+            const uint32_t q0 = (uint32_t) (s0 - b0 * Sx);
+            const uint8_t *ib = in + b0 * in_stride;
+            uint8_t *ob = out + b0 * out_stride;
             // The hot path of MIME-formatted rows (L % 4 == 0: RFC 2045's 76,
             // PEM's 64, so a line end is a dword boundary of a slot and the
             // merge a dword select): 24-bit slot mapping, the line division by
             // the model's 20-bit reciprocal, unguarded window loads,
             // non-temporal stores.  A row's last slot sits at the same place
-            // in every row, so its rule is wave-uniform constants: CARE_g /
-            // EXP_g, the bit-7 masks of its k model positions and of those
-            // that must be outside the alphabet (the ones from j0 on), and
-            // the separator bytes its span must end with.
+            // in every row, so its rule is wave-uniform constants: the masks
+            // of its k model positions and of those that must be outside the
+            // alphabet (the ones from j0 on), and
+            // the separator bytes its span must end with.  Slots from Sm to
+            // Sx - 1 of a row only store filler into the row's slack (see
+            // RowModel::Sx); their loads read the row's last slot instead.
+            // (VALU, not HBM, bounds this kernel: the table values are packed
+            // with v_perm, the groups and the non-alphabet mask come from
+            // v_dot4, and only the s separator bytes a line has are looked up.)
             const uint32_t kq = rm.F - 16 * (Sm - 1);  // model positions of a last slot
             const uint32_t iL = 16 * (Sm - 1), dL = iL / rm.L, colL = iL - dL * rm.L;
             const uint32_t cL = rm.L - colL < 16 ? rm.L - colL : 16u;
             const uint32_t spanL = len - (dL * rm.P + colL);
             const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
                                  : (spanL - cL < rm.s ? spanL - cL : rm.s);
-            uint32_t CARE[4], EXP[4];
-#pragma unroll
-            for (uint32_t g = 0; g < 4; g++) {
-                CARE[g] = EXP[g] = 0;
-#pragma unroll
-                for (uint32_t b = 0; b < 4; b++) {
-                    const uint32_t c = 4 * g + b;
-                    if (c < kq) CARE[g] |= 0x80u << (8 * b);
-                    if (c < kq && c >= j0) EXP[g] |= 0x80u << (8 * b);
-                }
-            }
-            if (j0 == kNoRowShape) EXP[0] |= 1;  // no last slot passes
-            const uint32_t need_s = sep_need(rm.s), need_L = sep_need(nsepL);
+            const uint32_t need_L = sep_need(nsepL), need_s = sep_need(rm.s);
+            // 128 x (the last slot's masks of non-alphabet characters): the
+            // ones it may have (its k positions) and the ones it must have
+            const uint32_t kmask = 128u * (kq >= 16 ? 0xFFFFu : (1u << kq) - 1u);
+            const uint32_t expm = j0 == kNoRowShape ? 1u : kmask & ~(128u * ((1u << j0) - 1u));
             uint32_t bl[U], qq[U], oo[U], cc[U];
             uint4 win[U];
             uint2 wx[U];
@@ -2940,22 +2980,29 @@ void k_decode_rows_lines(
             for (int u = 0; u < U; u++) {
                 const uint32_t rel = q0 + u * kThreads + threadIdx.x;
                 bl[u] = __umul24(rel, rcpS) >> 20;
-                qq[u] = rel - __umul24(bl[u], Sm);
-                const uint32_t i = 16 * qq[u];
+                qq[u] = rel - __umul24(bl[u], Sx);
+                const uint32_t i = 16 * (qq[u] < Sm ? qq[u] : Sm - 1);
                 const uint32_t dl = __umul24(i, rm.rcp) >> 20;
                 const uint32_t col = i - __umul24(dl, rm.L);
                 const uint32_t pos = __umul24(dl, rm.P) + col;
                 oo[u] = pos & 3u;
                 cc[u] = col;
                 const uint8_t *ab = ib + (__umul24(bl[u], (uint32_t) in_stride) + (pos & ~3u));
-                win[u] = load16_a4(ab);
-                const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
-                wx[u] = make_uint2(v.x, v.y);
+                if (!tail) {
+                    win[u] = load16_a4(ab);
+                    const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+                    wx[u] = make_uint2(v.x, v.y);
+                } else {
+                    const bool live = s0 + u * kThreads + threadIdx.x < (uint64_t) Sx * nbuf;
+                    win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
+                    wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t q = qq[u];
                 const bool last = q == Sm - 1;
+                const bool live = !tail || s0 + u * kThreads + threadIdx.x < (uint64_t) Sx * nbuf;
                 const uint32_t col = cc[u];
                 const bool hs = rm.L - col <= 16;
                 const uint32_t c = hs ? rm.L - col : 16u;
@@ -2963,34 +3010,55 @@ void k_decode_rows_lines(
                 uint32_t sep;
                 const uint4 d = slot_chars4(w6, oo[u], c >> 2, rm.s, &sep);
                 const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
-                uint32_t G[4], bad = 0;
+                uint32_t G[4], m128 = 0;
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const uint32_t P = (uint32_t) tab[dw[g] & 0xFFu] |
-                                       ((uint32_t) tab[(dw[g] >> 8) & 0xFFu] << 8) |
-                                       ((uint32_t) tab[(dw[g] >> 16) & 0xFFu] << 16) |
-                                       ((uint32_t) tab[dw[g] >> 24] << 24);
+                    const uint32_t P = tab_pack4(tab, dw[g]);
                     const uint32_t Pz = P & 0x3F3F3F3Fu;
                     G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
                            __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
-                    // interior: no byte outside the alphabet; last: exactly
-                    // the EXP ones among the CARE ones
-                    const uint32_t care = last ? CARE[g] : 0x80808080u;
-                    const uint32_t exp = last ? EXP[g] : 0u;
-                    bad |= (P & care) ^ exp;
+                    // 128 x the non-alphabet mask of the 16 characters, four
+                    // bits per dword (weights fit a byte within each half)
+                    const uint32_t w = (g & 1) ? 0x80402010u : 0x08040201u;
+                    const uint32_t part = __builtin_amdgcn_udot4(P & 0x80808080u, w, 0u, false);
+                    m128 += (g & 2) ? part << 8 : part;
                 }
+                // interior: all 16 in the alphabet; last: exactly the
+                // expected ones among its k positions outside it
+                uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
                 // the separator bytes of a line that ends in the span
-                const uint32_t need = last ? need_L : hs ? need_s : 0u;
-                bad |= (sep_nonalpha(tab, sep) & need) ^ need;
+#ifndef B64X_ROWS_SEPBR  // A/B builds only: 0 = branch-free separator check
+#define B64X_ROWS_SEPBR 1
+#endif
+                if (B64X_ROWS_SEPBR) {
+                    if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
+                             : (hs && !sep_ok_s(tab, sep, rm.s)))
+                        bad |= 1u;
+                } else {
+                    const uint32_t need = last ? need_L : hs ? need_s : 0u;
+                    bad |= (sep_nonalpha(tab, sep) & need) ^ need;
+                }
+                if (q >= Sm || !live) bad = 0;  // slack filler: the bytes are scratch
                 uint32_t o0, o1, o2;
                 groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
                 uint8_t *dst = ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u));
-                __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+                if (!tail)
+                    __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+                else if (live && q < Sm && bad == 0)
+                    store_bytes12(dst, o0, o1, o2, last ? nb_last : 12u);
                 const uint64_t junk = __ballot(bad != 0);
                 if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
             }
             return;
         }
+        const uint64_t ns_m = (uint64_t) Sm * nbuf;
+        const uint64_t tail_m = (uint64_t) Sm * (nbuf - 1);
+        if (s0 >= ns_m) return;
+        const uint64_t b0 = __umul64hi(s0, rm.m64);
+        const uint32_t q0 = (uint32_t) (s0 - b0 * Sm);
+        const uint8_t *ib = in + b0 * in_stride;
+        uint8_t *ob = out + b0 * out_stride;
+        const bool tail = s0 + U * kThreads > tail_m;
         const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
         uint32_t bl[U], qq[U], oo[U], cl[U], pp[U];
         uint4 win[U];
@@ -3831,7 +3899,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nwords + kThreads - 1) / kThreads,
                                                           (uint64_t) d->cus)),
                                dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in, (uint32_t) len,
-                               in_stride, (uint32_t) S, a, ws);
+                               in_stride, (uint32_t) S, out_stride, a, ws);
             if ((err = launch_status())) return err;
             const dim3 g((uint32_t) ((slots + per - 1) / per));
             // 32-bit offsets within a block's rows (relmax / S + 1 rows at most)

@@ -750,16 +750,23 @@ def test_strided_mime_rows_vs_oracle(n, L, sep):
     stride = max(len(r) for r in rows)
     flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
     x = dev(flat)
-    cap = (b64.decoded_cap(stride) + 15) // 16 * 16
-    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
-    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
-    b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen)
-    ol = outlen.cpu().tolist()
-    dh = dec.cpu().numpy()
-    for i, r in enumerate(rows):
-        want = orc.decode(r + b"\n" * (stride - len(r)))
-        assert ol[i] == len(want), i
-        assert dh[i * cap:i * cap + ol[i]].tobytes() == want, i
+    dcap = b64.decoded_cap(stride)
+    # output strides: rounded to 16; whole 12-byte slots (the MIME hot path
+    # then fills each row's slack); whole slots with room to spare
+    for cap in ((dcap + 15) // 16 * 16, (dcap + 11) // 12 * 12, (dcap + 11) // 12 * 12 + 48):
+        # the last row gets exactly its capacity, then a guard band that no
+        # store may touch (no slack filler past the last row)
+        size = (nbuf - 1) * cap + dcap
+        dec = torch.full((size + 64,), 0xA5, dtype=torch.uint8, device=DEV)
+        outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+        b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen)
+        ol = outlen.cpu().tolist()
+        dh = dec.cpu().numpy()
+        assert (dh[size:] == 0xA5).all(), cap
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)))
+            assert ol[i] == len(want), (cap, i)
+            assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (cap, i)
 
 
 def test_library_workspace_is_bounded():
