@@ -19,10 +19,11 @@
 //     regrouping is v_perm_b32, not shifts (k_encode_flat; batches:
 //     k_encode_tight2, k_encode_strided, k_encode_ragged).
 //   * decode is stateful only through the number of alphabet characters
-//     seen so far.  For inputs up to 2^31 characters: k_decode_probe (one
-//     wave) reads the stream's first 256 bytes for a line model -- lines of
-//     L alphabet characters and s separator bytes, L = 0 for clean input --
-//     under which every character's output place is known in closed form;
+//     seen so far.  For inputs up to 2^31 characters: k_decode_probe reads
+//     the stream's first 256 bytes for a line model -- lines of L alphabet
+//     characters and s separator bytes, L = 0 for clean input -- under which
+//     every character's output place is known in closed form, and checks
+//     256 samples further in against it (junk there cuts the model's slots);
 //     k_decode_lines is output-indexed (lane slot t = sextets [16t, 16t+16)
 //     = output bytes [12t, 12t+12)), loads each slot's span, drops the
 //     separator with funnel shifts, checks it and stores 12 bytes, and
@@ -118,6 +119,7 @@ DEV void build_dec_table(uint8_t *tab, const DecAlpha &a)
 // ------------------------------------------------------- memory helpers --
 
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x4a16 __attribute__((ext_vector_type(4), aligned(16)));
 
 // Store the first `nbytes` (0..12) bytes of {o0, o1, o2}: whole dwords when
 // `p` is dword aligned, then at most 3 single bytes.
@@ -896,6 +898,7 @@ static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of m
 struct DecodeWs {
     uint64_t *lfail;     // kFailWords words, kFailStride apart
     uint64_t *fail_any;  // nonzero: some failure word was published (own line)
+    uint32_t *wdone;     // k_decode_suffix_w: waves that have left (own line; zero between calls)
     LineModel *model;    // k_decode_lines' model, for k_decode_suffix
     uint64_t *fd;
     uint64_t *fd_cur;
@@ -906,6 +909,7 @@ struct DecodeWs {
     uint64_t *bases;
     uint64_t *status;
     uint64_t *fstatus;   // the single-pass decode's tile status words (zero between calls)
+    uint64_t *fsuper;    // k_decode_suffix_w's group sums: tiles counted << 56 | sum (zero between calls)
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
@@ -923,8 +927,12 @@ constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsStatus = 64;                                        // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
-constexpr uint64_t kWsFail = kWsFStatus + kMaxRanges / kFuseTile * 8;     // lines failures
-constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 1) * kFailStride * 8;  // counts, bases
+constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix_w: tiles per group sum
+constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
+constexpr uint64_t kWsFSuper = kWsFStatus + kMaxRanges / kFusePer * 8;    // suffix group sums
+constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kFusePer / kSfxGroup + 16) * 8;  // lines failures
+// failure words, fail_any, wdone: one 128-byte line each
+constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
 // Layout: 64-byte header (fd, fd_cur, ticket, fticket, sfx_start, model), the
 // zero-between-calls regions at fixed offsets, then the scratch counts and
@@ -941,8 +949,10 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.model = (LineModel *) (p + 32);
     w.status = (uint64_t *) (p + kWsStatus);
     w.fstatus = (uint64_t *) (p + kWsFStatus);
+    w.fsuper = (uint64_t *) (p + kWsFSuper);
     w.lfail = (uint64_t *) (p + kWsFail);
     w.fail_any = w.lfail + kFailWords * kFailStride;
+    w.wdone = (uint32_t *) (w.fail_any + kFailStride);
     w.counts = (uint32_t *) (p + kWsScratch);
     w.bases = (uint64_t *) (p + kWsScratch + ((uint64_t) nranges * 4 + 7) / 8 * 8);
     return w;
@@ -1375,6 +1385,12 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
 }
 
 // ---- pass 2, bit-stream form ----------------------------------------------
+#ifndef B64X_AB_NOOR  // A/B builds only (timing breakdowns, wrong output)
+#define B64X_AB_NOOR 0
+#endif
+#ifndef B64X_AB_NOSTORE
+#define B64X_AB_NOSTORE 0
+#endif
 //
 // The range's output is built in LDS directly as the decoded BIT stream (a
 // per-character scatter of sextets into LDS, read back and converted group
@@ -1386,7 +1402,8 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
 // laid out so that LDS byte 4 + (ob & 3) is output byte ob: its dwords map
 // onto aligned output dwords, and the store is a straight copy with byte
 // stores only for the first and last partial dwords.
-constexpr uint32_t kP2dBytes = 4 + 3 + kP2Range / 4 * 3 + 16;          // head, skew, out, slack
+// head, skew (decode_range aligns its window to 16 output bytes), out, slack
+constexpr uint32_t kP2dBytes = 16 + 15 + kP2Range / 4 * 3 + 16;
 constexpr uint32_t kP2dBlocks = (kP2dBytes + 15) / 16;                  // uint4 per wave
 
 struct __attribute__((aligned(16))) P2dSmem {
@@ -1470,6 +1487,32 @@ DEV void store_bits(const uint32_t *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
         if (from + i < to) dst0[from + i] = bb[from + i];
 }
 
+// Copy LDS bytes [lo, hi) of a wave's window `b` to dst0 + [lo, hi), where
+// dst0 = the output address of LDS byte 0, 16-byte aligned: the whole
+// 16-byte blocks as aligned ds_read_b128 / dwordx4 non-temporal pairs (lane
+// k takes block klo + k, conflict-free), the head and tail bytes of the
+// partial blocks (at most 15 each) as one byte store of up to 30 lanes.
+DEV void store_bits16(const uint4 *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t klo = (lo + 15) >> 4, khi = hi >> 4;  // whole blocks [klo, khi)
+    for (uint32_t k = klo + lane; k < khi; k += 64) {
+        const uint4 v = b[k];
+        __builtin_nontemporal_store(u32x4a16{v.x, v.y, v.z, v.w}, (u32x4a16 *) (dst0 + 16 * (uint64_t) k));
+    }
+    const uint32_t hend = 16 * klo < hi ? 16 * klo : hi;  // head bytes [lo, hend)
+    uint32_t i = 0;
+    bool act = false;
+    if (lane < 16) {
+        i = lo + lane;
+        act = i < hend;
+    } else if (lane < 32) {
+        i = 16 * khi + (lane - 16);  // tail bytes [max(16 khi, hend), hi)
+        act = i < hi && i >= hend;
+    }
+    if (act) dst0[i] = ((const uint8_t *) b)[i];
+}
+
 // Inclusive prefix sum over the wave with DPP (row shifts, then the two
 // row broadcasts of gfx9): six full-rate adds instead of a ballot per bit
 // plane; x may pack independent 16-bit counts.
@@ -1520,7 +1563,11 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
+#if B64X_AB_NOOR  // timing only (wrong output): the fields computed, one plain store
+            if (g == 3 && p == 0xFFFFFFFFu) bits[0] = group_dot(D);
+#else
             or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
+#endif
             p += 24u - 6u * bad[h][g];
         }
     }
@@ -1749,47 +1796,121 @@ DEV bool sep_ok_s(const uint8_t *tab, uint32_t sep, uint32_t s)
     return (acc & 0x80u) != 0;
 }
 
-// One wave: the model, the stream's interior slot count T and the division
-// constants into the workspace, for k_decode_lines (every block reads them
-// with one scalar load instead of probing -- 175 K probes of the same 256
-// bytes cost 7 % of a 1 GiB decode -- and of computing T and L's
-// reciprocals: hundreds of scalar instructions per wave) and k_decode_suffix.
-// n <= 2^31 (the launcher's bound), so sextet indices and positions fit in
-// 32 bits.
-__global__ void __launch_bounds__(64) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
-                                                     DecAlpha a, void *ws, uint32_t nranges)
+// The model, the stream's interior slot count T and the division constants
+// into the workspace, for k_decode_lines (every block reads them with one
+// scalar load instead of probing -- 175 K probes of the same 256 bytes cost
+// 7 % of a 1 GiB decode -- and of computing T and L's reciprocals: hundreds
+// of scalar instructions per wave) and k_decode_suffix.  n <= 2^31 (the
+// launcher's bound), so sextet indices and positions fit in 32 bits.
+//
+// Wave 0 probes the model from the first 256 bytes.  Every thread also
+// checks 64 bytes sampled further in (half of them over the stream's first
+// sixteenth, half over all of it, spaced quadratically), against the model: where a sample breaks it, every slot
+// from there on is left to k_decode_suffix (T is cut there), so that junk
+// the first window did not show -- sparse junk, one character in a thousand
+// -- is not decoded twice, once by k_decode_lines until its slots fail and
+// again by k_decode_suffix from the first failure.  Where T falls never
+// matters for the result (k_decode_lines takes slots [0, T) exactly or
+// publishes their failure; k_decode_suffix takes the rest), only for speed.
+constexpr uint32_t kProbeThreads = 256;
+constexpr uint64_t kProbeSampleMin = 1u << 18;  // shorter streams: the first window only
+constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
+
+__global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
+                                                                DecAlpha a, void *ws, uint32_t nranges)
 {
     __shared__ uint8_t tab[256];
-    build_dec_table(tab, a);
-    __syncthreads();
-    uint32_t pj = 0xFFFFFFFFu;
-    LineModel m = probe_lines(tab, in, n, &pj);
-    if (threadIdx.x != 0) return;
-    const uint32_t n32 = (uint32_t) n;
-    if (m.L == 0 && pj != 0xFFFFFFFFu) {
-        // junk in the window that no line model explains (unstructured
-        // junk, a short first line): under the clean model the slot holding
-        // it fails, so k_decode_lines takes only the slots before it, and
-        // k_decode_suffix everything from there
-        m.T = pj / 16;
-        m.skip = 1;
-        *ws_view(ws, nranges).lfail = ~(uint64_t) m.T;
-        *ws_view(ws, nranges).fail_any = 1;
-    } else if (m.L == 0) {
-        m.T = n32 / 16;
-    } else {
-        m.P = m.L + m.s;
-        // T: the slots whose spans lie wholly inside the input -- those whose
-        // 16 characters are model positions below n, less the last one if a
-        // line ends right after it and its separator is cut off
-        const uint32_t F = n32 / m.P * m.L + (n32 % m.P < m.L ? n32 % m.P : m.L);
-        m.T = F / 16;
-        if (m.T && (16 * m.T) % m.L == 0 && (16 * m.T) / m.L * m.P > n32) m.T--;
-        m.k = 32 - __builtin_clz(m.L - 1);  // ceil(log2 L)
-        m.m = (uint32_t) ((((uint64_t) 1 << (31 + m.k)) + m.L - 1) / m.L);
-        m.rcp = ((1u << 20) + m.L - 1) / m.L;
+    __shared__ LineModel s_m;
+    __shared__ uint32_t s_first;
+    // the samples' loads are issued first: they overlap the table build and
+    // the window probe
+    const bool sample = n >= kProbeSampleMin;
+    uint32_t sw[16];
+    uint32_t q = 0;
+    if (sample) {
+        // half the samples over the first 1/16 of the stream, half over all
+        // of it, each half at quadratically growing distances
+        const uint64_t W = n - kProbeTailKeep - 64 - 256;
+        const uint64_t span = threadIdx.x < kProbeThreads / 2 ? W / 16 : W;
+        const uint64_t i = threadIdx.x % (kProbeThreads / 2) + 1;
+        const uint64_t raw = 256 + span * i * i / ((uint64_t) kProbeThreads * kProbeThreads / 4);
+        const uint8_t *pa = (const uint8_t *) ((uintptr_t) (in + raw) & ~(uintptr_t) 15);
+        q = (uint32_t) (pa - in);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint4 x = *(const uint4 *) (pa + 16 * k);
+            sw[4 * k] = x.x;
+            sw[4 * k + 1] = x.y;
+            sw[4 * k + 2] = x.z;
+            sw[4 * k + 3] = x.w;
+        }
     }
-    *ws_view(ws, nranges).model = m;
+    build_dec_table(tab, a);
+    if (threadIdx.x == 0) s_first = 0xFFFFFFFFu;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t pj = 0xFFFFFFFFu;
+        LineModel m = probe_lines(tab, in, n, &pj);
+        if (threadIdx.x == 0) {
+            const uint32_t n32 = (uint32_t) n;
+            if (m.L == 0 && pj != 0xFFFFFFFFu) {
+                // junk in the window that no line model explains (unstructured
+                // junk, a short first line): under the clean model the slot
+                // holding it fails, so k_decode_lines takes only the slots
+                // before it, and k_decode_suffix everything from there
+                m.T = pj / 16;
+                m.skip = 1;
+            } else if (m.L == 0) {
+                m.T = n32 / 16;
+            } else {
+                m.P = m.L + m.s;
+                // T: the slots whose spans lie wholly inside the input -- those
+                // whose 16 characters are model positions below n, less the
+                // last one if a line ends right after it and its separator is
+                // cut off
+                const uint32_t F = n32 / m.P * m.L + (n32 % m.P < m.L ? n32 % m.P : m.L);
+                m.T = F / 16;
+                if (m.T && (16 * m.T) % m.L == 0 && (16 * m.T) / m.L * m.P > n32) m.T--;
+                m.k = 32 - __builtin_clz(m.L - 1);  // ceil(log2 L)
+                m.m = (uint32_t) ((((uint64_t) 1 << (31 + m.k)) + m.L - 1) / m.L);
+                m.rcp = ((1u << 20) + m.L - 1) / m.L;
+            }
+            s_m = m;
+        }
+    }
+    __syncthreads();
+    const LineModel m = s_m;
+    if (sample && !m.skip) {
+        // the first sampled byte the model gets wrong: outside the alphabet
+        // where a line character belongs, or inside it where a separator does
+        uint32_t r = m.L ? q % m.P : 0u, first = 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t j = 0; j < 64; j++) {
+            const bool al = tab[(sw[j >> 2] >> (8 * (j & 3))) & 0xFFu] < 64u;
+            const bool want = m.L == 0 || r < m.L;
+            if (al != want && first == 0xFFFFFFFFu) first = q + j;
+            if (m.L && ++r == m.P) r = 0;
+        }
+        if (first != 0xFFFFFFFFu) atomicMin(&s_first, first);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    LineModel mo = m;
+    const uint32_t pf = s_first;
+    if (!mo.skip && pf != 0xFFFFFFFFu) {
+        // the slot holding model position F(pf): every slot from there on is
+        // k_decode_suffix's
+        const uint32_t F = mo.L ? pf / mo.P * mo.L + (pf % mo.P < mo.L ? pf % mo.P : mo.L) : pf;
+        if (F / 16 < mo.T) {
+            mo.T = F / 16;
+            mo.skip = 1;
+        }
+    }
+    if (mo.skip) {
+        *ws_view(ws, nranges).lfail = ~(uint64_t) mo.T;
+        *ws_view(ws, nranges).fail_any = 1;
+    }
+    *ws_view(ws, nranges).model = mo;
 }
 
 // At least 6 waves per SIMD (80 VGPRs): unconstrained, the rarely taken
@@ -2028,8 +2149,10 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     const uint32_t lane = lane_id();
     uint32_t *bits = (uint32_t *) bq;
     int T = T0;
-    const uint32_t skew = (uint32_t) ((uintptr_t) ob & 3);
-    uint32_t lo = 4 + skew;       // LDS byte of output byte `done`
+    // the window is aligned to 16 output bytes: LDS byte 16 + (ob & 15) is
+    // output byte ob, so whole blocks copy as aligned 16-byte pairs
+    const uint32_t skew = (uint32_t) ((uintptr_t) ob & 15);
+    uint32_t lo = 16 + skew;      // LDS byte of output byte `done`
     int pb0 = 8 * (int) lo;       // window bit of relative sextet 0
     uint32_t done = 0;            // bytes flushed by earlier steps
     static_assert(kP2dBlocks > 64 && kP2dBlocks <= 128, "two zeroing stores per lane");
@@ -2049,22 +2172,23 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
         }
         T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
         if (pos + 2 * kChunk >= re) break;
-        // more of this range to come: flush the window's whole dwords
+        // more of this range to come: flush the window's whole blocks and
+        // carry the partial one to the front
         wave_lds_order();
         const int bit_end = pb0 + 6 * T;
-        const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~3u : 0u;
+        const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~15u : 0u;
         if (kcut > lo) {
-            store_bits(bits, lo, kcut, ob + done - lo);
+            store_bits16(bq, lo, kcut, ob + done - lo);
             done += kcut - lo;
-            const uint32_t keep = bits[kcut >> 2];
+            const uint4 keep = bq[kcut >> 4];
             wave_lds_order();
             bq[lane] = make_uint4(0, 0, 0, 0);
             if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
             wave_lds_order();
-            if (lane == 0) bits[1] = keep;
+            if (lane == 0) bq[1] = keep;
             wave_lds_order();
-            pb0 -= 8 * (int) (kcut - 4);
-            lo = 4;
+            pb0 -= 8 * (int) (kcut - 16);
+            lo = 16;
         }
     }
     bool at_end = last;
@@ -2102,7 +2226,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
         // src/base64decoder.c:59-62,71-76)
         const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
         const uint32_t total = 3 * ng + tail;
-        if (total > done) store_bits(bits, lo, lo + (total - done), ob + done - lo);
+        if (total > done && !B64X_AB_NOSTORE) store_bits16(bq, lo, lo + (total - done), ob + done - lo);
     }
     wave_lds_order();  // the next range re-zeroes the buffer
 }
@@ -2225,6 +2349,17 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 #ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD
 #define B64X_SFX_WPE 6
 #endif
+// A/B builds only, timing breakdowns of k_decode_suffix (wrong output):
+// NOWAIT skips the look-back, NODEC the decode, NOCOUNT the counting
+#ifndef B64X_AB_SFX_NOWAIT
+#define B64X_AB_SFX_NOWAIT 0
+#endif
+#ifndef B64X_AB_SFX_NODEC
+#define B64X_AB_SFX_NODEC 0
+#endif
+#ifndef B64X_AB_SFX_NOCOUNT
+#define B64X_AB_SFX_NOCOUNT 0
+#endif
 template <bool WHOLE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
 void k_decode_suffix(
@@ -2332,6 +2467,10 @@ void k_decode_suffix(
                 uint32_t cnt = 0;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
+                    if (B64X_AB_SFX_NOCOUNT) {
+                        cnt += nin[jj][h] & (c[jj][h].x | 16u);
+                        continue;
+                    }
                     uint32_t P[4];
                     lane_values(sm.tab, c[jj][h], nin[jj][h], P);
                     cnt += lane_valid_count(P);
@@ -2352,7 +2491,9 @@ void k_decode_suffix(
             uint64_t agg = 0;
             for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
             uint64_t excl = 0;
-            if (t > 0) {
+            if (B64X_AB_SFX_NOWAIT && t > 0) {
+                excl = (uint64_t) t * agg;  // timing only: no look-back (wrong output)
+            } else if (t > 0) {
                 if (lane == 0) st_store(&w.fstatus[t], kStAgg | agg);
                 for (int64_t p = (int64_t) t - 1;;) {
                     const int64_t q = p - lane;
@@ -2405,7 +2546,7 @@ void k_decode_suffix(
                 B += s_cnt[wv * kFusePer + j];
             }
         } else {
-        for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
+        for (uint32_t j = 0; j < kFusePer && rw + j < nranges && !B64X_AB_SFX_NODEC; j++) {
             const uint32_t r = rw + j;
             const uint64_t rb = (uint64_t) r * R;
             const uint64_t re = rb + R < n ? rb + R : n;
@@ -2447,6 +2588,256 @@ void k_decode_suffix(
                 }
             }
             return;  // this block draws no further ticket
+        }
+    }
+}
+
+// ---- single-pass exact decode, wave tiles with the count run ahead --------
+//
+// The same decode as k_decode_suffix (its header), but every wave is on its
+// own: it draws a tile of kFusePer ranges from the ticket, counts it and
+// publishes the count, then draws and counts its NEXT tile before it looks
+// back for the first one -- so by the time it looks back, every tile drawn
+// before its own has had a whole count's time to publish its inclusive
+// prefix and the look-back finds one within a step, where a block that
+// looked back right after its count waited on predecessors still counting
+// and walked back over hundreds of aggregates (k_decode_suffix: 157 of
+// 945 us on 1 GiB at junk density 0.05, profiles/r03_ab_sfx_breakdown.jsonl)
+// with its other three waves idle at a barrier.  Waves never wait for each
+// other: the only barrier is the table build.  Every wave counts a leaving
+// wave in `wdone`; the wave that decodes the last tile writes the record,
+// waits until every wave of the grid has left (so no look-back still reads
+// a status word), then clears the status words, the ticket, `wdone` and the
+// failure words.
+DEV uint32_t wave_draw(uint32_t *ticket)
+{
+    uint32_t t = 0;
+    if (lane_id() == 0) t = atomicAdd(ticket, 1u);
+    return (uint32_t) __builtin_amdgcn_readfirstlane((int) t);
+}
+
+// The idle test of k_decode_suffix<false>: false when k_decode_lines took
+// everything (its record is then mirrored to the host and the call is
+// done); else S, Vb of the first failing slot.  Every block.
+DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, uint64_t &S,
+                      uint64_t &Vb)
+{
+    __shared__ uint64_t s_key;
+    uint64_t key = 0;
+    if (scalar_load_u64(w.fail_any) != 0) {
+        if (threadIdx.x < 64) {
+            key = __hip_atomic_load((unsigned long long *) w.lfail + (threadIdx.x % kFailWords) *
+                                    kFailStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint64_t o = __shfl_xor(key, d, 64);
+                key = o > key ? o : key;
+            }
+        }
+        if (threadIdx.x == 0) s_key = key;
+        __syncthreads();
+        key = s_key;
+    }
+    if (key == 0) {
+        // nothing failed: k_decode_lines' record is final.  The host mirror
+        // is written only now, so a completion never finds a consistent but
+        // provisional record there.
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (hres) {
+                const b64x_dec_result r = *res;
+                *hres = r;
+            }
+            *w.sfx_start = ~0ull;
+        }
+        return false;
+    }
+    Vb = 16 * ~key;  // the first failing slot of k_decode_lines
+    S = line_pos(*w.model, Vb);
+    return true;
+}
+
+template <bool WHOLE>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
+void k_decode_suffix_w(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
+    uint32_t seq)
+{
+    constexpr uint64_t R = 2 * kChunk;
+    DecodeWs w = ws_view(ws, nranges);
+    uint64_t S = 0, Vb = 0;
+    if (!WHOLE && !suffix_start(w, res, hres, S, Vb)) return;
+    uint8_t *base_out = out + Vb / 4 * 3;
+    const uint32_t r0 = (uint32_t) (S / R);
+    const uint32_t ntiles = (nranges - r0 + kFusePer - 1) / kFusePer;
+    if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
+    __shared__ P2dSmem sm;
+    build_dec_table(sm.tab, a);
+    build_compact_sel(sm.sel);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *bq = sm.bits[wv];
+    uint32_t *wdone = w.wdone;
+
+    // Count tile t: lane j (< kFusePer) receives range j's alphabet count;
+    // returns the tile's total.  Two ranges' counts share one packed DPP
+    // scan (a range holds at most 2,048).
+    auto count_tile = [&](uint32_t t, uint32_t &mine) -> uint32_t {
+        const uint32_t rw = r0 + t * kFusePer;
+        uint32_t agg = 0;
+        mine = 0;
+        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
+            uint4 c[kFuseLoad][2];
+            uint32_t nin[kFuseLoad][2];
+#pragma unroll
+            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+                const uint32_t r = rw + j0 + jj;
+                const uint64_t rb = (uint64_t) r * R;
+                const uint64_t beg = rb > S ? rb : S;
+                const uint64_t re = rb + R < n ? rb + R : n;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
+                    nin[jj][h] = r >= nranges || p >= re
+                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                    c[jj][h] = nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
+                uint32_t cnt = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < 2; e++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        uint32_t P[4];
+                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
+                        cnt += lane_valid_count(P) << (16 * e);
+                    }
+                }
+                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
+                    (int) wave_incl_scan_dpp(cnt), 63);
+                const uint32_t j = j0 + jj;
+                if (lane == j) mine = tot & 0xFFFFu;
+                if (lane == j + 1) mine = tot >> 16;
+                agg += (tot & 0xFFFFu) + (tot >> 16);
+            }
+        }
+        return agg;
+    };
+    // The exclusive prefix of tile t: the counts of the tiles before it in
+    // its group of 64 (one status word per lane) plus the sums of the
+    // groups before that (up to 16 words per lane), all loaded at once --
+    // no chain of dependent loads, whatever the depth.  It waits only for
+    // tiles drawn before t to be counted.
+    auto look_back = [&](uint32_t t) -> uint32_t {
+        const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
+        const uint32_t ng = (k + 63) / 64;  // group words per lane (wave-uniform)
+        for (;;) {
+            uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
+            bool ok = (v & kStAgg) != 0;
+            uint32_t sum = (uint32_t) (v & 0xFFFFFFFFu);
+            for (uint32_t i = 0; i < ng; i++) {
+                const uint32_t j = lane + 64 * i;
+                const uint64_t g = j < k ? st_load(&w.fsuper[j]) : kGroupFull;
+                ok = ok && (g >> 56) == kSfxGroup;
+                sum += (uint32_t) (g & 0xFFFFFFFFu);
+            }
+            if (__all(ok))
+                return (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(sum), 63);
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    // Publish tile t's count: its status word and its group's sum.
+    auto publish = [&](uint32_t t, uint32_t agg) {
+        if (lane == 0) {
+            st_store(&w.fstatus[t], kStAgg | agg);
+            __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    auto decode_tile = [&](uint32_t t, uint32_t B, uint32_t mine) {
+        const uint32_t rw = r0 + t * kFusePer;
+        for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
+            const uint32_t r = rw + j;
+            const uint64_t rb = (uint64_t) r * R;
+            const uint64_t re = rb + R < n ? rb + R : n;
+            const bool first = r == r0, last = r + 1 == nranges;
+            const uint64_t start = first ? S : rb;
+            uint4 c[2];
+            uint32_t nin[2], la;
+            bool la_ok;
+            load_range(in, n, start, re, last, c, nin, la, la_ok);
+            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
+                         base_out + (B + 3) / 4 * 3, c, nin, la, la_ok, last, hold);
+            B += (uint32_t) __builtin_amdgcn_readlane((int) mine, (int) j);
+        }
+    };
+
+    bool owner = false;  // this wave decoded the last tile
+    uint32_t Vs = 0;     // then: the suffix's alphabet characters
+#ifndef B64X_SFX_AHEAD  // A/B builds only: count the next tile before looking back
+#define B64X_SFX_AHEAD 1
+#endif
+    if (!B64X_SFX_AHEAD) {
+        for (;;) {
+            const uint32_t t = wave_draw(w.fticket);
+            if (t >= ntiles) break;
+            uint32_t m = 0;
+            const uint32_t ag = count_tile(t, m);
+            publish(t, ag);
+            const uint32_t ex = t ? look_back(t) : 0u;
+            decode_tile(t, ex, m);
+            if (t == ntiles - 1) {
+                owner = true;
+                Vs = ex + ag;
+            }
+        }
+    }
+    uint32_t tA = B64X_SFX_AHEAD ? wave_draw(w.fticket) : ntiles, mA = 0, aA = 0;
+    if (tA < ntiles) {
+        aA = count_tile(tA, mA);
+        publish(tA, aA);
+    }
+    while (tA < ntiles) {
+        const uint32_t tB = wave_draw(w.fticket);
+        uint32_t mB = 0, aB = 0;
+        if (tB < ntiles) {
+            aB = count_tile(tB, mB);
+            publish(tB, aB);
+        }
+        const uint32_t ex = tA ? look_back(tA) : 0u;
+        decode_tile(tA, ex, mA);
+        if (tA == ntiles - 1) {
+            owner = true;
+            Vs = ex + aA;
+        }
+        tA = tB;
+        mA = mB;
+        aA = aB;
+    }
+    // every look-back and decode of this wave is over (relaxed: the look-back
+    // loads have returned -- their values decided the loop -- and a release
+    // at agent scope would write back the L2, once per wave)
+    if (lane == 0) __hip_atomic_fetch_add(wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!owner) return;
+    const uint64_t V = Vb + Vs;
+    if (lane == 0) write_result(res, hres, V, hold, n, seq);
+    find_tail_sextets(sm.tab, in, n, V, res, hres);
+    if (lane == 0) {
+        const uint32_t want = gridDim.x * kWavesPerBlock;
+        while (__hip_atomic_load(wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+    for (uint32_t i = lane; i < (ntiles + kSfxGroup - 1) / kSfxGroup; i += 64) st_store(&w.fsuper[i], 0);
+    if (lane == 0) {
+        __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!WHOLE) {
+            for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
+            *w.fail_any = 0;
         }
     }
 }
@@ -3779,18 +4170,23 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         // of whatever suffix it could not take -- nothing, on clean and
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
-        static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
+#ifndef B64X_SFX_WAVE  // A/B builds only: 1 = wave tiles with the count run ahead (k_decode_suffix_w)
+#define B64X_SFX_WAVE 0
+#endif
+        static const int occ_sfx = B64X_SFX_WAVE ? occupancy_of(k_decode_suffix_w<false>)
+                                                 : occupancy_of(k_decode_suffix<false>);
 #ifndef B64X_SFX_OCC  // A/B builds only: blocks per CU of the suffix grid (0: occupancy)
 #define B64X_SFX_OCC 0
 #endif
         const uint32_t sfx_grid = (uint32_t) d->cus * (B64X_SFX_OCC ? B64X_SFX_OCC : occ_sfx);
         if (flags & B64X_DEC_EXPECT_JUNK) {
-            hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL((B64X_SFX_WAVE ? k_decode_suffix_w<true> : k_decode_suffix<true>),
+                               dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq);
             return launch_status();
         }
-        hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(64), 0, s, (const uint8_t *) d_in, nchars,
+        hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s, (const uint8_t *) d_in, nchars,
                            a, ws, p.nranges);
         if ((err = launch_status())) return err;
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
@@ -3798,7 +4194,8 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
-        hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL((B64X_SFX_WAVE ? k_decode_suffix_w<false> : k_decode_suffix<false>),
+                           dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                            hold, d_res, h_res, seq);
         return launch_status();

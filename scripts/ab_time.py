@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib, steps):
+def child(lib, steps, only=()):
     sys.path.insert(0, ROOT)
     import torch
     from async_amd import _lib
@@ -30,12 +30,16 @@ def child(lib, steps):
     enc = b64.encode(x)
     dirty = crlf76(enc)
     junk = sprinkle(enc, 0.05)
+    junk1 = sprinkle(enc, 0.001)
     out = torch.empty(b64.decoded_cap(junk.numel()), dtype=torch.uint8, device="cuda")
     rr = torch.zeros(_lib.RES_BYTES, dtype=torch.uint8, device="cuda")
     ws = torch.zeros(b64.workspace_size(junk.numel()), dtype=torch.uint8, device="cuda")
     res = {}
 
     def timeit(name, fn):
+        if only and name not in only:
+            res[name] = (0.0, 0.0, 0.0)
+            return
         fn()
         torch.cuda.synchronize()
         ts = []
@@ -55,11 +59,21 @@ def child(lib, steps):
     ok = ok and torch.equal(out[:n], x)
     timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
     ok = ok and torch.equal(out[:n], x)
+    timeit("junk1", lambda: b64.decode(junk1, out=out, workspace=ws, result=rr))
+    ok = ok and torch.equal(out[:n], x)
+    timeit("junk_ej", lambda: b64.decode(junk, out=out, workspace=ws, result=rr,
+                                         expect_junk=True))
+    ok = ok and torch.equal(out[:n], x)
     timeit("crlf_ej", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
     ok = ok and torch.equal(out[:n], x)
     # config 4: 1 M x 1 KiB rows, strided decode (clean)
-    del dirty, junk, enc, out, x
+    del dirty, junk, junk1, enc, out, x
+    if only and not ({"rows_enc", "rows_dec", "rows_crlf", "ragged_dec"} & set(only)):
+        for k in ("rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
+            res[k] = (0.0, 0.0, 0.0)
+        print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
+        return
     nb, L = 1 << 20, 1024
     Es = b64.encoded_len(L)
     cap = 12 * ((Es + 15) // 16)
@@ -117,15 +131,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated legs (default: all)")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     if a.child:
-        return child(a.libs[0], a.steps)
+        return child(a.libs[0], a.steps, tuple(x for x in a.only.split(",") if x))
     agg = {lib: {} for lib in a.libs}
     for r in range(a.rounds):
         for lib in a.libs:
-            p = subprocess.run([sys.executable, __file__, "--child", "--steps", str(a.steps), lib],
+            p = subprocess.run([sys.executable, __file__, "--child", "--steps", str(a.steps), "--only", a.only, lib],
                                capture_output=True, text=True, timeout=300)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
             if p.returncode or not line:
@@ -133,7 +148,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("encode", "decode", "crlf", "junk", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
+            for k in ("encode", "decode", "crlf", "junk", "junk1", "junk_ej", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)

@@ -725,6 +725,43 @@ def test_decode_lines_takes_clean_and_mime_whole(aligned):
             assert start <= brk and brk - start < 1 << 12, (brk, start)
 
 
+def _probe_model(ws: torch.Tensor):
+    """The line model k_decode_probe left in the workspace (header bytes
+    32..63): (L, s, T, skip)."""
+    torch.cuda.synchronize()
+    m = np.frombuffer(ws[32:64].cpu().numpy().tobytes(), np.uint32)
+    return int(m[0]), int(m[1]), int(m[3]), int(m[7])
+
+
+def test_probe_samples_cut_sparse_junk():
+    """k_decode_probe checks samples past its first window against the
+    model: sparse junk the window does not show cuts k_decode_lines' slots
+    near the first sampled junk (so the exact suffix does not redo them),
+    while clean and MIME text, and junk only in the stream's last bytes, keep
+    every slot with k_decode_lines."""
+    rng = np.random.default_rng(43)
+    chars = orc.encode(rng.integers(0, 256, 3_000_000, dtype=np.uint8))
+    n = len(chars)
+    ws = torch.zeros(b64.workspace_size(n * 2), dtype=torch.uint8, device=DEV)
+    sparse = chars[:4096] + _junk(rng, chars[4096:], 1e-3)
+    tail = chars[:-1000] + b"!" + chars[-1000:]
+    mime = _wrap(chars, 76, b"\r\n")
+    mime_sparse = mime[:8192] + _junk(rng, mime[8192:], 1e-3)
+    for name, text, cut in (("clean", chars, False), ("mime", mime, False), ("tail", tail, False),
+                            ("sparse", sparse, True), ("mime_sparse", mime_sparse, True)):
+        out = torch.empty(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+        d = b64.decode(dev(text), out=out, workspace=ws)
+        assert d.bytes().cpu().numpy().tobytes() == orc.decode(text), name
+        L, s, T, skip = _probe_model(ws)
+        assert L == (76 if name.startswith("mime") else 0), name
+        if cut:
+            # 256 samples, dense near the start: at 0.1 % junk the first one
+            # that finds junk lies within the first few percent of the stream
+            assert skip == 1 and 16 * T < len(text) // 20, (name, T)
+        else:
+            assert skip == 0, name
+
+
 def _mime_batch(nbuf, n, L, sep, rng, deviants=()):
     rows = []
     for i in range(nbuf):
