@@ -875,13 +875,14 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //           scalar load instead of a wave reading all 64 words per block
 //   model   the line model k_decode_probe found, for k_decode_lines and
 //           k_decode_suffix
-//   fticket, fstatus  k_decode_suffix's tile ticket and status words
+//   fticket, fstatus, fsuper, wdone  k_decode_suffix's tile ticket, tile
+//           counts, group sums and count of blocks that have left
 //   sfx_start  where the last call's k_decode_suffix<false> started (its
 //           first failing slot's span), ~0 when it had nothing to do; read
 //           by the tests only (clean and MIME input must never need it)
-// The regions that must be zero between calls (status, fstatus, lfail) sit
-// at fixed offsets after the header, sized for the largest plan, so calls of
-// different sizes on one workspace never find another call's scratch
+// The regions that must be zero between calls (status, fstatus, fsuper, lfail,
+// wdone) sit at fixed offsets after the header, sized for the largest plan,
+// so calls of different sizes on one workspace never find another call's scratch
 // (counts, bases) where they expect zeros.
 // The line model of k_decode_lines (see there): lines of L alphabet
 // characters, each followed by s separator bytes; L = 0: no separators.
@@ -898,7 +899,7 @@ static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of m
 struct DecodeWs {
     uint64_t *lfail;     // kFailWords words, kFailStride apart
     uint64_t *fail_any;  // nonzero: some failure word was published (own line)
-    uint32_t *wdone;     // k_decode_suffix_w: waves that have left (own line; zero between calls)
+    uint32_t *wdone;     // k_decode_suffix: blocks that have left (own line; zero between calls)
     LineModel *model;    // k_decode_lines' model, for k_decode_suffix
     uint64_t *fd;
     uint64_t *fd_cur;
@@ -909,7 +910,7 @@ struct DecodeWs {
     uint64_t *bases;
     uint64_t *status;
     uint64_t *fstatus;   // the single-pass decode's tile status words (zero between calls)
-    uint64_t *fsuper;    // k_decode_suffix_w's group sums: tiles counted << 56 | sum (zero between calls)
+    uint64_t *fsuper;    // k_decode_suffix's group sums: tiles counted << 56 | sum (zero between calls)
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
@@ -918,19 +919,15 @@ constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 #endif
 constexpr uint32_t kFusePer = B64X_FUSE_PER;  // ranges per wave in the single-pass decode
 constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
-#ifndef B64X_FUSE_HOLD  // A/B builds only
-#define B64X_FUSE_HOLD 0
-#endif
-constexpr bool kFuseHold = B64X_FUSE_HOLD;
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsStatus = 64;                                        // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
-constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix_w: tiles per group sum
+constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix: tiles per group sum
 constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
-constexpr uint64_t kWsFSuper = kWsFStatus + kMaxRanges / kFusePer * 8;    // suffix group sums
-constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kFusePer / kSfxGroup + 16) * 8;  // lines failures
+constexpr uint64_t kWsFSuper = kWsFStatus + kMaxRanges / kFuseTile * 8;   // suffix group sums
+constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kFuseTile / kSfxGroup + 16) * 8;  // lines failures
 // failure words, fail_any, wdone: one 128-byte line each
 constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
@@ -1385,12 +1382,6 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
 }
 
 // ---- pass 2, bit-stream form ----------------------------------------------
-#ifndef B64X_AB_NOOR  // A/B builds only (timing breakdowns, wrong output)
-#define B64X_AB_NOOR 0
-#endif
-#ifndef B64X_AB_NOSTORE
-#define B64X_AB_NOSTORE 0
-#endif
 //
 // The range's output is built in LDS directly as the decoded BIT stream (a
 // per-character scatter of sextets into LDS, read back and converted group
@@ -1536,42 +1527,39 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
     // per dword: table values, the v_perm compaction selector (by the
-    // invalid-byte pattern, via v_dot4 of the bit-7s) and the count of
-    // non-alphabet bytes; both chunks' counts in one packed DPP scan
-    uint32_t P[2][4], sel[2][4], bad[2][4], cnt = 0;
+    // invalid-byte pattern, via v_dot4 of the bit-7s) and 6 x the count of
+    // non-alphabet bytes; the scan runs over the lanes' BIT counts (both
+    // chunks packed in one DPP scan), so positions need no multiply
+    uint32_t P[2][4], sel[2][4], six[2][4], cnt = 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         lane_values(sm.tab, c[h], nin[h], P[h]);
-        uint32_t nb = 0;
+        uint32_t nb6 = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
             const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
             sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-            bad[h][g] = __builtin_amdgcn_udot4(iv, 0x01010101u, 0u, false);
-            nb += bad[h][g];
+            six[h][g] = __builtin_amdgcn_udot4(iv, 0x06060606u, 0u, false);
+            nb6 += six[h][g];
         }
-        cnt |= (16u - nb) << (16 * h);
+        cnt |= (96u - nb6) << (16 * h);  // the lane's output bits in chunk h (<= 96)
     }
-    const uint32_t incl = wave_incl_scan_dpp(cnt);
+    const uint32_t incl = wave_incl_scan_dpp(cnt);  // halves <= 6,144
     const uint32_t ex = incl - cnt;
     const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        const int before = h ? (int) (tot & 0xFFFFu) : 0;
-        uint32_t p = (uint32_t) (bit0 + 6 * (before + (int) ((ex >> (16 * h)) & 0xFFFFu)));
+        const uint32_t before = h ? tot & 0xFFFFu : 0u;
+        uint32_t p = (uint32_t) bit0 + before + ((ex >> (16 * h)) & 0xFFFFu);
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
-#if B64X_AB_NOOR  // timing only (wrong output): the fields computed, one plain store
-            if (g == 3 && p == 0xFFFFFFFFu) bits[0] = group_dot(D);
-#else
             or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
-#endif
-            p += 24u - 6u * bad[h][g];
+            p += 24u - six[h][g];
         }
     }
-    return (tot & 0xFFFFu) + (tot >> 16);
+    return ((tot & 0xFFFFu) + (tot >> 16)) / 6u;  // alphabet characters (scalar)
 }
 
 // ---- line-structured single-pass decode ------------------------------------
@@ -1931,6 +1919,11 @@ void k_decode_lines(
     const uint64_t mw0 = scalar_load_u64(mp), mw1 = scalar_load_u64(mp + 1),
                    mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
     build_dec_table(tab, a);
+    // a block wholly past slot T (the probe cut the model's slots at junk)
+    // leaves before the barrier: on junk-laden input nearly every block of
+    // this launch does.  (Tested before the table build, the model's load
+    // no longer overlapped the build: MIME text +2 %.)
+    if (blockIdx.x * kWavesPerBlock * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
     __syncthreads();
     LineModel m;
     m.L = (uint32_t) mw0;
@@ -2142,9 +2135,33 @@ void k_decode_lines(
 // flushed between steps and its partial dword carried to the front (as
 // decode_buf_bits does); the bytes flushed early are final and never reach
 // the next range's output.
+// One wave copies 64 x 16 bytes from gsrc (per lane) to LDS at lds_dst +
+// 16 x lane, straight into LDS (global_load_lds_dwordx4: no VGPR holds the
+// data).  Issued as inline asm so that the compiler does not track the copy:
+// it cannot tell the copy's destination from the decode's other LDS traffic
+// (the window's atomic ORs go through a pointer) and waited for every copy
+// in flight (vmcnt(0)) at the first of them, right after the copy was
+// issued.  The reader waits itself (vm_wait_all) before it reads the copy.
+DEV void lds_dma16(const void *gsrc, void *lds_dst)
+{
+    const uint32_t l = (uint32_t) (uintptr_t) (__attribute__((address_space(3))) void *) lds_dst;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
+}
+
+DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// la_lds (optional): where the lookahead bytes sit in LDS (the next range,
+// prefetched there by k_decode_suffix); read only when the range's last
+// group needs them, so the prefetch has the whole range's time to land.
+// la_late: the lookahead bytes are read from `in` only when needed (la
+// and la_ok are ignored), so no global load is in flight during the range.
 DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ in, uint64_t n,
                       uint64_t start, uint64_t re, int T0, uint8_t *ob, const uint4 c[2],
-                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold)
+                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold,
+                      const uint8_t *la_lds = nullptr, bool la_late = false)
 {
     const uint32_t lane = lane_id();
     uint32_t *bits = (uint32_t *) bq;
@@ -2159,21 +2176,13 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     bq[lane] = make_uint4(0, 0, 0, 0);
     if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
     wave_lds_order();
-    for (uint64_t pos = start;; pos += 2 * kChunk) {
-        uint4 ch[2] = {c[0], c[1]};
-        uint32_t nh[2] = {nin[0], nin[1]};
-        if (pos != start) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
-                nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
-                ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
-            }
-        }
-        T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
-        if (pos + 2 * kChunk >= re) break;
-        // more of this range to come: flush the window's whole blocks and
-        // carry the partial one to the front
+    // the first step from the chunks given (its own code: joined with the
+    // loads of the later steps, the compiler waited for every load in
+    // flight before the step, ranges read ahead included)
+    T += (int) bits_step(sm, bits, c, nin, pb0 + 6 * T);
+    for (uint64_t pos = start + 2 * kChunk; pos < re; pos += 2 * kChunk) {
+        // more of this range: flush the window's whole blocks and carry the
+        // partial one to the front
         wave_lds_order();
         const int bit_end = pb0 + 6 * T;
         const uint32_t kcut = bit_end > 0 ? ((uint32_t) bit_end >> 3) & ~15u : 0u;
@@ -2190,11 +2199,28 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
             pb0 -= 8 * (int) (kcut - 16);
             lo = 16;
         }
+        uint4 ch[2];
+        uint32_t nh[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint64_t q = pos + (uint64_t) h * kChunk + 16 * lane;
+            nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
+            ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
+        }
+        T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
     }
     bool at_end = last;
     if (!last && T > 0 && (T & 3)) {
         // complete the range's last group from the characters after it
         bool ok = la_ok;
+        if (la_lds) {
+            vm_wait_all();  // the next range's copy, issued when this range began
+            ok = true;      // (the next range is whole)
+            la = la_lds[lane_id()];
+        } else if (la_late) {
+            ok = re + lane_id() < n;
+            la = ok ? in[re + lane_id()] : 0u;
+        }
         for (uint64_t q = re;;) {
             const uint32_t t = ok ? sm.tab[la] : 0xFFu;
             const bool v = t < 64u;
@@ -2226,7 +2252,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
         // src/base64decoder.c:59-62,71-76)
         const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
         const uint32_t total = 3 * ng + tail;
-        if (total > done && !B64X_AB_NOSTORE) store_bits16(bq, lo, lo + (total - done), ob + done - lo);
+        if (total > done) store_bits16(bq, lo, lo + (total - done), ob + done - lo);
     }
     wave_lds_order();  // the next range re-zeroes the buffer
 }
@@ -2334,287 +2360,33 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 //
 // Ranges are the pass-1 ranges of R = 2,048 characters, aligned to the
 // stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
-// tiles of kFuseTile ranges from a ticket in the order they start (so a
-// tile's predecessors are running or done); each wave counts its kFusePer
-// ranges, the block publishes the tile's count and looks back over its
-// predecessors' status words as k_decode_scan2 does, then each wave decodes
-// its ranges with decode_range, re-reading them (the tile was just read:
-// L2/MALL hits).  The last tile writes the result record, waits until every
-// other block has drawn its final ticket (so every look-back is over), then
-// clears the status words, the ticket and the failure word.
-// At least 6 waves per SIMD (80 VGPRs; WHOLE took 96 and 5 waves): 1 GiB of
-// CRLF-76 under EXPECT_JUNK 998 -> 947 us, junk density 0.05 1045 -> 1026 us.
-// (Prefetching each range's chunks during the previous range's decode needed
-// 107 VGPRs and lost, with or without this bound.)
+// tiles of kFuseTile ranges (kFusePer per wave) from a ticket in the order
+// they start, so a tile's predecessors are running or done whatever else
+// shares the GPU.  A block counts its tile and publishes the count, then
+// draws and counts its NEXT tile before it takes the first one's prefix, and
+// decodes the first one with decode_range (re-reading it).  The prefix is not
+// a chained look-back: it is the counts of the tiles before it in its group
+// of 64 tiles (one status word per lane) plus the sums of the earlier groups
+// (every tile adds its count into its group's word), all loaded at once, so
+// it takes one memory round trip at any depth and waits only for tiles drawn
+// before this one to be counted -- which, counted one tile ahead, they are.
+// (Round 2's chained look-back -- back over predecessors' aggregates 64 at a
+// time to the first inclusive prefix, right after the count, three waves
+// idle at a barrier -- cost 157 of 945 us on 1 GiB at junk density 0.05,
+// profiles/r03_ab_sfx_breakdown.jsonl.)  Every block counts itself out in
+// `wdone` when it leaves; the block that decodes the last tile writes the
+// record, waits until every block has left (so no prefix read is in
+// flight), then clears the status and group words, the ticket, `wdone` and
+// the failure words.
+// At least 6 waves per SIMD (80 VGPRs).
 #ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD
 #define B64X_SFX_WPE 6
 #endif
-// A/B builds only, timing breakdowns of k_decode_suffix (wrong output):
-// NOWAIT skips the look-back, NODEC the decode, NOCOUNT the counting
-#ifndef B64X_AB_SFX_NOWAIT
-#define B64X_AB_SFX_NOWAIT 0
-#endif
-#ifndef B64X_AB_SFX_NODEC
-#define B64X_AB_SFX_NODEC 0
-#endif
-#ifndef B64X_AB_SFX_NOCOUNT
-#define B64X_AB_SFX_NOCOUNT 0
-#endif
-template <bool WHOLE>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
-void k_decode_suffix(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
-    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
-    uint32_t seq)
-{
-    constexpr uint64_t R = 2 * kChunk;
-    DecodeWs w = ws_view(ws, nranges);
-    uint64_t S = 0, Vb = 0;
-    if (!WHOLE) {
-        if (scalar_load_u64(w.fail_any) == 0) {
-            // nothing failed (the common case; one scalar load per block):
-            // k_decode_lines took everything and its record is final.  The
-            // host mirror is written only now, so a completion never finds a
-            // consistent but provisional record there.
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
-                if (hres) {
-                    const b64x_dec_result r = *res;
-                    *hres = r;
-                }
-                *w.sfx_start = ~0ull;
-            }
-            return;
-        }
-        // the first failing slot: the largest key over the failure words
-        // (one wave reads them all, every block)
-        uint64_t key = 0;
-        if (threadIdx.x < 64) {
-            key = __hip_atomic_load((unsigned long long *) w.lfail + (threadIdx.x % kFailWords) *
-                                    kFailStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const uint64_t o = __shfl_xor(key, d, 64);
-                key = o > key ? o : key;
-            }
-        }
-        __shared__ uint64_t s_key;
-        if (threadIdx.x == 0) s_key = key;
-        __syncthreads();
-        key = s_key;
-        if (key == 0) {
-            // k_decode_lines took everything: its record is final.  The host
-            // mirror is written only now, so a completion never finds a
-            // consistent but provisional record there.
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
-                if (hres) {
-                    const b64x_dec_result r = *res;
-                    *hres = r;
-                }
-                *w.sfx_start = ~0ull;
-            }
-            return;
-        }
-        const uint64_t tf = ~key;  // the first failing slot of k_decode_lines
-        Vb = 16 * tf;
-        S = line_pos(*w.model, Vb);
-    }
-    const uint8_t *base_in = in;
-    uint8_t *base_out = out + Vb / 4 * 3;
-    const uint32_t r0 = (uint32_t) (S / R);
-    const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
-    if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
-    __shared__ P2dSmem sm;
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_cnt[kFuseTile];
-    __shared__ uint64_t s_excl, s_agg;
-    build_dec_table(sm.tab, a);
-    build_compact_sel(sm.sel);
-    const uint32_t lane = lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint4 *bq = sm.bits[wv];
-    for (;;) {
-        __syncthreads();  // s_tile / s_cnt of the previous tile are consumed
-        if (threadIdx.x == 0) s_tile = atomicAdd(w.fticket, 1u);
-        __syncthreads();
-        const uint32_t t = s_tile;
-        if (t >= ntiles) return;
-        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
-        // counts; all of the wave's loads are issued before any is counted
-        // HOLD: the wave's ranges all fit one load group; its chunks stay in
-        // registers for the decode instead of being re-read (B64X_FUSE_HOLD)
-        constexpr bool kHold = kFuseHold && kFusePer <= kFuseLoad;
-        uint4 hc[kHold ? kFuseLoad : 1][2];
-        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
-            uint4 c[kFuseLoad][2];
-            uint32_t nin[kFuseLoad][2];
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                const uint32_t r = rw + j0 + jj;
-                const uint64_t rb = (uint64_t) r * R;
-                const uint64_t beg = rb > S ? rb : S;
-                const uint64_t re = rb + R < n ? rb + R : n;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
-                    nin[jj][h] = r >= nranges || p >= re
-                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                    c[jj][h] =
-                        nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                uint32_t cnt = 0;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    if (B64X_AB_SFX_NOCOUNT) {
-                        cnt += nin[jj][h] & (c[jj][h].x | 16u);
-                        continue;
-                    }
-                    uint32_t P[4];
-                    lane_values(sm.tab, c[jj][h], nin[jj][h], P);
-                    cnt += lane_valid_count(P);
-                }
-                cnt = wave_sum(cnt);
-                if (lane == 0) s_cnt[wv * kFusePer + j0 + jj] = cnt;
-            }
-            if constexpr (kHold) {
-#pragma unroll
-                for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                    hc[jj][0] = c[jj][0];
-                    hc[jj][1] = c[jj][1];
-                }
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            uint64_t agg = 0;
-            for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
-            uint64_t excl = 0;
-            if (B64X_AB_SFX_NOWAIT && t > 0) {
-                excl = (uint64_t) t * agg;  // timing only: no look-back (wrong output)
-            } else if (t > 0) {
-                if (lane == 0) st_store(&w.fstatus[t], kStAgg | agg);
-                for (int64_t p = (int64_t) t - 1;;) {
-                    const int64_t q = p - lane;
-                    const uint64_t v = q >= 0 ? st_load(&w.fstatus[q]) : kStIncl;
-                    const uint32_t f = (uint32_t) (v >> 62);
-                    const uint64_t inc = __ballot(f == 2);
-                    const uint32_t k =
-                        inc ? (uint32_t) __ffsll((unsigned long long) inc) - 1 : 63u;
-                    if (!__all(lane > k || f != 0)) {
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    uint64_t part = lane <= k ? (v & kStVal) : 0;
-#pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
-                    excl += part;
-                    if (inc) break;
-                    p -= 64;
-                }
-            }
-            if (lane == 0) {
-                st_store(&w.fstatus[t], kStIncl | (excl + agg));
-                s_excl = excl;
-                s_agg = agg;
-            }
-        }
-        __syncthreads();
-        uint64_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
-        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
-        if constexpr (kHold) {
-            // the wave's ranges from the chunks held since the count
-#pragma unroll
-            for (uint32_t j = 0; j < kFusePer; j++) {
-                const uint32_t r = rw + j;
-                if (r >= nranges) break;
-                const uint64_t rb = (uint64_t) r * R;
-                const uint64_t re = rb + R < n ? rb + R : n;
-                const bool first = r == r0, last = r + 1 == nranges;
-                const uint64_t start = first ? S : rb;
-                uint32_t nin[2];
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                }
-                const bool la_ok = !last && re + lane < n;
-                const uint32_t la = la_ok ? base_in[re + lane] : 0u;
-                decode_range(sm, bq, base_in, n, start, re, first ? 0 : range_skip(B),
-                             base_out + (B + 3) / 4 * 3, hc[j], nin, la, la_ok, last, hold);
-                B += s_cnt[wv * kFusePer + j];
-            }
-        } else {
-        for (uint32_t j = 0; j < kFusePer && rw + j < nranges && !B64X_AB_SFX_NODEC; j++) {
-            const uint32_t r = rw + j;
-            const uint64_t rb = (uint64_t) r * R;
-            const uint64_t re = rb + R < n ? rb + R : n;
-            const bool first = r == r0, last = r + 1 == nranges;
-            const uint64_t start = first ? S : rb;
-            uint4 c[2];
-            uint32_t nin[2], la;
-            bool la_ok;
-            load_range(base_in, n, start, re, last, c, nin, la, la_ok);
-            decode_range(sm, bq, base_in, n, start, re, first ? 0 : range_skip(B),
-                         base_out + (B + 3) / 4 * 3, c, nin, la, la_ok, last, hold);
-            B += s_cnt[wv * kFusePer + j];
-        }
-        }
-        if (t == ntiles - 1) {
-            if (wv == 0) {
-                const uint64_t V = Vb + s_excl + s_agg;
-                if (lane == 0) write_result(res, hres, V, hold, n, seq);
-                find_tail_sextets(sm.tab, in, n, V, res, hres);
-                // Every other block has drawn its final ticket -> every
-                // look-back is over (a block draws its next ticket only after
-                // finishing its tile, look-back included), so the status words
-                // can be cleared and the ticket re-armed.  (This used to wait
-                // for every status word to read inclusive first: one dependent
-                // device-scope load per 64 tiles, ~170 round trips per GiB at
-                // the end of every call, and redundant with the ticket.)
-                if (lane == 0) {
-                    const uint32_t want = ntiles + gridDim.x - 1;
-                    while (__hip_atomic_load(w.fticket, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) != want)
-                        __builtin_amdgcn_s_sleep(1);
-                }
-                for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
-                if (lane == 0) {
-                    __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!WHOLE)
-                        for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
-                    if (!WHOLE) *w.fail_any = 0;
-                }
-            }
-            return;  // this block draws no further ticket
-        }
-    }
-}
 
-// ---- single-pass exact decode, wave tiles with the count run ahead --------
-//
-// The same decode as k_decode_suffix (its header), but every wave is on its
-// own: it draws a tile of kFusePer ranges from the ticket, counts it and
-// publishes the count, then draws and counts its NEXT tile before it looks
-// back for the first one -- so by the time it looks back, every tile drawn
-// before its own has had a whole count's time to publish its inclusive
-// prefix and the look-back finds one within a step, where a block that
-// looked back right after its count waited on predecessors still counting
-// and walked back over hundreds of aggregates (k_decode_suffix: 157 of
-// 945 us on 1 GiB at junk density 0.05, profiles/r03_ab_sfx_breakdown.jsonl)
-// with its other three waves idle at a barrier.  Waves never wait for each
-// other: the only barrier is the table build.  Every wave counts a leaving
-// wave in `wdone`; the wave that decodes the last tile writes the record,
-// waits until every wave of the grid has left (so no look-back still reads
-// a status word), then clears the status words, the ticket, `wdone` and the
-// failure words.
-DEV uint32_t wave_draw(uint32_t *ticket)
-{
-    uint32_t t = 0;
-    if (lane_id() == 0) t = atomicAdd(ticket, 1u);
-    return (uint32_t) __builtin_amdgcn_readfirstlane((int) t);
-}
+#ifndef B64X_SFX_DMA  // A/B builds only: read ranges ahead into LDS (global_load_lds)
+#define B64X_SFX_DMA 1
+#endif
+constexpr bool kSfxDma = B64X_SFX_DMA;
 
 // The idle test of k_decode_suffix<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
@@ -2625,6 +2397,7 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
     __shared__ uint64_t s_key;
     uint64_t key = 0;
     if (scalar_load_u64(w.fail_any) != 0) {
+        // the first failing slot: the largest key over the failure words
         if (threadIdx.x < 64) {
             key = __hip_atomic_load((unsigned long long *) w.lfail + (threadIdx.x % kFailWords) *
                                     kFailStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2658,7 +2431,7 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
 
 template <bool WHOLE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
-void k_decode_suffix_w(
+void k_decode_suffix(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
     uint32_t seq)
@@ -2669,24 +2442,26 @@ void k_decode_suffix_w(
     if (!WHOLE && !suffix_start(w, res, hres, S, Vb)) return;
     uint8_t *base_out = out + Vb / 4 * 3;
     const uint32_t r0 = (uint32_t) (S / R);
-    const uint32_t ntiles = (nranges - r0 + kFusePer - 1) / kFusePer;
+    const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
     if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
+    const bool dma = (((uintptr_t) in) & 15) == 0;
     __shared__ P2dSmem sm;
+    // per wave: two ranges read ahead (an LDS object of its own, so that the
+    // compiler sees table and window reads cannot alias the copies in flight)
+    __shared__ uint4 s_rng[kWavesPerBlock][2][kSfxDma ? 128 : 1];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_cnt[2][kFuseTile];
+    __shared__ uint32_t s_excl;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
-    __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
-    uint32_t *wdone = w.wdone;
 
-    // Count tile t: lane j (< kFusePer) receives range j's alphabet count;
-    // returns the tile's total.  Two ranges' counts share one packed DPP
-    // scan (a range holds at most 2,048).
-    auto count_tile = [&](uint32_t t, uint32_t &mine) -> uint32_t {
-        const uint32_t rw = r0 + t * kFusePer;
-        uint32_t agg = 0;
-        mine = 0;
+    // Count tile t into s_cnt[b] (each wave its kFusePer ranges; every
+    // wave's loads issued before any is counted).  Block-uniform call.
+    auto count_tile = [&](uint32_t t, uint32_t b) {
+        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
         for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
             uint4 c[kFuseLoad][2];
             uint32_t nin[kFuseLoad][2];
@@ -2705,136 +2480,153 @@ void k_decode_suffix_w(
                 }
             }
 #pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
+            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
                 uint32_t cnt = 0;
 #pragma unroll
-                for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        uint32_t P[4];
-                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
-                        cnt += lane_valid_count(P) << (16 * e);
-                    }
+                for (int h = 0; h < 2; h++) {
+                    uint32_t P[4];
+                    lane_values(sm.tab, c[jj][h], nin[jj][h], P);
+                    cnt += lane_valid_count(P);
                 }
-                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
-                    (int) wave_incl_scan_dpp(cnt), 63);
-                const uint32_t j = j0 + jj;
-                if (lane == j) mine = tot & 0xFFFFu;
-                if (lane == j + 1) mine = tot >> 16;
-                agg += (tot & 0xFFFFu) + (tot >> 16);
+                cnt = wave_sum(cnt);
+                if (lane == 0) s_cnt[b][wv * kFusePer + j0 + jj] = cnt;
             }
         }
-        return agg;
     };
-    // The exclusive prefix of tile t: the counts of the tiles before it in
-    // its group of 64 (one status word per lane) plus the sums of the
-    // groups before that (up to 16 words per lane), all loaded at once --
-    // no chain of dependent loads, whatever the depth.  It waits only for
-    // tiles drawn before t to be counted.
-    auto look_back = [&](uint32_t t) -> uint32_t {
+    // Publish tile t's count (s_cnt[b] complete): its status word and its
+    // group's sum.  Thread 0.
+    auto publish = [&](uint32_t t, uint32_t b) {
+        uint32_t agg = 0;
+        for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[b][i];
+        st_store(&w.fstatus[t], kStAgg | agg);
+        __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // The alphabet characters of the suffix before tile t.  Wave 0.
+    auto prefix = [&](uint32_t t) -> uint32_t {
         const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
-        const uint32_t ng = (k + 63) / 64;  // group words per lane (wave-uniform)
+        const uint32_t ng = (k + 63) / 64;  // group words per lane (uniform)
         for (;;) {
-            uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
+            const uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
             bool ok = (v & kStAgg) != 0;
-            uint32_t sum = (uint32_t) (v & 0xFFFFFFFFu);
+            uint32_t sum = (uint32_t) v;
             for (uint32_t i = 0; i < ng; i++) {
                 const uint32_t j = lane + 64 * i;
                 const uint64_t g = j < k ? st_load(&w.fsuper[j]) : kGroupFull;
                 ok = ok && (g >> 56) == kSfxGroup;
-                sum += (uint32_t) (g & 0xFFFFFFFFu);
+                sum += (uint32_t) g;
             }
-            if (__all(ok))
-                return (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(sum), 63);
-            __builtin_amdgcn_s_sleep(1);
+            if (__all(ok)) return wave_sum(sum);
+            __builtin_amdgcn_s_sleep(2);
         }
     };
-    // Publish tile t's count: its status word and its group's sum.
-    auto publish = [&](uint32_t t, uint32_t agg) {
-        if (lane == 0) {
-            st_store(&w.fstatus[t], kStAgg | agg);
-            __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+
+    __syncthreads();  // the tables
+    if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
+    __syncthreads();
+    uint32_t tA = s_tile[0], bA = 0;
+    if (tA < ntiles) {
+        count_tile(tA, 0);
+        __syncthreads();
+        if (threadIdx.x == 0) publish(tA, 0);
+    }
+    bool owner = false;  // this block decoded the last tile
+    uint32_t Vs = 0;     // then: the suffix's alphabet characters
+    while (tA < ntiles) {
+        const uint32_t bB = bA ^ 1u;
+        if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
+        __syncthreads();  // also: s_cnt[bB] of two tiles back is consumed
+        const uint32_t tB = s_tile[bB];
+        if (tB < ntiles) count_tile(tB, bB);
+        __syncthreads();
+        if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
+        if (wv == 0) {
+            const uint32_t ex = tA ? prefix(tA) : 0u;
+            if (lane == 0) s_excl = ex;
         }
-    };
-    auto decode_tile = [&](uint32_t t, uint32_t B, uint32_t mine) {
-        const uint32_t rw = r0 + t * kFusePer;
+        __syncthreads();
+        uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
+        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
+        const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
+        // A whole range (2,048 characters from its aligned start) of a
+        // 16-byte aligned input is read ahead into LDS by two direct
+        // global->LDS copies (no VGPRs held) while the range before it
+        // decodes; the others (the first, from S; the stream's last) load
+        // as they decode.
+        auto whole = [&](uint32_t r) {
+            return kSfxDma && dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
+        };
+        auto fetch = [&](uint32_t r, uint32_t buf) {
+            const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
+            lds_dma16(src, &s_rng[wv][buf][0]);
+            lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
+        };
+        if (whole(rw)) fetch(rw, 0);
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
             const uint64_t rb = (uint64_t) r * R;
             const uint64_t re = rb + R < n ? rb + R : n;
             const bool first = r == r0, last = r + 1 == nranges;
             const uint64_t start = first ? S : rb;
-            uint4 c[2];
-            uint32_t nin[2], la;
-            bool la_ok;
-            load_range(in, n, start, re, last, c, nin, la, la_ok);
-            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
-                         base_out + (B + 3) / 4 * 3, c, nin, la, la_ok, last, hold);
-            B += (uint32_t) __builtin_amdgcn_readlane((int) mine, (int) j);
-        }
-    };
-
-    bool owner = false;  // this wave decoded the last tile
-    uint32_t Vs = 0;     // then: the suffix's alphabet characters
-#ifndef B64X_SFX_AHEAD  // A/B builds only: count the next tile before looking back
-#define B64X_SFX_AHEAD 1
-#endif
-    if (!B64X_SFX_AHEAD) {
-        for (;;) {
-            const uint32_t t = wave_draw(w.fticket);
-            if (t >= ntiles) break;
-            uint32_t m = 0;
-            const uint32_t ag = count_tile(t, m);
-            publish(t, ag);
-            const uint32_t ex = t ? look_back(t) : 0u;
-            decode_tile(t, ex, m);
-            if (t == ntiles - 1) {
-                owner = true;
-                Vs = ex + ag;
+            const bool next_dma = j + 1 < kFusePer && whole(r + 1);
+            uint4 *buf = s_rng[wv][j & 1];
+            uint32_t nin[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
             }
+            // Every range goes through the LDS buffer, so that one code path
+            // decodes them all: a joined path made the compiler wait for the
+            // register path's loads (vmcnt(0), draining the copy in flight)
+            // on the copied path too.  A whole range waits for its copy; any
+            // other is loaded here (and waited for) and written there.
+            if (whole(r)) {
+                vm_wait_all();
+            } else {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                    buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+                }
+            }
+            uint4 c[2];
+            c[0] = buf[lane];
+            c[1] = buf[64 + lane];
+            // then the next range's copy: in flight while this one decodes
+            // (no global load of the compiler's is outstanding from here on)
+            if (next_dma) fetch(r + 1, (j + 1) & 1);
+            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
+                         base_out + (B + 3) / 4 * 3, c, nin, 0u, !last, last, hold,
+                         next_dma ? (const uint8_t *) s_rng[wv][(j + 1) & 1] : nullptr, true);
+            B += s_cnt[bA][wv * kFusePer + j];
         }
-    }
-    uint32_t tA = B64X_SFX_AHEAD ? wave_draw(w.fticket) : ntiles, mA = 0, aA = 0;
-    if (tA < ntiles) {
-        aA = count_tile(tA, mA);
-        publish(tA, aA);
-    }
-    while (tA < ntiles) {
-        const uint32_t tB = wave_draw(w.fticket);
-        uint32_t mB = 0, aB = 0;
-        if (tB < ntiles) {
-            aB = count_tile(tB, mB);
-            publish(tB, aB);
-        }
-        const uint32_t ex = tA ? look_back(tA) : 0u;
-        decode_tile(tA, ex, mA);
         if (tA == ntiles - 1) {
             owner = true;
-            Vs = ex + aA;
+            Vs = s_excl;
+            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[bA][i];
         }
         tA = tB;
-        mA = mB;
-        aA = aB;
+        bA = bB;
     }
-    // every look-back and decode of this wave is over (relaxed: the look-back
-    // loads have returned -- their values decided the loop -- and a release
-    // at agent scope would write back the L2, once per wave)
-    if (lane == 0) __hip_atomic_fetch_add(wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!owner) return;
+    // every prefix read of this block is over (relaxed: the loads have
+    // returned -- their values decided the loop -- and a release at agent
+    // scope would write back the L2)
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!owner || wv != 0) return;
     const uint64_t V = Vb + Vs;
     if (lane == 0) write_result(res, hres, V, hold, n, seq);
     find_tail_sextets(sm.tab, in, n, V, res, hres);
     if (lane == 0) {
-        const uint32_t want = gridDim.x * kWavesPerBlock;
-        while (__hip_atomic_load(wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want)
+        while (__hip_atomic_load(w.wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
             __builtin_amdgcn_s_sleep(1);
     }
     for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
     for (uint32_t i = lane; i < (ntiles + kSfxGroup - 1) / kSfxGroup; i += 64) st_store(&w.fsuper[i], 0);
     if (lane == 0) {
         __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w.wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!WHOLE) {
             for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
             *w.fail_any = 0;
@@ -4170,18 +3962,13 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
         // of whatever suffix it could not take -- nothing, on clean and
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
-#ifndef B64X_SFX_WAVE  // A/B builds only: 1 = wave tiles with the count run ahead (k_decode_suffix_w)
-#define B64X_SFX_WAVE 0
-#endif
-        static const int occ_sfx = B64X_SFX_WAVE ? occupancy_of(k_decode_suffix_w<false>)
-                                                 : occupancy_of(k_decode_suffix<false>);
+        static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
 #ifndef B64X_SFX_OCC  // A/B builds only: blocks per CU of the suffix grid (0: occupancy)
 #define B64X_SFX_OCC 0
 #endif
         const uint32_t sfx_grid = (uint32_t) d->cus * (B64X_SFX_OCC ? B64X_SFX_OCC : occ_sfx);
         if (flags & B64X_DEC_EXPECT_JUNK) {
-            hipLaunchKernelGGL((B64X_SFX_WAVE ? k_decode_suffix_w<true> : k_decode_suffix<true>),
-                               dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq);
             return launch_status();
@@ -4194,8 +3981,7 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
                            dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
-        hipLaunchKernelGGL((B64X_SFX_WAVE ? k_decode_suffix_w<false> : k_decode_suffix<false>),
-                           dim3(sfx_grid), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                            hold, d_res, h_res, seq);
         return launch_status();
