@@ -919,6 +919,7 @@ constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 #endif
 constexpr uint32_t kFusePer = B64X_FUSE_PER;  // ranges per wave in the single-pass decode
 constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
+static_assert(kFuseLoad % 2 == 0, "counts are reduced two ranges at a time");
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
@@ -1421,15 +1422,19 @@ DEV void build_compact_sel(uint32_t *sel)
 DEV uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
 
 // OR a left-aligned field (bits 23..24-w of F; the rest zero) into the
-// big-endian bit stream held little-endian-per-byte in `bits` (dwords), its
-// first bit at stream bit p.
+// big-endian bit stream held in `bits` (dwords), its first bit at stream
+// bit p.  BE: the dwords hold the stream big-endian (the reader swaps each
+// dword once when it stores: decode_range's 16-byte blocks), else
+// little-endian per byte, the output bytes as they are (decode_buf_bits).
+template <bool BE = false>
 DEV void or_field(uint32_t *bits, uint32_t p, uint32_t F)
 {
-    const uint32_t k = p >> 5, o = p & 31u;
+    const uint32_t o = p & 31u;
     const uint64_t W = (uint64_t) F << (40u - o);
-    __hip_atomic_fetch_or(bits + k, bswap32((uint32_t) (W >> 32)), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_or(bits + k + 1, bswap32((uint32_t) W), __ATOMIC_RELAXED,
+    uint32_t *q = (uint32_t *) ((uint8_t *) bits + ((p >> 3) & ~3u));
+    const uint32_t hi = (uint32_t) (W >> 32), lo = (uint32_t) W;
+    __hip_atomic_fetch_or(q, BE ? hi : bswap32(hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(q + 1, BE ? lo : bswap32(lo), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
@@ -1478,7 +1483,8 @@ DEV void store_bits(const uint32_t *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
         if (from + i < to) dst0[from + i] = bb[from + i];
 }
 
-// Copy LDS bytes [lo, hi) of a wave's window `b` to dst0 + [lo, hi), where
+// Copy stream bytes [lo, hi) of a wave's big-endian window `b` (or_field<true>)
+// to dst0 + [lo, hi), where
 // dst0 = the output address of LDS byte 0, 16-byte aligned: the whole
 // 16-byte blocks as aligned ds_read_b128 / dwordx4 non-temporal pairs (lane
 // k takes block klo + k, conflict-free), the head and tail bytes of the
@@ -1488,8 +1494,9 @@ DEV void store_bits16(const uint4 *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
     const uint32_t lane = lane_id();
     const uint32_t klo = (lo + 15) >> 4, khi = hi >> 4;  // whole blocks [klo, khi)
     for (uint32_t k = klo + lane; k < khi; k += 64) {
-        const uint4 v = b[k];
-        __builtin_nontemporal_store(u32x4a16{v.x, v.y, v.z, v.w}, (u32x4a16 *) (dst0 + 16 * (uint64_t) k));
+        const uint4 v = b[k];  // big-endian dwords (or_field<true>)
+        __builtin_nontemporal_store(u32x4a16{bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)},
+                                    (u32x4a16 *) (dst0 + 16 * (uint64_t) k));
     }
     const uint32_t hend = 16 * klo < hi ? 16 * klo : hi;  // head bytes [lo, hend)
     uint32_t i = 0;
@@ -1501,7 +1508,7 @@ DEV void store_bits16(const uint4 *b, uint32_t lo, uint32_t hi, uint8_t *dst0)
         i = 16 * khi + (lane - 16);  // tail bytes [max(16 khi, hend), hi)
         act = i < hi && i >= hend;
     }
-    if (act) dst0[i] = ((const uint8_t *) b)[i];
+    if (act) dst0[i] = ((const uint8_t *) b)[i ^ 3u];
 }
 
 // Inclusive prefix sum over the wave with DPP (row shifts, then the two
@@ -1523,6 +1530,7 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
 // sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
 // up to 18 bits past the window's byte 4: skipped sextets land in its
 // head).  Returns the step's alphabet characters.
+template <bool BE = false>
 DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
@@ -1555,7 +1563,7 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
-            or_field(bits, p, group_dot(D));  // absent sextets are zero bytes
+            or_field<BE>(bits, p, group_dot(D));  // absent sextets are zero bytes
             p += 24u - six[h][g];
         }
     }
@@ -2179,7 +2187,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     // the first step from the chunks given (its own code: joined with the
     // loads of the later steps, the compiler waited for every load in
     // flight before the step, ranges read ahead included)
-    T += (int) bits_step(sm, bits, c, nin, pb0 + 6 * T);
+    T += (int) bits_step<true>(sm, bits, c, nin, pb0 + 6 * T);
     for (uint64_t pos = start + 2 * kChunk; pos < re; pos += 2 * kChunk) {
         // more of this range: flush the window's whole blocks and carry the
         // partial one to the front
@@ -2207,7 +2215,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
             nh[h] = q >= re ? 0u : (re - q >= 16 ? 16u : (uint32_t) (re - q));
             ch[h] = nh[h] ? load_chars(in + q, nh[h]) : make_uint4(0, 0, 0, 0);
         }
-        T += (int) bits_step(sm, bits, ch, nh, pb0 + 6 * T);
+        T += (int) bits_step<true>(sm, bits, ch, nh, pb0 + 6 * T);
     }
     bool at_end = last;
     if (!last && T > 0 && (T & 3)) {
@@ -2229,7 +2237,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
                 (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
             const int need = 4 - (T & 3);
             if (v && (int) rank < need)
-                or_field(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
+                or_field<true>(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
             const int got = __popcll(m);
             if (got >= need) {
                 T += need;
@@ -2479,17 +2487,26 @@ void k_decode_suffix(
                     c[jj][h] = nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
                 }
             }
+            // two ranges' counts (each <= 2,048) share one packed DPP scan
+            // (a shuffle reduction per range cost 25 VALU and 6 LDS ops)
 #pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
                 uint32_t cnt = 0;
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    uint32_t P[4];
-                    lane_values(sm.tab, c[jj][h], nin[jj][h], P);
-                    cnt += lane_valid_count(P);
+                for (uint32_t e = 0; e < 2; e++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        uint32_t P[4];
+                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
+                        cnt += lane_valid_count(P) << (16 * e);
+                    }
                 }
-                cnt = wave_sum(cnt);
-                if (lane == 0) s_cnt[b][wv * kFusePer + j0 + jj] = cnt;
+                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
+                    (int) wave_incl_scan_dpp(cnt), 63);
+                if (lane == 0) {
+                    s_cnt[b][wv * kFusePer + j0 + jj] = tot & 0xFFFFu;
+                    s_cnt[b][wv * kFusePer + j0 + jj + 1] = tot >> 16;
+                }
             }
         }
     };
@@ -2570,12 +2587,7 @@ void k_decode_suffix(
             const uint64_t start = first ? S : rb;
             const bool next_dma = j + 1 < kFusePer && whole(r + 1);
             uint4 *buf = s_rng[wv][j & 1];
-            uint32_t nin[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-                nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-            }
+            uint32_t nin[2] = {16u, 16u};
             // Every range goes through the LDS buffer, so that one code path
             // decodes them all: a joined path made the compiler wait for the
             // register path's loads (vmcnt(0), draining the copy in flight)
@@ -2587,6 +2599,7 @@ void k_decode_suffix(
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
                     buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
                 }
             }

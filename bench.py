@@ -25,7 +25,8 @@ Also reported on the same JSON line:
                 one exchange step (allgather of per-rank output totals);
                 whole-job and per-rank GiB/s and roofline fractions;
   mime_decode   MIME-formatted (CRLF-76) decode of config 2's characters and
-                config 4's rows, bit-checked (rank 0 at N=1);
+                config 4's rows, and config 2's characters with unstructured
+                junk at densities 0.001 and 0.05, bit-checked (rank 0 at N=1);
   cfg5_egress   BASELINE config 5 through the product's stage stack, host
                 memory in and out, 1 and 16 loops, with the oracle's stack
                 timed beside it (rank 0 at N=1; skipped with --no-cpu);
@@ -475,7 +476,33 @@ def bench_mime(args, b64, steps=10):
               "ms": ms, "GiB_s": N / (ms * 1e-3) / 2**30,
               "alg_GBps": alg / (ms * 1e-3) / 1e9,
               "roofline_frac": alg / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9)}
-    del x, text, out, ws
+    del text, out, ws
+    # unstructured junk (not a BASELINE workload; the verdict's sparse and
+    # 5 % cases): a '!' before each character with probability d
+    junk = {}
+    chars = b64.encode(x)
+    for d in (0.001, 0.05):
+        g = torch.Generator(device="cuda").manual_seed(7)
+        mask = torch.rand(chars.numel(), device="cuda", generator=g) < d
+        idx = torch.arange(chars.numel(), device="cuda") + torch.cumsum(mask, 0)
+        text = torch.full((chars.numel() + int(mask.sum()),), ord("!"), dtype=torch.uint8,
+                          device="cuda")
+        text[idx] = chars
+        del mask, idx
+        out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device="cuda")
+        ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device="cuda")
+        ms_j = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream))
+        info = b64.Decoded(out, res).info()
+        if info.out_len != N or not torch.equal(out[:N], x):
+            raise SystemExit(f"junk {d} decode mismatch")
+        alg_j = text.numel() + N
+        junk[f"cfg2_junk{d:g}"] = {
+            "workload": f"cfg2 characters with junk density {d:g}: {text.numel()} bytes -> {N}",
+            "ms": ms_j, "GiB_s": N / (ms_j * 1e-3) / 2**30,
+            "alg_GBps": alg_j / (ms_j * 1e-3) / 1e9,
+            "roofline_frac": alg_j / (ms_j * 1e-3) / (HBM_PEAK_GBS * 1e9)}
+        del text, out, ws
+    del x, chars
     # config 4's rows, each in CRLF-76 lines (1,368 characters -> 18 lines)
     nbuf, L = 1 << 20, 1024
     E = b64.encoded_len(L)
@@ -504,7 +531,7 @@ def bench_mime(args, b64, steps=10):
              "ms": ms4, "GiB_s": nbuf * L / (ms4 * 1e-3) / 2**30,
              "alg_GBps": alg4 / (ms4 * 1e-3) / 1e9,
              "roofline_frac": alg4 / (ms4 * 1e-3) / (HBM_PEAK_GBS * 1e9)}
-    return {"cfg2_crlf76": single, "cfg4_crlf76": batch, "unit": "ms, GiB/s payload"}
+    return {"cfg2_crlf76": single, "cfg4_crlf76": batch, **junk, "unit": "ms, GiB/s payload"}
 
 
 def bench_cfg5(args, world=1, rank=0):
