@@ -915,9 +915,14 @@ struct DecodeWs {
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 #ifndef B64X_FUSE_PER  // A/B builds only
-#define B64X_FUSE_PER 16
+#define B64X_FUSE_PER 8
 #endif
-constexpr uint32_t kFusePer = B64X_FUSE_PER;  // ranges per wave in the single-pass decode
+// ranges per wave tile in the single-pass decode: with the group-sum prefix
+// and the count run one tile ahead, small tiles win (1 GiB at junk density
+// 0.05, single pass: 2: 1,195 us, 4: 758, 8: 766, 16: 841, 32: 885;
+// profiles/r03_ab_sfx_tiles*.jsonl); 8 keeps the ticket atomics at half of 4's
+// (round 2's chained look-back was best at 16)
+constexpr uint32_t kFusePer = B64X_FUSE_PER;
 constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
 static_assert(kFuseLoad % 2 == 0, "counts are reduced two ranges at a time");
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
@@ -1809,7 +1814,10 @@ DEV bool sep_ok_s(const uint8_t *tab, uint32_t sep, uint32_t s)
 // matters for the result (k_decode_lines takes slots [0, T) exactly or
 // publishes their failure; k_decode_suffix takes the rest), only for speed.
 constexpr uint32_t kProbeThreads = 256;
-constexpr uint64_t kProbeSampleMin = 1u << 18;  // shorter streams: the first window only
+#ifndef B64X_PROBE_SAMPLES  // A/B builds only: 0 = the first window only
+#define B64X_PROBE_SAMPLES 1
+#endif
+constexpr uint64_t kProbeSampleMin = B64X_PROBE_SAMPLES ? 1u << 18 : ~0ull;  // shorter streams: the first window only
 constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
 
 __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
