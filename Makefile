@@ -19,8 +19,12 @@ ARCH     ?= gfx950
 # -Wno-pass-failed: k_encode_flat's `#pragma unroll` loops (compile-time trip
 # counts) are reported "not unrolled" after they have already been fully
 # unrolled by an earlier pass; the ISA is the unrolled one.
+# -amdgpu-kernarg-preload-count: the first 16 dwords of kernel arguments
+# arrive in SGPRs, so a wave's first address needs no kernarg load (encode
+# -2 us, CRLF-76 decode -2.5 us per 1 GiB in A/B; the code object keeps the
+# loading prologue for firmware without preload).
 HIPFLAGS  = --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -Iasync_amd/csrc \
-            -Wall -Wno-pass-failed -Iinclude
+            -Wall -Wno-pass-failed -Iinclude -mllvm -amdgpu-kernarg-preload-count=16
 CFLAGS    = -O2 -std=c11 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude
 
 LIB      = async_amd/libasync_b64.so

@@ -12,10 +12,9 @@
 //
 // How it runs here (DESIGN.md §5 has the byte budget and the rooflines):
 //   * encode is stateless per 3-byte group.  One lane turns 12 input bytes
-//     (one dwordx3 load) into 16 characters (one dwordx4 store); the
-//     64-entry alphabet is held one character per lane and read across
-//     lanes with ds_bpermute (k_encode_flat; the batch kernels keep it in
-//     LDS and read it with ds_read_u8).  Byte
+//     (one dwordx3 load) into 16 characters (one dwordx4 store), one quad
+//     per lane; the 64-entry alphabet sits in LDS and is read with
+//     ds_read_u8 (k_encode_flat and the batch kernels).  Byte
 //     regrouping is v_perm_b32, not shifts (k_encode_flat; batches:
 //     k_encode_tight2, k_encode_strided, k_encode_ragged).
 //   * decode is stateful only through the number of alphabet characters
@@ -424,11 +423,13 @@ DEV u32x3a4 ld12(const uint8_t *p)
 // and stores are non-temporal.  Launched with one block per tile (a
 // non-persistent grid streams fastest here: tests/tools/copy_sweep.hip; the
 // loop only matters past 2^31 tiles).  The last, partial tile and the final
-// n mod 12 bytes (with padding) are done by the last block.  Round 1's A/B
-// of tile depth (1-8 quads), software pipelining and cached loads picked
-// this form (profiles/r01_v6_*).
+// n mod 12 bytes (with padding) are done by the last block.  One quad per
+// lane with the LDS table (round 3, profiles/r03_ab_enc*.jsonl: 406 -> 397
+// us per 1 GiB; the copy with encode's 12 -> 16 mix is also fastest at one
+// load per lane); round 1's A/B of software pipelining and cached loads
+// still holds (profiles/r01_v6_*).
 #ifndef B64X_FLAT_U  // A/B builds only (scripts/ab_variants.sh)
-#define B64X_FLAT_U 2
+#define B64X_FLAT_U 1
 #endif
 constexpr int kFlatU = B64X_FLAT_U;
 #ifndef B64X_ENC_NTL  // A/B builds only: non-temporal loads / stores
@@ -438,31 +439,75 @@ constexpr int kFlatU = B64X_FLAT_U;
 #define B64X_ENC_NTS true
 #endif
 
-__global__ __launch_bounds__(kThreads) void k_encode_flat(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, EncAlpha a)
+// The per-lane alphabet character of enc_quad_bp (lane v: sextet v's),
+// branch-free: the ternary chain of enc_char compiled to three nested
+// exec-masked branches, each waiting on the kernel arguments, ahead of
+// the first load.
+DEV uint32_t enc_lane_char(uint32_t v, uint32_t p62, uint32_t p63)
 {
+    // 'A' + v, + 6 past 'Z' (v > 25), - 75 past 'z' (v > 51): v in [0, 64)
+    uint32_t c = v + 65 + 6 * ((v + 230) >> 8) - 75 * ((v + 204) >> 8);
+    c = v == 62 ? p62 : c;
+    return v == 63 ? p63 : c;
+}
+
+// A/B builds only (scripts/ab_variants.sh): block size, a wave's quads
+// contiguous instead of a block's, an LDS alphabet table, and a pricing
+// form that stores the loaded bytes instead of encoding them (wrong output)
+#ifndef B64X_ENC_TH
+#define B64X_ENC_TH 256
+#endif
+#ifndef B64X_ENC_WS
+#define B64X_ENC_WS 0
+#endif
+#ifndef B64X_ENC_LDS
+#define B64X_ENC_LDS 1
+#endif
+#ifndef B64X_ENC_PRICE
+#define B64X_ENC_PRICE 0
+#endif
+constexpr uint32_t kEncTH = B64X_ENC_TH;
+
+__global__ __launch_bounds__(kEncTH) void k_encode_flat(
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t full, uint64_t n,
+    EncAlpha a)
+{
+    // `full` (the whole tiles of kFlatU quads per lane) comes from the host,
+    // so a wave issues its loads without a 64-bit division by 12 first.
     __shared__ uint8_t tab[64];
-    const uint64_t nq = n / 12;
-    const uint64_t tile = (uint64_t) kThreads * kFlatU;
-    const uint64_t full = nq / tile;
+    const uint64_t tile = (uint64_t) kEncTH * kFlatU;
     const uint32_t tid = threadIdx.x;
-    // the alphabet one character per lane, read across lanes (enc_quad_bp):
-    // no LDS table and no block barrier before the first load (1 % faster)
-    const uint32_t lc = (uint32_t) enc_char(threadIdx.x & 63u, a);
-    for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
-        u32x3a4 cur[kFlatU];
-        const uint8_t *src = in + (t * tile + tid) * 12;
-#pragma unroll
-        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<B64X_ENC_NTL>(src + u * kThreads * 12);
-        uint8_t *dst = out + (t * tile + tid) * 16;
-#pragma unroll
-        for (int u = 0; u < kFlatU; u++)
-            store16<B64X_ENC_NTS>(dst + u * kThreads * 16, enc_quad_bp(lc, cur[u].x, cur[u].y, cur[u].z));
-    }
-    if (blockIdx.x == gridDim.x - 1) {
+    // the lane's first quad in its tile and the step between its quads
+    const uint32_t q0 = B64X_ENC_WS ? (tid & ~63u) * kFlatU + (tid & 63u) : tid;
+    constexpr uint32_t qs = B64X_ENC_WS ? 64u : kEncTH;
+    if (B64X_ENC_LDS) {
         build_enc_table(tab, a);
         __syncthreads();
-        for (uint64_t q = full * tile + tid; q < nq; q += kThreads) {
+    }
+    for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
+        u32x3a4 cur[kFlatU];
+        const uint8_t *src = in + (t * tile + q0) * 12;
+#pragma unroll
+        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<B64X_ENC_NTL>(src + u * qs * 12);
+        // B64X_ENC_LDS = 0: the alphabet one character per lane, read across
+        // lanes (enc_quad_bp, round 2's form): no LDS table and no barrier,
+        // but 16 cross-lane permutes per quad (445 vs 397 us at one quad
+        // per lane, profiles/r03_ab_enc2.jsonl)
+        const uint32_t lc = enc_lane_char(tid & 63u, a.p62, a.p63);
+        uint8_t *dst = out + (t * tile + q0) * 16;
+#pragma unroll
+        for (int u = 0; u < kFlatU; u++) {
+            const uint4 o = B64X_ENC_PRICE ? make_uint4(cur[u].x, cur[u].y, cur[u].z, cur[u].x ^ cur[u].z)
+                          : B64X_ENC_LDS   ? enc_quad(tab, cur[u].x, cur[u].y, cur[u].z)
+                                           : enc_quad_bp(lc, cur[u].x, cur[u].y, cur[u].z);
+            store16<B64X_ENC_NTS>(dst + u * qs * 16, o);
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        const uint64_t nq = n / 12;
+        build_enc_table(tab, a);
+        __syncthreads();
+        for (uint64_t q = full * tile + tid; q < nq; q += kEncTH) {
             const u32x3a4 v = *(const u32x3a4 *) (in + q * 12);
             store16<true>(out + q * 16, enc_quad(tab, v.x, v.y, v.z));
         }
@@ -653,6 +698,20 @@ DEV void wave_lds_order()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The 256-entry decode table in the wave's own LDS slice (one dword of four
+// entries per lane): no block barrier, so a wave never waits for the
+// block's other waves before its lookups.
+[[maybe_unused]] DEV const uint8_t *wave_dec_table(uint32_t *slice, const DecAlpha &a)
+{
+    const uint32_t l = lane_id();
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) v |= dec_value(4 * l + j, a) << (8 * j);
+    slice[l] = v;
+    wave_lds_order();
+    return (const uint8_t *) slice;
 }
 
 // Four groups -> 12 output bytes as three little-endian dwords.
@@ -1923,17 +1982,25 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
 #ifndef B64X_LINES_WPE  // A/B builds only: minimum waves per SIMD
 #define B64X_LINES_WPE 6
 #endif
+#ifndef B64X_LINES_WTAB  // A/B builds only: 1 = each wave builds its own table, no block barrier
+#define B64X_LINES_WTAB 0
+#endif
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, uint32_t seq)
 {
+#if B64X_LINES_WTAB
+    __shared__ uint32_t tabw[kWavesPerBlock][64];
+#else
     __shared__ uint8_t tab[256];
+#endif
     __shared__ uint8_t s_tail[64];
     // the scalar loads of the model overlap the table build
     const uint64_t *mp = (const uint64_t *) ws_view(ws, nranges).model;
     const uint64_t mw0 = scalar_load_u64(mp), mw1 = scalar_load_u64(mp + 1),
                    mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
+#if !B64X_LINES_WTAB
     build_dec_table(tab, a);
     // a block wholly past slot T (the probe cut the model's slots at junk)
     // leaves before the barrier: on junk-laden input nearly every block of
@@ -1941,6 +2008,7 @@ void k_decode_lines(
     // no longer overlapped the build: MIME text +2 %.)
     if (blockIdx.x * kWavesPerBlock * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
     __syncthreads();
+#endif
     LineModel m;
     m.L = (uint32_t) mw0;
     m.s = (uint32_t) (mw0 >> 32);
@@ -1958,6 +2026,9 @@ void k_decode_lines(
     const uint32_t wv = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
     const uint32_t t0 = (blockIdx.x * kWavesPerBlock + wv) * kLinesSlots;
     if (t0 > T) return;
+#if B64X_LINES_WTAB
+    const uint8_t *tab = wave_dec_table(tabw[wv], a);
+#endif
     const uint32_t ns = T - t0 >= kLinesSlots ? kLinesSlots : T - t0;  // interior slots here
     const bool full = ns == kLinesSlots;
     const bool oal = (((uintptr_t) out) & 3) == 0;
@@ -1984,7 +2055,16 @@ void k_decode_lines(
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
             uint32_t G[4], bad;
-            map_fast(tab, c[u], 16, G, bad);
+#ifndef B64X_LINES_PRICE  // A/B builds only: store the loaded bytes (wrong output)
+#define B64X_LINES_PRICE 0
+#endif
+            if (B64X_LINES_PRICE) {
+                G[0] = c[u].x & 0xFFFFFFu, G[1] = c[u].y & 0xFFFFFFu;
+                G[2] = c[u].z & 0xFFFFFFu, G[3] = c[u].w & 0xFFFFFFu;
+                bad = 0;
+            } else {
+                map_fast(tab, c[u], 16, G, bad);
+            }
             const uint64_t fb = __ballot(bad != 0);
             if (fb && fail_u == kLinesU) {
                 fail_u = u;
@@ -3785,10 +3865,10 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
     if (((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 3) == 0) {
-        const uint64_t tiles = n / 12 / ((uint64_t) kThreads * kFlatU);
+        const uint64_t tiles = n / 12 / ((uint64_t) kEncTH * kFlatU);
         hipLaunchKernelGGL(k_encode_flat, dim3(cap_grid(tiles, (uint64_t) 1 << 31)),
-                           dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in, n,
-                           (uint8_t *) d_out, enc_alpha(abc));
+                           dim3(kEncTH), 0, (hipStream_t) stream, (const uint8_t *) d_in,
+                           (uint8_t *) d_out, tiles, n, enc_alpha(abc));
         return launch_status();
     }
     // Misaligned buffers: the generic slot kernel (bytewise where needed).
@@ -3816,7 +3896,10 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (slots > 0xFFFFFFFFull - 4096) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-    constexpr int U = 2;
+#ifndef B64X_TIGHT_U  // A/B builds only: output slots per lane of k_encode_tight2
+#define B64X_TIGHT_U 2
+#endif
+    constexpr int U = B64X_TIGHT_U;
     const EncAlpha ea = enc_alpha(abc);
     const uint64_t E = b64x_encoded_len(len, ea.pad);
     const uint32_t r = (uint32_t) (len % 3);
@@ -3841,8 +3924,9 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
         }
     }
     // Any other layout: one lane per (buffer, quad).
-    const uint64_t per_block = (uint64_t) kThreads * U;
-    hipLaunchKernelGGL((k_encode_strided<U, true>), dim3((uint32_t) ((slots + per_block - 1) / per_block)),
+    constexpr int US = 2;
+    const uint64_t per_block = (uint64_t) kThreads * US;
+    hipLaunchKernelGGL((k_encode_strided<US, true>), dim3((uint32_t) ((slots + per_block - 1) / per_block)),
                        dim3(kThreads), 0, (hipStream_t) stream, (const uint8_t *) d_in,
                        in_stride, len, nbuf, (uint8_t *) d_out, out_stride, (uint32_t) qpb,
                        (uint32_t) slots, enc_alpha(abc));

@@ -52,6 +52,19 @@ def child(lib, steps, only=()):
             ts.append(a.elapsed_time(b) * 1e3)
         res[name] = (statistics.median(ts), statistics.mean(ts), min(ts))
 
+    # the copy ceiling beside the kernels, same process and box: one 16-byte
+    # (or 12-byte) non-temporal load and store per lane with the leg's own
+    # read/write mix (tests/csrc/libb64x_hooks.so, bench.py copy_ceilings)
+    import ctypes
+    hooks = ctypes.CDLL(os.path.join(ROOT, "tests", "csrc", "libb64x_hooks.so"))
+    hooks.b64x__test_copy_mix.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    st = torch.cuda.current_stream().cuda_stream
+    ue, ud = n // 12 // 256 * 256, enc.numel() // 16 // 256 * 256
+    timeit("copy_enc", lambda: hooks.b64x__test_copy_mix(x.data_ptr(), enc.data_ptr(), ue, st,
+                                                         0, 0))
+    timeit("copy_dec", lambda: hooks.b64x__test_copy_mix(enc.data_ptr(), out.data_ptr(), ud, st,
+                                                         1, 0))
     timeit("encode", lambda: b64.encode(x, out=enc))
     timeit("decode", lambda: b64.decode(enc, out=out, workspace=ws, result=rr))
     ok = torch.equal(out[:n], x)
@@ -148,7 +161,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("encode", "decode", "crlf", "junk", "junk1", "junk_ej", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
+            for k in ("copy_enc", "copy_dec", "encode", "decode", "crlf", "junk", "junk1", "junk_ej", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
