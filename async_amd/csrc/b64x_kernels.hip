@@ -1418,18 +1418,72 @@ DEV uint64_t scalar_load_u64(const uint64_t *p)
     return *(const __attribute__((address_space(4))) uint64_t *) p;
 }
 
+// tab_pack4 of a slot's four dwords: each byte's LDS address is the table's
+// base (a constant the backend folds, 0 in the kernels that use this) plus
+// the byte -- one v_and / v_bfe / v_lshr; bytes
+// 0 and 1 of a dword load into two registers and bytes 2 and 3 into their
+// high halves (ds_read_u8_d16_hi keeps the low half), so one shift-or packs
+// the dword -- 1 VALU per dword after the loads instead of 3.  The 16 loads
+// are issued together and waited for once.
+DEV void tab_pack16_d16(const uint8_t *tab, const uint32_t dw[4], uint32_t P[4])
+{
+    const uint32_t base =
+        (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint8_t *) tab;
+    uint32_t a[16];
+#pragma unroll
+    for (int g = 0; g < 4; g++)
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) a[4 * g + k] = base + ((dw[g] >> (8 * k)) & 0xFFu);
+    uint32_t lo0, hi0, lo1, hi1, lo2, hi2, lo3, hi3;
+    asm volatile(
+        "ds_read_u8 %0, %8\n\t"
+        "ds_read_u8 %1, %9\n\t"
+        "ds_read_u8 %2, %12\n\t"
+        "ds_read_u8 %3, %13\n\t"
+        "ds_read_u8 %4, %16\n\t"
+        "ds_read_u8 %5, %17\n\t"
+        "ds_read_u8 %6, %20\n\t"
+        "ds_read_u8 %7, %21\n\t"
+        "ds_read_u8_d16_hi %0, %10\n\t"
+        "ds_read_u8_d16_hi %1, %11\n\t"
+        "ds_read_u8_d16_hi %2, %14\n\t"
+        "ds_read_u8_d16_hi %3, %15\n\t"
+        "ds_read_u8_d16_hi %4, %18\n\t"
+        "ds_read_u8_d16_hi %5, %19\n\t"
+        "ds_read_u8_d16_hi %6, %22\n\t"
+        "ds_read_u8_d16_hi %7, %23\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(lo0), "=&v"(hi0), "=&v"(lo1), "=&v"(hi1), "=&v"(lo2), "=&v"(hi2), "=&v"(lo3),
+          "=&v"(hi3)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+          "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]),
+          "v"(a[15])
+        : "memory");
+    P[0] = lo0 | (hi0 << 8);
+    P[1] = lo1 | (hi1 << 8);
+    P[2] = lo2 | (hi2 << 8);
+    P[3] = lo3 | (hi3 << 8);
+}
+
 // The 16 table values of a lane's characters, packed 4 per dword; the
 // characters at and past `nin` read as non-alphabet.
+#ifndef B64X_LV_D16  // A/B builds only: lane_values by tab_pack16_d16
+#define B64X_LV_D16 0
+#endif
 DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
 {
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
+    if (B64X_LV_D16) {
+        tab_pack16_d16(tab, dw, P);  // the table is P2dSmem's, 256-byte aligned
+    } else {
 #pragma unroll
-    for (uint32_t g = 0; g < 4; g++) {
-        const uint32_t t0 = tab[dw[g] & 0xFFu];
-        const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
-        const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
-        const uint32_t t3 = tab[dw[g] >> 24];
-        P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
+        for (uint32_t g = 0; g < 4; g++) {
+            const uint32_t t0 = tab[dw[g] & 0xFFu];
+            const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
+            const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
+            const uint32_t t3 = tab[dw[g] >> 24];
+            P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
+        }
     }
     if (nin < 16) {
 #pragma unroll
@@ -1462,8 +1516,8 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
 constexpr uint32_t kP2dBytes = 16 + 15 + kP2Range / 4 * 3 + 16;
 constexpr uint32_t kP2dBlocks = (kP2dBytes + 15) / 16;                  // uint4 per wave
 
-struct __attribute__((aligned(16))) P2dSmem {
-    uint8_t tab[256];
+struct __attribute__((aligned(256))) P2dSmem {
+    uint8_t tab[256];  // 256-byte aligned: tab_pack16_d16
     uint32_t sel[16];
     uint4 bits[kWavesPerBlock][kP2dBlocks];
 };
@@ -3194,7 +3248,7 @@ void k_decode_rows_lines(
     uint8_t *__restrict__ out, uint64_t out_stride, uint32_t S, uint32_t magic, uint64_t m64,
     uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws)
 {
-    __shared__ uint8_t tab[256];
+    __shared__ __attribute__((aligned(256))) uint8_t tab[256];  // tab_pack16_d16
     const uint64_t *rmw = (const uint64_t *) row_model(ws);
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
@@ -3295,9 +3349,18 @@ void k_decode_rows_lines(
                 const uint4 d = slot_chars4(w6, oo[u], c >> 2, rm.s, &sep);
                 const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
                 uint32_t G[4], m128 = 0;
+#ifndef B64X_ROWS_PRICE  // A/B builds only: no lookups (wrong output)
+#define B64X_ROWS_PRICE 0
+#endif
+#ifndef B64X_ROWS_D16  // A/B builds only: tab_pack16_d16 instead of tab_pack4
+#define B64X_ROWS_D16 0
+#endif
+                uint32_t PP[4];
+                if (B64X_ROWS_D16) tab_pack16_d16(tab, dw, PP);
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const uint32_t P = tab_pack4(tab, dw[g]);
+                    const uint32_t P = B64X_ROWS_PRICE ? dw[g] & 0x3F3F3F3Fu
+                                     : B64X_ROWS_D16   ? PP[g] : tab_pack4(tab, dw[g]);
                     const uint32_t Pz = P & 0x3F3F3F3Fu;
                     G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
                            __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);

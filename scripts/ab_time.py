@@ -66,20 +66,21 @@ def child(lib, steps, only=()):
     timeit("copy_dec", lambda: hooks.b64x__test_copy_mix(enc.data_ptr(), out.data_ptr(), ud, st,
                                                          1, 0))
     timeit("encode", lambda: b64.encode(x, out=enc))
+    ran = lambda k: not only or k in only  # noqa: E731 -- checks only for legs that ran
     timeit("decode", lambda: b64.decode(enc, out=out, workspace=ws, result=rr))
-    ok = torch.equal(out[:n], x)
+    ok = not ran("decode") or torch.equal(out[:n], x)
     timeit("crlf", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr))
-    ok = ok and torch.equal(out[:n], x)
+    ok = ok and (not ran("crlf") or torch.equal(out[:n], x))
     timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
-    ok = ok and torch.equal(out[:n], x)
+    ok = ok and (not ran("junk") or torch.equal(out[:n], x))
     timeit("junk1", lambda: b64.decode(junk1, out=out, workspace=ws, result=rr))
-    ok = ok and torch.equal(out[:n], x)
+    ok = ok and (not ran("junk1") or torch.equal(out[:n], x))
     timeit("junk_ej", lambda: b64.decode(junk, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
-    ok = ok and torch.equal(out[:n], x)
+    ok = ok and (not ran("junk_ej") or torch.equal(out[:n], x))
     timeit("crlf_ej", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
-    ok = ok and torch.equal(out[:n], x)
+    ok = ok and (not ran("crlf_ej") or torch.equal(out[:n], x))
     # config 4: 1 M x 1 KiB rows, strided decode (clean)
     del dirty, junk, junk1, enc, out, x
     if only and not ({"rows_enc", "rows_dec", "rows_crlf", "ragged_dec"} & set(only)):
@@ -95,9 +96,11 @@ def child(lib, steps, only=()):
     eb = torch.empty(nb * Es, dtype=torch.uint8, device="cuda")
     db = torch.empty(nb * cap, dtype=torch.uint8, device="cuda")
     ol = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    b64.encode_strided(xb, L, L, nb, eb, Es)  # the rows the decode legs read
     timeit("rows_enc", lambda: b64.encode_strided(xb, L, L, nb, eb, Es))
     timeit("rows_dec", lambda: b64.decode_strided(eb, Es, Es, nb, db, cap, ol))
-    ok = ok and bool((ol == L).all()) and torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L))
+    ok = ok and (not ran("rows_dec") or (bool((ol == L).all()) and
+                                         torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L))))
     # the same rows MIME-formatted (76-character lines, CRLF)
     lines = (Es + 75) // 76
     rows = eb.view(nb, Es)
@@ -111,7 +114,8 @@ def child(lib, steps, only=()):
     cap2 = 12 * ((D + 15) // 16)
     db2 = torch.empty(nb * cap2, dtype=torch.uint8, device="cuda")
     timeit("rows_crlf", lambda: b64.decode_strided(mb, D, D, nb, db2, cap2, ol))
-    ok = ok and bool((ol == L).all()) and torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L))
+    ok = ok and (not ran("rows_crlf") or (bool((ol == L).all()) and
+                                          torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L))))
     # a ragged batch of 65,536 messages of 100-4,000 bytes (the hub's shape)
     del mb, db2, db, eb, xb
     g = torch.Generator().manual_seed(5)
