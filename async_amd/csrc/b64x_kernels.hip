@@ -1418,72 +1418,16 @@ DEV uint64_t scalar_load_u64(const uint64_t *p)
     return *(const __attribute__((address_space(4))) uint64_t *) p;
 }
 
-// tab_pack4 of a slot's four dwords: each byte's LDS address is the table's
-// base (a constant the backend folds, 0 in the kernels that use this) plus
-// the byte -- one v_and / v_bfe / v_lshr; bytes
-// 0 and 1 of a dword load into two registers and bytes 2 and 3 into their
-// high halves (ds_read_u8_d16_hi keeps the low half), so one shift-or packs
-// the dword -- 1 VALU per dword after the loads instead of 3.  The 16 loads
-// are issued together and waited for once.
-DEV void tab_pack16_d16(const uint8_t *tab, const uint32_t dw[4], uint32_t P[4])
-{
-    const uint32_t base =
-        (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint8_t *) tab;
-    uint32_t a[16];
-#pragma unroll
-    for (int g = 0; g < 4; g++)
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) a[4 * g + k] = base + ((dw[g] >> (8 * k)) & 0xFFu);
-    uint32_t lo0, hi0, lo1, hi1, lo2, hi2, lo3, hi3;
-    asm volatile(
-        "ds_read_u8 %0, %8\n\t"
-        "ds_read_u8 %1, %9\n\t"
-        "ds_read_u8 %2, %12\n\t"
-        "ds_read_u8 %3, %13\n\t"
-        "ds_read_u8 %4, %16\n\t"
-        "ds_read_u8 %5, %17\n\t"
-        "ds_read_u8 %6, %20\n\t"
-        "ds_read_u8 %7, %21\n\t"
-        "ds_read_u8_d16_hi %0, %10\n\t"
-        "ds_read_u8_d16_hi %1, %11\n\t"
-        "ds_read_u8_d16_hi %2, %14\n\t"
-        "ds_read_u8_d16_hi %3, %15\n\t"
-        "ds_read_u8_d16_hi %4, %18\n\t"
-        "ds_read_u8_d16_hi %5, %19\n\t"
-        "ds_read_u8_d16_hi %6, %22\n\t"
-        "ds_read_u8_d16_hi %7, %23\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(lo0), "=&v"(hi0), "=&v"(lo1), "=&v"(hi1), "=&v"(lo2), "=&v"(hi2), "=&v"(lo3),
-          "=&v"(hi3)
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
-          "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]),
-          "v"(a[15])
-        : "memory");
-    P[0] = lo0 | (hi0 << 8);
-    P[1] = lo1 | (hi1 << 8);
-    P[2] = lo2 | (hi2 << 8);
-    P[3] = lo3 | (hi3 << 8);
-}
-
-// The 16 table values of a lane's characters, packed 4 per dword; the
-// characters at and past `nin` read as non-alphabet.
-#ifndef B64X_LV_D16  // A/B builds only: lane_values by tab_pack16_d16
-#define B64X_LV_D16 0
-#endif
 DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
 {
     const uint32_t dw[4] = {w.x, w.y, w.z, w.w};
-    if (B64X_LV_D16) {
-        tab_pack16_d16(tab, dw, P);  // the table is P2dSmem's, 256-byte aligned
-    } else {
 #pragma unroll
-        for (uint32_t g = 0; g < 4; g++) {
-            const uint32_t t0 = tab[dw[g] & 0xFFu];
-            const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
-            const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
-            const uint32_t t3 = tab[dw[g] >> 24];
-            P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
-        }
+    for (uint32_t g = 0; g < 4; g++) {
+        const uint32_t t0 = tab[dw[g] & 0xFFu];
+        const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
+        const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
+        const uint32_t t3 = tab[dw[g] >> 24];
+        P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
     }
     if (nin < 16) {
 #pragma unroll
@@ -1516,8 +1460,8 @@ DEV uint32_t lane_valid_count(const uint32_t P[4])
 constexpr uint32_t kP2dBytes = 16 + 15 + kP2Range / 4 * 3 + 16;
 constexpr uint32_t kP2dBlocks = (kP2dBytes + 15) / 16;                  // uint4 per wave
 
-struct __attribute__((aligned(256))) P2dSmem {
-    uint8_t tab[256];  // 256-byte aligned: tab_pack16_d16
+struct __attribute__((aligned(16))) P2dSmem {
+    uint8_t tab[256];
     uint32_t sel[16];
     uint4 bits[kWavesPerBlock][kP2dBlocks];
 };
@@ -3063,8 +3007,16 @@ struct RowModel {
                             // only filler, so consecutive rows' writes are contiguous)
     uint32_t pad;
     uint64_t m64x;          // ceil(2^64 / Sx)
+    // Row-group mapping of the line-structured hot path (k_decode_rows_lines,
+    // B64X_ROWS_RG): a lane keeps one row slot q for all its U slots, which
+    // lie in rows Ru apart; NB blocks of kThreads lanes cover Ru rows' Sx
+    // slots (NB kThreads = Ru Sx = lcm(kThreads, Sx)), so the line position
+    // of q is computed once per lane, not once per slot.
+    uint32_t nb, ru;        // blocks per row band, rows per band
+    uint32_t mx;            // ceil(2^32 / Sx): exact for slot offsets below NB kThreads
+    uint32_t rg;            // 1: the mapping applies
 };
-static_assert(sizeof(RowModel) == 80, "RowModel layout");
+static_assert(sizeof(RowModel) == 96, "RowModel layout");
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the model, in the region pass 1
@@ -3206,6 +3158,16 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
     const uint64_t relmax = Sq + (uint64_t) kRowsU * kThreads;
     if ((!r.L || 16ull * Sr <= 4096) && relmax * ((uint64_t) rS * Sq - (1u << 20)) < (1u << 20))
         r.rcpS = rS;
+    if (r.L && r.Sx < 4096) {
+        const uint32_t g = (r.Sx & (0u - r.Sx)) < kThreads ? (r.Sx & (0u - r.Sx)) : kThreads;
+        r.nb = r.Sx / g;          // Sx / gcd(Sx, kThreads)
+        r.ru = kThreads / g;      // kThreads / gcd(Sx, kThreads)
+        r.mx = (uint32_t) ((0xFFFFFFFFull + r.Sx) / r.Sx);
+        // 32-bit lane offsets within a band (rin < ru rows), 24-bit products
+        r.rg = (uint64_t) r.ru * in_stride + len + 32 < (1ull << 31) &&
+               (uint64_t) r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
+               out_stride < (1u << 24);
+    }
     if (threadIdx.x == 0) *row_model(ws) = r;
 }
 
@@ -3241,6 +3203,9 @@ DEV void mark_failed_rows(unsigned long long *bm, uint64_t junk, uint32_t q, uin
         atomicOr(bm + (row >> 6), 1ull << (row & 63));
 }
 
+#ifndef B64X_ROWS_PRICE  // A/B builds only: no lookups (wrong output)
+#define B64X_ROWS_PRICE 0
+#endif
 template <int U, bool O32>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
 void k_decode_rows_lines(
@@ -3248,7 +3213,7 @@ void k_decode_rows_lines(
     uint8_t *__restrict__ out, uint64_t out_stride, uint32_t S, uint32_t magic, uint64_t m64,
     uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws)
 {
-    __shared__ __attribute__((aligned(256))) uint8_t tab[256];  // tab_pack16_d16
+    __shared__ uint8_t tab[256];
     const uint64_t *rmw = (const uint64_t *) row_model(ws);
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
@@ -3274,6 +3239,97 @@ void k_decode_rows_lines(
         const uint32_t Sm = rm.S;
         const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
         const uint32_t Sx = (uint32_t) scalar_load_u64(rmw + 8);
+#ifndef B64X_ROWS_RG  // A/B builds only: 0 = round 2's slot-by-slot mapping
+#define B64X_ROWS_RG 1
+#endif
+        const uint64_t r10 = scalar_load_u64(rmw + 10), r11 = scalar_load_u64(rmw + 11);
+        if (B64X_ROWS_RG && O32 && rcpS && (rm.L & 3) == 0 && (uint32_t) (r11 >> 32)) {
+            const uint32_t NB = (uint32_t) r10, Ru = (uint32_t) (r10 >> 32), mx = (uint32_t) r11;
+            const uint32_t st = blockIdx.x / NB, bi = blockIdx.x - st * NB;  // scalar
+            const uint64_t row_st = (uint64_t) st * (U * Ru);  // the block's first row
+            if (row_st >= nbuf) return;
+            // blocks with rows at or past the last: page-safe loads, decoded
+            // bytes only (as below)
+            const bool tail = row_st + U * Ru > nbuf - 1;
+            const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
+            const uint32_t nb_last = j0 == kNoRowShape ? 0u : 3 * (j0 >> 2) + ((6 * (j0 & 3)) >> 3);
+            const uint32_t kq = rm.F - 16 * (Sm - 1);
+            const uint32_t iL = 16 * (Sm - 1), dL = iL / rm.L, colL = iL - dL * rm.L;
+            const uint32_t cL = rm.L - colL < 16 ? rm.L - colL : 16u;
+            const uint32_t spanL = len - (dL * rm.P + colL);
+            const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
+                                 : (spanL - cL < rm.s ? spanL - cL : rm.s);
+            const uint32_t need_L = sep_need(nsepL);
+            const uint32_t kmask = 128u * (kq >= 16 ? 0xFFFFu : (1u << kq) - 1u);
+            const uint32_t expm = j0 == kNoRowShape ? 1u : kmask & ~(128u * ((1u << j0) - 1u));
+            // the lane's slot q and row in the band, once for its U slots
+            const uint32_t F = bi * kThreads + threadIdx.x;  // < NB kThreads = Ru Sx
+            const uint32_t rin = __umulhi(F, mx);
+            const uint32_t q = F - __umul24(rin, Sx);
+            const uint32_t i = 16 * (q < Sm ? q : Sm - 1);
+            const uint32_t dl = __umul24(i, rm.rcp) >> 20;
+            const uint32_t col = i - __umul24(dl, rm.L);
+            const uint32_t pos = __umul24(dl, rm.P) + col;
+            const uint32_t oo = pos & 3u;
+            const bool last = q == Sm - 1;
+            const bool hs = rm.L - col <= 16;
+            const uint32_t c = hs ? rm.L - col : 16u;
+            const uint32_t ioff = __umul24(rin, (uint32_t) in_stride) + (pos & ~3u);
+            const uint32_t ooff = __umul24(rin, (uint32_t) out_stride) + __umul24(q, 12u);
+            const uint8_t *ib = in + row_st * in_stride;
+            uint8_t *ob = out + row_st * out_stride;
+            const uint64_t ui = (uint64_t) Ru * in_stride, uo = (uint64_t) Ru * out_stride;
+            uint4 win[U];
+            uint2 wx[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint8_t *ab = ib + u * ui + ioff;
+                if (!tail) {
+                    win[u] = load16_a4(ab);
+                    const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+                    wx[u] = make_uint2(v.x, v.y);
+                } else {
+                    const bool live = row_st + u * Ru + rin < nbuf;
+                    win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
+                    wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t row = row_st + u * Ru + rin;
+                const bool live = !tail || row < nbuf;
+                const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+                uint32_t sep;
+                const uint4 d = slot_chars4(w6, oo, c >> 2, rm.s, &sep);
+                const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+                uint32_t G[4], m128 = 0;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const uint32_t P = tab_pack4(tab, dw[g]);
+                    const uint32_t Pz = P & 0x3F3F3F3Fu;
+                    G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
+                           __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
+                    const uint32_t w = (g & 1) ? 0x80402010u : 0x08040201u;
+                    const uint32_t part = __builtin_amdgcn_udot4(P & 0x80808080u, w, 0u, false);
+                    m128 += (g & 2) ? part << 8 : part;
+                }
+                uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
+                if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
+                         : (hs && !sep_ok_s(tab, sep, rm.s)))
+                    bad |= 1u;
+                if (q >= Sm || !live) bad = 0;  // slack filler: the bytes are scratch
+                uint32_t o0, o1, o2;
+                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
+                uint8_t *dst = ob + u * uo + ooff;
+                if (!tail)
+                    __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
+                else if (live && q < Sm && bad == 0)
+                    store_bytes12(dst, o0, o1, o2, last ? nb_last : 12u);
+                const uint64_t junk = __ballot(bad != 0);
+                if (junk) mark_failed_rows(bm, junk, q, row);
+            }
+            return;
+        }
         if (O32 && rcpS && (rm.L & 3) == 0) {
             if (s0 >= (uint64_t) Sx * nbuf) return;
             // blocks that touch the last row: page-safe loads, no slack
@@ -3349,18 +3405,9 @@ void k_decode_rows_lines(
                 const uint4 d = slot_chars4(w6, oo[u], c >> 2, rm.s, &sep);
                 const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
                 uint32_t G[4], m128 = 0;
-#ifndef B64X_ROWS_PRICE  // A/B builds only: no lookups (wrong output)
-#define B64X_ROWS_PRICE 0
-#endif
-#ifndef B64X_ROWS_D16  // A/B builds only: tab_pack16_d16 instead of tab_pack4
-#define B64X_ROWS_D16 0
-#endif
-                uint32_t PP[4];
-                if (B64X_ROWS_D16) tab_pack16_d16(tab, dw, PP);
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const uint32_t P = B64X_ROWS_PRICE ? dw[g] & 0x3F3F3F3Fu
-                                     : B64X_ROWS_D16   ? PP[g] : tab_pack4(tab, dw[g]);
+                    const uint32_t P = B64X_ROWS_PRICE ? dw[g] & 0x3F3F3F3Fu : tab_pack4(tab, dw[g]);
                     const uint32_t Pz = P & 0x3F3F3F3Fu;
                     G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
                            __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
@@ -4252,7 +4299,9 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                                dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in, (uint32_t) len,
                                in_stride, (uint32_t) S, out_stride, a, ws);
             if ((err = launch_status())) return err;
-            const dim3 g((uint32_t) ((slots + per - 1) / per));
+            // + S blocks: the row-group mapping rounds the rows up to whole
+            // bands of U Ru rows (NB <= S blocks each); spare blocks return
+            const dim3 g((uint32_t) ((slots + per - 1) / per + S));
             // 32-bit offsets within a block's rows (relmax / S + 1 rows at most)
             const uint64_t brows = relmax / S + 1;
             const bool o32 = in_stride < (1u << 24) && out_stride < (1u << 24) &&

@@ -67,26 +67,32 @@ def child(lib, steps, only=()):
                                                          1, 0))
     timeit("encode", lambda: b64.encode(x, out=enc))
     ran = lambda k: not only or k in only  # noqa: E731 -- checks only for legs that ran
+    bad = []
+
+    def chk(name, good):
+        if ran(name) and not good:
+            bad.append(name)
+        return True
     timeit("decode", lambda: b64.decode(enc, out=out, workspace=ws, result=rr))
-    ok = not ran("decode") or torch.equal(out[:n], x)
+    ok = chk("decode", torch.equal(out[:n], x))
     timeit("crlf", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr))
-    ok = ok and (not ran("crlf") or torch.equal(out[:n], x))
+    ok = chk("crlf", torch.equal(out[:n], x))
     timeit("junk", lambda: b64.decode(junk, out=out, workspace=ws, result=rr))
-    ok = ok and (not ran("junk") or torch.equal(out[:n], x))
+    ok = chk("junk", torch.equal(out[:n], x))
     timeit("junk1", lambda: b64.decode(junk1, out=out, workspace=ws, result=rr))
-    ok = ok and (not ran("junk1") or torch.equal(out[:n], x))
+    ok = chk("junk1", torch.equal(out[:n], x))
     timeit("junk_ej", lambda: b64.decode(junk, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
-    ok = ok and (not ran("junk_ej") or torch.equal(out[:n], x))
+    ok = chk("junk_ej", torch.equal(out[:n], x))
     timeit("crlf_ej", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
-    ok = ok and (not ran("crlf_ej") or torch.equal(out[:n], x))
+    ok = chk("crlf_ej", torch.equal(out[:n], x))
     # config 4: 1 M x 1 KiB rows, strided decode (clean)
     del dirty, junk, junk1, enc, out, x
     if only and not ({"rows_enc", "rows_dec", "rows_crlf", "ragged_dec"} & set(only)):
         for k in ("rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
             res[k] = (0.0, 0.0, 0.0)
-        print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
+        print(json.dumps({"lib": lib, "ok": not bad, "bad": bad, **res}), flush=True)
         return
     nb, L = 1 << 20, 1024
     Es = b64.encoded_len(L)
@@ -99,8 +105,7 @@ def child(lib, steps, only=()):
     b64.encode_strided(xb, L, L, nb, eb, Es)  # the rows the decode legs read
     timeit("rows_enc", lambda: b64.encode_strided(xb, L, L, nb, eb, Es))
     timeit("rows_dec", lambda: b64.decode_strided(eb, Es, Es, nb, db, cap, ol))
-    ok = ok and (not ran("rows_dec") or (bool((ol == L).all()) and
-                                         torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L))))
+    ok = chk("rows_dec", bool((ol == L).all()) and torch.equal(db.view(nb, cap)[:, :L], xb.view(nb, L)))
     # the same rows MIME-formatted (76-character lines, CRLF)
     lines = (Es + 75) // 76
     rows = eb.view(nb, Es)
@@ -114,8 +119,8 @@ def child(lib, steps, only=()):
     cap2 = 12 * ((D + 15) // 16)
     db2 = torch.empty(nb * cap2, dtype=torch.uint8, device="cuda")
     timeit("rows_crlf", lambda: b64.decode_strided(mb, D, D, nb, db2, cap2, ol))
-    ok = ok and (not ran("rows_crlf") or (bool((ol == L).all()) and
-                                          torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L))))
+    ok = chk("rows_crlf", bool((ol == L).all()) and
+             torch.equal(db2.view(nb, cap2)[:, :L], xb.view(nb, L)))
     # a ragged batch of 65,536 messages of 100-4,000 bytes (the hub's shape)
     del mb, db2, db, eb, xb
     g = torch.Generator().manual_seed(5)
@@ -137,11 +142,11 @@ def child(lib, steps, only=()):
     doff_d = doff.cuda()
     olr = torch.zeros(65536, dtype=torch.int64, device="cuda")
     timeit("ragged_dec", lambda: b64.decode_batch(er, eoff_d, dr, doff_d[:-1], olr))
-    ok = ok and bool((olr.cpu() == lens).all())
+    ok = chk("ragged_dec", bool((olr.cpu() == lens).all()))
     for i in (0, 1, 777, 65535):
         a0, d0 = int(ioff[i]), int(doff[i])
-        ok = ok and torch.equal(dr[d0:d0 + int(lens[i])], xr[a0:a0 + int(lens[i])])
-    print(json.dumps({"lib": lib, "ok": bool(ok), **res}), flush=True)
+        ok = chk("ragged_dec", torch.equal(dr[d0:d0 + int(lens[i])], xr[a0:a0 + int(lens[i])]))
+    print(json.dumps({"lib": lib, "ok": not bad, "bad": bad, **res}), flush=True)
 
 
 def main():

@@ -806,6 +806,34 @@ def test_strided_mime_rows_vs_oracle(n, L, sep):
             assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (cap, i)
 
 
+@pytest.mark.parametrize("n,L,sep,nbuf", [(1024, 76, b"\r\n", 2600), (1000, 64, b"\n", 1100),
+                                          (3000, 76, b"\r\n", 700)])
+def test_strided_mime_rows_bands_vs_oracle(n, L, sep, nbuf):
+    """The row-group mapping of the MIME rows kernel (RowModel::nb/ru: a
+    lane's U slots share one row slot q, U bands of Ru rows apart) over
+    batches with whole bands and a partial last one, deviant rows inside
+    whole bands and in the last, and a guard band after the output."""
+    rng = np.random.default_rng(n + nbuf)
+    dv = {5: "junk", nbuf // 3: "len", nbuf // 2: "junk", nbuf - 2: "len", nbuf - 1: "junk"}
+    rows = _mime_batch(nbuf, n, L, sep, rng, deviants=dv)
+    stride = max(len(r) for r in rows)
+    flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
+    x = dev(flat)
+    dcap = b64.decoded_cap(stride)
+    for cap in ((dcap + 11) // 12 * 12, (dcap + 15) // 16 * 16):
+        size = (nbuf - 1) * cap + dcap
+        dec = torch.full((size + 64,), 0xA5, dtype=torch.uint8, device=DEV)
+        outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+        b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen)
+        ol = outlen.cpu().tolist()
+        dh = dec.cpu().numpy()
+        assert (dh[size:] == 0xA5).all(), cap
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)))
+            assert ol[i] == len(want), (cap, i)
+            assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (cap, i)
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
