@@ -122,6 +122,19 @@ typedef uint32_t u32x4a16 __attribute__((ext_vector_type(4), aligned(16)));
 
 // Store the first `nbytes` (0..12) bytes of {o0, o1, o2}: whole dwords when
 // `p` is dword aligned, then at most 3 single bytes.
+// The first nbytes (<= 12) bytes of o0:o1:o2 one at a time, in a loop the
+// compiler keeps rolled: for the rare tail blocks of a hot kernel, whose
+// unrolled byte tests (store_bytes12) the compiler hoists out of the
+// kernel's slot loop as SGPR masks that then spill.
+DEV void store_bytes12_rolled(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t nbytes)
+{
+#pragma unroll 1
+    for (uint32_t k = 0; k < nbytes; k++) {
+        const uint32_t w = k < 4 ? o0 : k < 8 ? o1 : o2;
+        p[k] = (uint8_t) (w >> (8 * (k & 3)));
+    }
+}
+
 DEV void store_bytes12(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2,
                        uint32_t nbytes)
 {
@@ -3164,8 +3177,8 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
         r.ru = kThreads / g;      // kThreads / gcd(Sx, kThreads)
         r.mx = (uint32_t) ((0xFFFFFFFFull + r.Sx) / r.Sx);
         // 32-bit lane offsets within a band (rin < ru rows), 24-bit products
-        r.rg = (uint64_t) r.ru * in_stride + len + 32 < (1ull << 31) &&
-               (uint64_t) r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
+        r.rg = (uint64_t) kRowsU * r.ru * in_stride + len + 32 < (1ull << 31) &&
+               (uint64_t) kRowsU * r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
                out_stride < (1u << 24);
     }
     if (threadIdx.x == 0) *row_model(ws) = r;
@@ -3205,6 +3218,9 @@ DEV void mark_failed_rows(unsigned long long *bm, uint64_t junk, uint32_t q, uin
 
 #ifndef B64X_ROWS_PRICE  // A/B builds only: no lookups (wrong output)
 #define B64X_ROWS_PRICE 0
+#endif
+#ifndef B64X_ROWS_SEPBR  // A/B builds only: 0 = branch-free separator check
+#define B64X_ROWS_SEPBR 1
 #endif
 template <int U, bool O32>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
@@ -3259,7 +3275,7 @@ void k_decode_rows_lines(
             const uint32_t spanL = len - (dL * rm.P + colL);
             const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
                                  : (spanL - cL < rm.s ? spanL - cL : rm.s);
-            const uint32_t need_L = sep_need(nsepL);
+            const uint32_t need_L = sep_need(nsepL), need_s = sep_need(rm.s);
             const uint32_t kmask = 128u * (kq >= 16 ? 0xFFFFu : (1u << kq) - 1u);
             const uint32_t expm = j0 == kNoRowShape ? 1u : kmask & ~(128u * ((1u << j0) - 1u));
             // the lane's slot q and row in the band, once for its U slots
@@ -3274,16 +3290,21 @@ void k_decode_rows_lines(
             const bool last = q == Sm - 1;
             const bool hs = rm.L - col <= 16;
             const uint32_t c = hs ? rm.L - col : 16u;
+            const uint32_t need = last ? need_L : hs ? need_s : 0u;  // separator bytes to check
             const uint32_t ioff = __umul24(rin, (uint32_t) in_stride) + (pos & ~3u);
             const uint32_t ooff = __umul24(rin, (uint32_t) out_stride) + __umul24(q, 12u);
+            // one 64-bit base per block; every lane offset is 32-bit (the
+            // prep checks U bands of rows span under 2^31 bytes), so the
+            // loads and stores take a scalar base and a VGPR offset and the
+            // per-band bases cost no SGPR pairs (they spilled to VGPR lanes)
             const uint8_t *ib = in + row_st * in_stride;
             uint8_t *ob = out + row_st * out_stride;
-            const uint64_t ui = (uint64_t) Ru * in_stride, uo = (uint64_t) Ru * out_stride;
+            const uint32_t ui = Ru * (uint32_t) in_stride, uo = Ru * (uint32_t) out_stride;
             uint4 win[U];
             uint2 wx[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint8_t *ab = ib + u * ui + ioff;
+                const uint8_t *ab = ib + (ioff + u * ui);
                 if (!tail) {
                     win[u] = load16_a4(ab);
                     const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
@@ -3314,17 +3335,21 @@ void k_decode_rows_lines(
                     m128 += (g & 2) ? part << 8 : part;
                 }
                 uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
-                if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
-                         : (hs && !sep_ok_s(tab, sep, rm.s)))
-                    bad |= 1u;
+                if (B64X_ROWS_SEPBR) {
+                    if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
+                             : (hs && !sep_ok_s(tab, sep, rm.s)))
+                        bad |= 1u;
+                } else {
+                    bad |= (sep_nonalpha(tab, sep) & need) ^ need;  // need: per lane, above
+                }
                 if (q >= Sm || !live) bad = 0;  // slack filler: the bytes are scratch
                 uint32_t o0, o1, o2;
                 groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-                uint8_t *dst = ob + u * uo + ooff;
+                uint8_t *dst = ob + (ooff + u * uo);
                 if (!tail)
                     __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
                 else if (live && q < Sm && bad == 0)
-                    store_bytes12(dst, o0, o1, o2, last ? nb_last : 12u);
+                    store_bytes12_rolled(dst, o0, o1, o2, last ? nb_last : 12u);
                 const uint64_t junk = __ballot(bad != 0);
                 if (junk) mark_failed_rows(bm, junk, q, row);
             }
@@ -3421,9 +3446,6 @@ void k_decode_rows_lines(
                 // expected ones among its k positions outside it
                 uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
                 // the separator bytes of a line that ends in the span
-#ifndef B64X_ROWS_SEPBR  // A/B builds only: 0 = branch-free separator check
-#define B64X_ROWS_SEPBR 1
-#endif
                 if (B64X_ROWS_SEPBR) {
                     if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
                              : (hs && !sep_ok_s(tab, sep, rm.s)))
