@@ -5093,8 +5093,9 @@ uint64_t b64x__test_range_chunks(uint64_t chunks)
 
 const char *b64x_build_info(void)
 {
-    return "b64x abi=2 arch=gfx950 enc:quad12->16 bpermute-alphabet unroll=4; "
-           "dec:probe+line-model single pass (4 slots/lane) + exact suffix (look-back)";
+    return "b64x abi=2 arch=gfx950 enc:quad12->16 lds-alphabet 1 quad/lane; "
+           "dec:probe+line-model single pass (4 slots/lane) + exact suffix (group sums); "
+           "rows:line model in row bands";
 }
 
 const char *b64x_strerror(int err)
