@@ -1888,6 +1888,10 @@ constexpr uint32_t kProbeThreads = 256;
 #define B64X_PROBE_SAMPLES 1
 #endif
 constexpr uint64_t kProbeSampleMin = B64X_PROBE_SAMPLES ? 1u << 18 : ~0ull;  // shorter streams: the first window only
+#ifndef B64X_PROBE_NS  // A/B builds only: sampling threads (<= kProbeThreads)
+#define B64X_PROBE_NS 256
+#endif
+constexpr uint32_t kProbeNS = B64X_PROBE_NS;
 constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
 
 __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
@@ -1898,16 +1902,16 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
     __shared__ uint32_t s_first;
     // the samples' loads are issued first: they overlap the table build and
     // the window probe
-    const bool sample = n >= kProbeSampleMin;
+    const bool sample = n >= kProbeSampleMin && threadIdx.x < kProbeNS;
     uint32_t sw[16];
     uint32_t q = 0;
     if (sample) {
         // half the samples over the first 1/16 of the stream, half over all
         // of it, each half at quadratically growing distances
         const uint64_t W = n - kProbeTailKeep - 64 - 256;
-        const uint64_t span = threadIdx.x < kProbeThreads / 2 ? W / 16 : W;
-        const uint64_t i = threadIdx.x % (kProbeThreads / 2) + 1;
-        const uint64_t raw = 256 + span * i * i / ((uint64_t) kProbeThreads * kProbeThreads / 4);
+        const uint64_t span = threadIdx.x < kProbeNS / 2 ? W / 16 : W;
+        const uint64_t i = threadIdx.x % (kProbeNS / 2) + 1;
+        const uint64_t raw = 256 + span * i * i / ((uint64_t) kProbeNS * kProbeNS / 4);
         const uint8_t *pa = (const uint8_t *) ((uintptr_t) (in + raw) & ~(uintptr_t) 15);
         q = (uint32_t) (pa - in);
 #pragma unroll
