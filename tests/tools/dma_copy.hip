@@ -22,6 +22,19 @@ __global__ __launch_bounds__(256) void plain(const v4u *__restrict__ in, v4u *__
     for (int u = 0; u < U; u++) __builtin_nontemporal_store(v[u], out + b + u * 256);
 }
 
+// plain with a dword-aligned (not 16-byte aligned) source
+template <int U>
+__global__ __launch_bounds__(256) void plain_mis(const uint8_t *__restrict__ in, v4u *__restrict__ out)
+{
+    typedef uint32_t v4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const uint64_t b = (uint64_t) blockIdx.x * 256 * U + threadIdx.x;
+    v4a4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load((const v4a4 *) in + b + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(v4u{v[u].x, v[u].y, v[u].z, v[u].w}, out + b + u * 256);
+}
+
 // the wave's 1 KiB per step read straight into its LDS slice (M0 = the
 // slice, each lane's 16 bytes at lane * 16), then read back and stored
 template <int U, int NT>
@@ -85,6 +98,12 @@ int main()
         printf("plain U1      %.4f ms %.0f GB/s\n", ms, gb / ms * 1e3);
         ms = timeit([&] { plain<2><<<half / 8192, 256>>>((const v4u *) in, (v4u *) out); });
         printf("plain U2      %.4f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+        // the same copy reading from 8 bytes past a 16-byte boundary (every
+        // 16-byte load straddles two 16-byte blocks: config 4's odd rows)
+        ms = timeit([&] { plain_mis<1><<<half / 4096 - 1, 256>>>(in + 8, (v4u *) out); });
+        printf("plain U1 +8   %.4f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+        ms = timeit([&] { plain_mis<1><<<half / 4096 - 1, 256>>>(in + 4, (v4u *) out); });
+        printf("plain U1 +4   %.4f ms %.0f GB/s\n", ms, gb / ms * 1e3);
         ms = timeit([&] { dma<1, 0><<<half / 4096, 256>>>(in, (v4u *) out); });
         printf("dma U1        %.4f ms %.0f GB/s\n", ms, gb / ms * 1e3);
         ms = timeit([&] { dma<1, 1><<<half / 4096, 256>>>(in, (v4u *) out); });
