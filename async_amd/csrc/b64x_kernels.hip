@@ -2000,13 +2000,17 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
 #ifndef B64X_LINES_WTAB  // A/B builds only: 1 = each wave builds its own table, no block barrier
 #define B64X_LINES_WTAB 0
 #endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
+#ifndef B64X_LINES_TH  // A/B builds only: lanes per block of k_decode_lines
+#define B64X_LINES_TH 256
+#endif
+constexpr uint32_t kLinesTH = B64X_LINES_TH, kLinesWaves = kLinesTH / 64;
+__global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, uint32_t seq)
 {
 #if B64X_LINES_WTAB
-    __shared__ uint32_t tabw[kWavesPerBlock][64];
+    __shared__ uint32_t tabw[kLinesWaves][64];
 #else
     __shared__ uint8_t tab[256];
 #endif
@@ -2021,7 +2025,7 @@ void k_decode_lines(
     // leaves before the barrier: on junk-laden input nearly every block of
     // this launch does.  (Tested before the table build, the model's load
     // no longer overlapped the build: MIME text +2 %.)
-    if (blockIdx.x * kWavesPerBlock * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
+    if (blockIdx.x * kLinesWaves * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
     __syncthreads();
 #endif
     LineModel m;
@@ -2039,7 +2043,7 @@ void k_decode_lines(
     // and output address are then scalar (a vector t0 cost a 64-bit
     // multiply-add per slot store and a 32-bit multiply per wave)
     const uint32_t wv = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
-    const uint32_t t0 = (blockIdx.x * kWavesPerBlock + wv) * kLinesSlots;
+    const uint32_t t0 = (blockIdx.x * kLinesWaves + wv) * kLinesSlots;
     if (t0 > T) return;
 #if B64X_LINES_WTAB
     const uint8_t *tab = wave_dec_table(tabw[wv], a);
@@ -4218,8 +4222,8 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
                            a, ws, p.nranges);
         if ((err = launch_status())) return err;
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
-        hipLaunchKernelGGL(k_decode_lines, dim3((uint32_t) ((waves + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kThreads), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
+        hipLaunchKernelGGL(k_decode_lines, dim3((uint32_t) ((waves + kLinesWaves - 1) / kLinesWaves)),
+                           dim3(kLinesTH), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
         hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
