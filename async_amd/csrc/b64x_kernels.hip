@@ -3224,9 +3224,6 @@ DEV void mark_failed_rows(unsigned long long *bm, uint64_t junk, uint32_t q, uin
         atomicOr(bm + (row >> 6), 1ull << (row & 63));
 }
 
-#ifndef B64X_ROWS_PRICE  // A/B builds only: no lookups (wrong output)
-#define B64X_ROWS_PRICE 0
-#endif
 #ifndef B64X_ROWS_SEPBR  // A/B builds only: 0 = branch-free separator check
 #define B64X_ROWS_SEPBR 1
 #endif
@@ -3263,7 +3260,7 @@ void k_decode_rows_lines(
         const uint32_t Sm = rm.S;
         const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
         const uint32_t Sx = (uint32_t) scalar_load_u64(rmw + 8);
-#ifndef B64X_ROWS_RG  // A/B builds only: 0 = round 2's slot-by-slot mapping
+#ifndef B64X_ROWS_RG  // A/B builds only: 0 = every MIME batch through the general path
 #define B64X_ROWS_RG 1
 #endif
         const uint64_t r10 = scalar_load_u64(rmw + 10), r11 = scalar_load_u64(rmw + 11);
@@ -3363,118 +3360,10 @@ void k_decode_rows_lines(
             }
             return;
         }
-        if (O32 && rcpS && (rm.L & 3) == 0) {
-            if (s0 >= (uint64_t) Sx * nbuf) return;
-            // blocks that touch the last row: page-safe loads, no slack
-            // filler (the last row's capacity may end before out_stride),
-            // decoded bytes only
-            const bool tail = s0 + U * kThreads > (uint64_t) Sx * (nbuf - 1);
-            const uint8_t *end = in + (uint64_t) (nbuf - 1) * in_stride + len;
-            const uint32_t nb_last = j0 == kNoRowShape ? 0u : 3 * (j0 >> 2) + ((6 * (j0 & 3)) >> 3);
-            const uint64_t b0 = __umul64hi(s0, scalar_load_u64(rmw + 9));
-            const uint32_t q0 = (uint32_t) (s0 - b0 * Sx);
-            const uint8_t *ib = in + b0 * in_stride;
-            uint8_t *ob = out + b0 * out_stride;
-            // The hot path of MIME-formatted rows (L % 4 == 0: RFC 2045's 76,
-            // PEM's 64, so a line end is a dword boundary of a slot and the
-            // merge a dword select): 24-bit slot mapping, the line division by
-            // the model's 20-bit reciprocal, unguarded window loads,
-            // non-temporal stores.  A row's last slot sits at the same place
-            // in every row, so its rule is wave-uniform constants: the masks
-            // of its k model positions and of those that must be outside the
-            // alphabet (the ones from j0 on), and
-            // the separator bytes its span must end with.  Slots from Sm to
-            // Sx - 1 of a row only store filler into the row's slack (see
-            // RowModel::Sx); their loads read the row's last slot instead.
-            // (VALU, not HBM, bounds this kernel: the table values are packed
-            // with v_perm, the groups and the non-alphabet mask come from
-            // v_dot4, and only the s separator bytes a line has are looked up.)
-            const uint32_t kq = rm.F - 16 * (Sm - 1);  // model positions of a last slot
-            const uint32_t iL = 16 * (Sm - 1), dL = iL / rm.L, colL = iL - dL * rm.L;
-            const uint32_t cL = rm.L - colL < 16 ? rm.L - colL : 16u;
-            const uint32_t spanL = len - (dL * rm.P + colL);
-            const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
-                                 : (spanL - cL < rm.s ? spanL - cL : rm.s);
-            const uint32_t need_L = sep_need(nsepL), need_s = sep_need(rm.s);
-            // 128 x (the last slot's masks of non-alphabet characters): the
-            // ones it may have (its k positions) and the ones it must have
-            const uint32_t kmask = 128u * (kq >= 16 ? 0xFFFFu : (1u << kq) - 1u);
-            const uint32_t expm = j0 == kNoRowShape ? 1u : kmask & ~(128u * ((1u << j0) - 1u));
-            uint32_t bl[U], qq[U], oo[U], cc[U];
-            uint4 win[U];
-            uint2 wx[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t rel = q0 + u * kThreads + threadIdx.x;
-                bl[u] = __umul24(rel, rcpS) >> 20;
-                qq[u] = rel - __umul24(bl[u], Sx);
-                const uint32_t i = 16 * (qq[u] < Sm ? qq[u] : Sm - 1);
-                const uint32_t dl = __umul24(i, rm.rcp) >> 20;
-                const uint32_t col = i - __umul24(dl, rm.L);
-                const uint32_t pos = __umul24(dl, rm.P) + col;
-                oo[u] = pos & 3u;
-                cc[u] = col;
-                const uint8_t *ab = ib + (__umul24(bl[u], (uint32_t) in_stride) + (pos & ~3u));
-                if (!tail) {
-                    win[u] = load16_a4(ab);
-                    const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
-                    wx[u] = make_uint2(v.x, v.y);
-                } else {
-                    const bool live = s0 + u * kThreads + threadIdx.x < (uint64_t) Sx * nbuf;
-                    win[u] = live ? load_win16(ab, end) : make_uint4(0, 0, 0, 0);
-                    wx[u] = live ? load_win8(ab + 16, end) : make_uint2(0, 0);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t q = qq[u];
-                const bool last = q == Sm - 1;
-                const bool live = !tail || s0 + u * kThreads + threadIdx.x < (uint64_t) Sx * nbuf;
-                const uint32_t col = cc[u];
-                const bool hs = rm.L - col <= 16;
-                const uint32_t c = hs ? rm.L - col : 16u;
-                const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
-                uint32_t sep;
-                const uint4 d = slot_chars4(w6, oo[u], c >> 2, rm.s, &sep);
-                const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
-                uint32_t G[4], m128 = 0;
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const uint32_t P = B64X_ROWS_PRICE ? dw[g] & 0x3F3F3F3Fu : tab_pack4(tab, dw[g]);
-                    const uint32_t Pz = P & 0x3F3F3F3Fu;
-                    G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
-                           __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
-                    // 128 x the non-alphabet mask of the 16 characters, four
-                    // bits per dword (weights fit a byte within each half)
-                    const uint32_t w = (g & 1) ? 0x80402010u : 0x08040201u;
-                    const uint32_t part = __builtin_amdgcn_udot4(P & 0x80808080u, w, 0u, false);
-                    m128 += (g & 2) ? part << 8 : part;
-                }
-                // interior: all 16 in the alphabet; last: exactly the
-                // expected ones among its k positions outside it
-                uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
-                // the separator bytes of a line that ends in the span
-                if (B64X_ROWS_SEPBR) {
-                    if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
-                             : (hs && !sep_ok_s(tab, sep, rm.s)))
-                        bad |= 1u;
-                } else {
-                    const uint32_t need = last ? need_L : hs ? need_s : 0u;
-                    bad |= (sep_nonalpha(tab, sep) & need) ^ need;
-                }
-                if (q >= Sm || !live) bad = 0;  // slack filler: the bytes are scratch
-                uint32_t o0, o1, o2;
-                groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
-                uint8_t *dst = ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u));
-                if (!tail)
-                    __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) dst);
-                else if (live && q < Sm && bad == 0)
-                    store_bytes12(dst, o0, o1, o2, last ? nb_last : 12u);
-                const uint64_t junk = __ballot(bad != 0);
-                if (junk) mark_failed_rows(bm, junk, q, b0 + bl[u]);
-            }
-            return;
-        }
+        // (Round 2's slot-by-slot hot path for these rows, the fallback when
+        // the row bands do not apply, was removed in round 3: with the bands
+        // only oversized strides reached it, so every such batch now takes
+        // the general path below.)
         const uint64_t ns_m = (uint64_t) Sm * nbuf;
         const uint64_t tail_m = (uint64_t) Sm * (nbuf - 1);
         if (s0 >= ns_m) return;
