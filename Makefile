@@ -38,7 +38,8 @@ OBJDIR   = build
 
 KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
 HOST_SRC   = async_amd/csrc/fsalloc.c async_amd/csrc/loop.c async_amd/csrc/streams.c \
-             async_amd/csrc/framing.c async_amd/csrc/b64_hub.c async_amd/csrc/b64_stages.c
+             async_amd/csrc/framing.c async_amd/csrc/fdstreams.c async_amd/csrc/b64_hub.c \
+             async_amd/csrc/b64_stages.c
 HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))

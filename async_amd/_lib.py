@@ -75,6 +75,9 @@ SIGNATURES = {
     "b64x_decode_workspace_size": (_u64, [_u64]),
     "b64x_encode_dev": (_int, [_vp, _u64, _vp, _ap, _vp]),
     "b64x_decode_dev": (_int, [_vp, _u64, _vp, _vp, _ap, ctypes.c_uint, _vp, _vp]),
+    "b64x_decode_dev_seq": (_int, [_vp, _u64, _vp, _vp, _ap, ctypes.c_uint, _vp, _vp,
+                                   ctypes.POINTER(_u32)]),
+    "b64x_result_check": (_int, [ctypes.POINTER(DecResult), _u64, ctypes.c_uint, _u32]),
     "b64x_encode_strided": (_int, [_vp, _u64, _u64, _u32, _vp, _u64, _ap, _vp]),
     "b64x_decode_strided": (_int, [_vp, _u64, _u64, _u32, _vp, _u64, _vp, _ap, _vp]),
     "b64x_encode_batch": (_int, [_vp, _vp, _u32, _vp, _vp, _ap, _vp]),

@@ -82,10 +82,23 @@ def encode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
 class Decoded:
     out: torch.Tensor          # capacity-sized output buffer
     result: torch.Tensor       # b64x_dec_result (RES_BYTES) on the device
+    nchars: int = 0            # the call's character count, flags and the
+    flags: int = 0             # sequence number it drew: what its record
+    seq: int = 0               # must echo (b64x_result_check)
+    stream: object = None      # the stream the decode ran on
 
     def info(self) -> DecResult:
+        """The call's result record, checked: waits for the decode's own
+        stream, copies the record back and refuses one that is not this
+        call's or is inconsistent (b64x_result_check)."""
+        s = self.stream if self.stream is not None else torch.cuda.current_stream()
+        s.synchronize()
         host = self.result[:RES_BYTES].cpu().numpy()  # keep alive across the copy
-        return DecResult.from_buffer_copy(host.tobytes())
+        r = DecResult.from_buffer_copy(host.tobytes())
+        if self.seq:
+            _lib.check("b64x_result_check", _lib.load().b64x_result_check(
+                ctypes.byref(r), self.nchars, self.flags, self.seq))
+        return r
 
     def bytes(self) -> torch.Tensor:
         """The decoded bytes (synchronises to read the length)."""
@@ -113,11 +126,13 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
         result = torch.zeros(RES_BYTES, dtype=torch.uint8, device=x.device)
     if workspace is None:  # must start zeroed; the library keeps it re-armed
         workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
-    _lib.check("b64x_decode_dev", lib.b64x_decode_dev(
-        _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a),
-        (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0),
-        _ptr(workspace), _stream(stream)))
-    return Decoded(out, result)
+    flags = (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0)
+    seq = ctypes.c_uint32(0)
+    _lib.check("b64x_decode_dev_seq", lib.b64x_decode_dev_seq(
+        _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a), flags,
+        _ptr(workspace), _stream(stream), ctypes.byref(seq)))
+    return Decoded(out, result, n, flags & HOLD_TAIL, seq.value,
+                   stream if stream is not None else torch.cuda.current_stream())
 
 
 def encode_strided(x: torch.Tensor, in_stride: int, length: int, nbuf: int,

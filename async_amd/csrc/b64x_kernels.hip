@@ -3749,15 +3749,29 @@ bool g_info_done[kMaxDevices];
 // Library-owned decode workspaces, one per (device, stream): a workspace
 // carries state from one kernel of a decode to the next, so streams must
 // not share one.  At most kWsCache of them are kept (about 12.7 MiB of HBM
-// each); the least recently used goes when another stream needs one, or
-// when its stream is released (b64x_release_stream).
+// each); the least recently used idle one goes when another stream needs
+// one, or when its stream is released (b64x_release_stream).
+//  - A call pins its entry from the lookup until its kernels are enqueued
+//    and an event is recorded behind them (`pins`), so no other thread can
+//    free a workspace between handing it out and enqueuing on it; an entry
+//    that is pinned is never evicted (a call on a ninth stream while all
+//    eight are mid-enqueue gets -EBUSY).
+//  - Eviction unlinks the entry under g_ws_mu and frees it outside the lock,
+//    after waiting on the event recorded behind its last use (the stream
+//    itself may be gone by then): no device-wide synchronisation, and no
+//    lock held while waiting, so a host callback on any stream that calls
+//    back into the library cannot deadlock on it.
 struct WsEntry {
     int dev;
     void *stream;
     void *ws;
-    uint64_t used;  // last use (g_ws_tick)
+    hipEvent_t last;    // recorded after the entry's last enqueued use
+    uint64_t used;      // last use (g_ws_tick)
+    int pins;           // calls between lookup and their event record
+    bool release;       // b64x_release_stream while pinned: free at unpin
 };
 constexpr int kWsCache = 8;
+std::mutex g_ws_mu;     // g_ws, g_ws_tick (never held while waiting on HIP)
 WsEntry g_ws[kWsCache];
 uint64_t g_ws_tick;
 
@@ -3977,70 +3991,123 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
     return launch_status();
 }
 
-// Free a cached workspace.  Work still queued on its stream may use it, and
-// the stream itself may have been destroyed since (its handle is then not
-// to be used): wait for the whole device, then free.  Eviction is rare (a
-// ninth stream decoding with a library-owned workspace).  Called with g_mu
-// held.
-static void ws_drop(WsEntry &e)
+// Free an unlinked workspace (outside g_ws_mu): wait for the work queued
+// behind its last use, then release it on its device.
+static void ws_free(const WsEntry &e)
 {
     if (!e.ws) return;
     int prev = 0;
     (void) hipGetDevice(&prev);
     (void) hipSetDevice(e.dev);
-    (void) hipDeviceSynchronize();
+    if (e.last) {
+        (void) hipEventSynchronize(e.last);
+        (void) hipEventDestroy(e.last);
+    }
     (void) hipFree(e.ws);
     (void) hipSetDevice(prev);
-    e = WsEntry{};
 }
 
-static void *library_workspace(void *stream, int *err)
+// The workspace of (current device, stream), pinned; *slot receives its
+// entry for ws_unpin().  A new stream takes a free entry or the least
+// recently used idle one (freed outside the lock); -EBUSY when every entry
+// is pinned by a call in progress.
+static void *library_workspace(void *stream, int *slot, int *err)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
         *err = -ENODEV;
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(g_mu);
-    int victim = -1;
-    for (int i = 0; i < kWsCache; i++) {
-        WsEntry &e = g_ws[i];
-        if (e.ws && e.dev == dev && e.stream == stream) {
-            e.used = ++g_ws_tick;
-            *err = 0;
-            return e.ws;
+    WsEntry victim{};
+    int v = -1;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        for (int i = 0; i < kWsCache; i++) {
+            WsEntry &e = g_ws[i];
+            if (e.ws && e.dev == dev && e.stream == stream && !e.release) {
+                e.used = ++g_ws_tick;
+                e.pins++;
+                *slot = i;
+                *err = 0;
+                return e.ws;
+            }
         }
+        // a free entry (no workspace and not reserved by a call that is
+        // allocating one: such an entry is pinned), else the LRU idle one
+        for (int i = 0; i < kWsCache && v < 0; i++)
+            if (!g_ws[i].ws && !g_ws[i].pins) v = i;
+        for (int i = 0; i < kWsCache && v < 0; i++)
+            if (!g_ws[i].pins) v = i;
+        if (v < 0) {
+            *err = -EBUSY;
+            return nullptr;
+        }
+        if (g_ws[v].ws)
+            for (int i = 0; i < kWsCache; i++)
+                if (g_ws[i].ws && !g_ws[i].pins && g_ws[i].used < g_ws[v].used) v = i;
+        victim = g_ws[v];
+        // reserve the slot (no ws yet: nobody else looks it up) while the
+        // old workspace is freed and the new one allocated
+        g_ws[v] = WsEntry{dev, stream, nullptr, nullptr, ++g_ws_tick, 1, false};
     }
-    for (int i = 0; i < kWsCache && victim < 0; i++)
-        if (!g_ws[i].ws) victim = i;
-    if (victim < 0) {
-        victim = 0;
-        for (int i = 1; i < kWsCache; i++)
-            if (g_ws[i].used < g_ws[victim].used) victim = i;
-    }
-    // A new stream: the least recently used entry (or a free one) goes.
-    ws_drop(g_ws[victim]);
+    ws_free(victim);
     void *p = nullptr;
+    hipEvent_t ev = nullptr;
     hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
     if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    std::lock_guard<std::mutex> lk(g_ws_mu);
     if (e != hipSuccess) {
         if (p) (void) hipFree(p);
+        if (ev) (void) hipEventDestroy(ev);
+        g_ws[v] = WsEntry{};
         *err = hip_err(e);
         return nullptr;
     }
-    g_ws[victim] = WsEntry{dev, stream, p, ++g_ws_tick};
+    g_ws[v].ws = p;
+    g_ws[v].last = ev;
+    *slot = v;
     *err = 0;
     return p;
+}
+
+// The call that pinned entry `slot` has enqueued its kernels on `stream`:
+// record the entry's last-use event behind them and unpin it.
+static void ws_unpin(int slot, void *stream)
+{
+    WsEntry doomed{};
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        WsEntry &e = g_ws[slot];
+        (void) hipEventRecord(e.last, (hipStream_t) stream);
+        if (--e.pins == 0 && e.release) {
+            doomed = e;
+            e = WsEntry{};
+        }
+    }
+    ws_free(doomed);
 }
 
 void b64x_release_stream(void *stream)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (int i = 0; i < kWsCache; i++)
-        if (g_ws[i].ws && g_ws[i].dev == dev && g_ws[i].stream == stream)
-            ws_drop(g_ws[i]);
+    WsEntry doomed[kWsCache];
+    int n = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        for (int i = 0; i < kWsCache; i++) {
+            WsEntry &e = g_ws[i];
+            if (!e.ws || e.dev != dev || e.stream != stream) continue;
+            if (e.pins) {
+                e.release = true;  // the last unpin frees it
+            } else {
+                doomed[n++] = e;
+                e = WsEntry{};
+            }
+        }
+    }
+    for (int i = 0; i < n; i++) ws_free(doomed[i]);
 }
 
 __global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres,
@@ -4065,27 +4132,14 @@ static uint32_t next_seq()
     return v;
 }
 
-// b64x_decode_dev, plus an optional host mirror of the result record that
-// the kernels write themselves (sessions; see write_result).
-static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
-                           b64x_dec_result *d_res, b64x_dec_result *h_res,
-                           const b64x_alphabet *abc, unsigned flags, void *d_workspace,
-                           void *stream, uint32_t seq)
+// decode_dev_impl's launches on a given workspace.
+static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
+                         b64x_dec_result *d_res, b64x_dec_result *h_res,
+                         const b64x_alphabet *abc, unsigned flags, void *ws, void *stream,
+                         uint32_t seq, const DeviceInfo *d)
 {
-    if (!d_res) return -EINVAL;
-    if (flags & ~(unsigned) (B64X_DEC_HOLD_TAIL | B64X_DEC_EXPECT_JUNK)) return -EINVAL;
-    if (nchars && (!d_in || !d_out)) return -EINVAL;
-    const DeviceInfo *d = device_info();
-    if (!d) return -ENODEV;
     hipStream_t s = (hipStream_t) stream;
-    if (nchars == 0) {
-        hipLaunchKernelGGL(k_result_zero, dim3(1), dim3(64), 0, s, d_res, h_res,
-                           flags & B64X_DEC_HOLD_TAIL, seq);
-        return launch_status();
-    }
     int err = 0;
-    void *ws = d_workspace ? d_workspace : library_workspace(stream, &err);
-    if (!ws) return err;
     const RangePlan p = plan_ranges(nchars);
     const uint32_t blocks = (p.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const DecAlpha a = dec_alpha(abc);
@@ -4139,12 +4193,58 @@ static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
     return launch_status();
 }
 
+// b64x_decode_dev, plus an optional host mirror of the result record that
+// the kernels write themselves (sessions; see write_result).
+static int decode_dev_impl(const void *d_in, uint64_t nchars, void *d_out,
+                           b64x_dec_result *d_res, b64x_dec_result *h_res,
+                           const b64x_alphabet *abc, unsigned flags, void *d_workspace,
+                           void *stream, uint32_t seq)
+{
+    if (!d_res) return -EINVAL;
+    if (flags & ~(unsigned) (B64X_DEC_HOLD_TAIL | B64X_DEC_EXPECT_JUNK)) return -EINVAL;
+    if (nchars && (!d_in || !d_out)) return -EINVAL;
+    const DeviceInfo *d = device_info();
+    if (!d) return -ENODEV;
+    hipStream_t s = (hipStream_t) stream;
+    if (nchars == 0) {
+        hipLaunchKernelGGL(k_result_zero, dim3(1), dim3(64), 0, s, d_res, h_res,
+                           flags & B64X_DEC_HOLD_TAIL, seq);
+        return launch_status();
+    }
+    if (d_workspace)
+        return decode_dev_ws(d_in, nchars, d_out, d_res, h_res, abc, flags, d_workspace, stream,
+                             seq, d);
+    int err = 0, slot = -1;
+    void *ws = library_workspace(stream, &slot, &err);
+    if (!ws) return err;
+    err = decode_dev_ws(d_in, nchars, d_out, d_res, h_res, abc, flags, ws, stream, seq, d);
+    ws_unpin(slot, stream);
+    return err;
+}
+
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream)
 {
     return decode_dev_impl(d_in, nchars, d_out, d_res, nullptr, abc, flags, d_workspace,
                            stream, next_seq());
+}
+
+int b64x_decode_dev_seq(const void *d_in, uint64_t nchars, void *d_out,
+                        b64x_dec_result *d_res, const b64x_alphabet *abc,
+                        unsigned flags, void *d_workspace, void *stream, uint32_t *seq)
+{
+    const uint32_t q = next_seq();
+    if (seq) *seq = q;
+    return decode_dev_impl(d_in, nchars, d_out, d_res, nullptr, abc, flags, d_workspace,
+                           stream, q);
+}
+
+int b64x_result_check(const b64x_dec_result *res, uint64_t nchars, unsigned flags,
+                      uint32_t seq)
+{
+    if (!res) return -EINVAL;
+    return b64x_result_ok(res, nchars, flags, seq, nullptr) ? 0 : -EAGAIN;
 }
 
 // rv: d_outlen receives alphabet counts V (the hub's jobs) instead of bytes.
@@ -4205,10 +4305,11 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
         const uint64_t e = (uint64_t) magic * S - (1ull << 32);
         const uint64_t relmax = S + (uint64_t) U * kThreads;
         void *ws = nullptr;
+        int slot = -1;
         const uint64_t bitmap = ((uint64_t) nbuf + 63) / 64 * 8 + sizeof(RowModel);
         if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40) &&
             bitmap <= b64x_decode_workspace_size(0) - kWsScratch &&
-            (ws = library_workspace(stream, &err))) {
+            (ws = library_workspace(stream, &slot, &err))) {
             const uint64_t m64 = ~0ull / S + 1;
             const uint64_t per = (uint64_t) U * kThreads;
             const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
@@ -4217,7 +4318,10 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                                                           (uint64_t) d->cus)),
                                dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in, (uint32_t) len,
                                in_stride, (uint32_t) S, out_stride, a, ws);
-            if ((err = launch_status())) return err;
+            if ((err = launch_status())) {
+                ws_unpin(slot, stream);
+                return err;
+            }
             // + S blocks: the row-group mapping rounds the rows up to whole
             // bands of U Ru rows (NB <= S blocks each); spare blocks return
             const dim3 g((uint32_t) ((slots + per - 1) / per + S));
@@ -4229,12 +4333,17 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                                g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, (uint32_t) len, (uint8_t *) d_out,
                                out_stride, (uint32_t) S, magic, m64, slots, tail_slot, a, nbuf, ws);
-            if ((err = launch_status())) return err;
+            if ((err = launch_status())) {
+                ws_unpin(slot, stream);
+                return err;
+            }
             const uint32_t fg = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) /
                                          (64 * kWavesPerBlock), (uint64_t) d->cus * 8);
             hipLaunchKernelGGL(k_rows_finish, dim3(fg), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a, ws);
-            return launch_status();
+            err = launch_status();
+            ws_unpin(slot, stream);
+            return err;
         } else if (err) {
             return err;
         }

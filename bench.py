@@ -208,11 +208,8 @@ def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
     (strong scaling: the batch is fixed, each rank owns 1/N of it), strided
     encode + decode, plus the one exchange step (all-gather of per-rank
     output totals).  Buffer i holds bytes [i L, (i+1) L) of the splitmix64
-    (0x5EED) stream; buffer 0's characters are checked against the G4
-    digest prefix recorded from the reference and every
-    buffer round-trips bit-exactly before timing."""
-    import hashlib
-
+    (0x5EED) stream; every buffer round-trips bit-exactly before timing and
+    the whole output is checked against its digest (_batch_digest_check)."""
     from async_amd import shard
 
     lo, nbuf = shard.by_index(total_buf, world, rank)
@@ -220,9 +217,12 @@ def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
     # decode rows: 12 bytes per 16-character slot (>= capacity; the row kernel
     # writes whole slots, so consecutive rows form one contiguous byte stream)
     cap = 12 * ((Es + 15) // 16)
-    x = torch.empty((lo + nbuf) * L, dtype=torch.uint8, device="cuda")
-    b64.fill_splitmix64(x, 0x5EED)
-    x = x[lo * L:].clone()  # this rank's share of the one stream
+    # this rank's share of the one splitmix64 stream: word k of the stream is
+    # a function of seed + k * 0x9E3779B97F4A7C15, so the share starting at
+    # byte lo*L (a multiple of 8) is the stream of a shifted seed
+    assert (lo * L) % 8 == 0
+    x = torch.empty(nbuf * L, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, (0x5EED + (lo * L // 8) * 0x9E3779B97F4A7C15) % (1 << 64))
     enc = torch.empty(nbuf * Es, dtype=torch.uint8, device="cuda")
     dec = torch.empty(nbuf * cap, dtype=torch.uint8, device="cuda")
     outlen = torch.zeros(nbuf, dtype=torch.int64, device="cuda")
@@ -240,14 +240,7 @@ def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
                                                         x.view(nbuf, L)))
     if not ok:
         raise SystemExit(f"rank {rank}: {name} batch round trip mismatch")
-    g4 = None
-    if lo == 0:
-        want = _golden_digest(f"G4_{L}")
-        if want is not None:
-            got = hashlib.sha256(enc[:Es].cpu().numpy().tobytes()).hexdigest()
-            g4 = got.startswith(want)
-            if not g4:
-                raise SystemExit(f"{name}: buffer 0 does not match the G4_{L} digest")
+    digest = _batch_digest_check(name, lo, nbuf, L, Es, x, enc, dec, cap)
     # warm the exchange path too (first reduction / collective launches load
     # their code objects and set up communicators)
     for _ in range(2):
@@ -301,7 +294,7 @@ def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
         "encode_roofline_frac": alg / (enc_ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
         "decode_roofline_frac": alg / (dec_ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
         "roofline_frac": rank_frac,
-        "g4_digest_ok": g4,
+        "whole_output_check": digest,
         "per_rank_GiB_s": [p[0] for p in per_rank],
         "per_rank_roofline_frac": [p[1] for p in per_rank],
         "per_rank_kernel_ms": [[p[2], p[3]] for p in per_rank],
@@ -310,15 +303,38 @@ def bench_batch(args, world, rank, b64, total_buf=1 << 20, L=1024, name="cfg4"):
     }
 
 
-def _golden_digest(key: str):
-    """A digest prefix from tests/golden/digests.json (recorded from the
-    reference); None when the file is absent."""
+def _batch_digest_check(name, lo, nbuf, L, Es, x, enc, dec, cap):
+    """The batch's whole output against tests/golden/batch_digests.json
+    (oracle-checked, make_golden.py --batch): with every buffer on this rank
+    (N = 1), the SHA-256 of all characters and of the decoded rows (= the
+    input stream's); on a share, every digested chunk of buffers the share
+    holds whole.  Outside the timed region; exits on a mismatch."""
+    import hashlib
     try:
-        with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
-            d = json.load(f)[key]
+        with open(os.path.join(ROOT, "tests", "golden", "batch_digests.json")) as f:
+            g = json.load(f)[name]
     except (OSError, KeyError, ValueError):
         return None
-    return d.get("out_sha256_prefix") or d.get("out_sha256")
+    if g["nbuf"] == nbuf and lo == 0:
+        e_ok = hashlib.sha256(enc.cpu().numpy()).hexdigest() == g["out_sha256"]
+        rows = dec.view(nbuf, cap)[:, :L].contiguous().cpu().numpy()
+        d_ok = hashlib.sha256(rows).hexdigest() == g["in_sha256"]
+        del rows
+        if not (e_ok and d_ok):
+            raise SystemExit(f"{name}: whole-output digest mismatch (encode {e_ok}, "
+                             f"decode {d_ok})")
+        return {"scope": "whole batch", "encode_sha256_ok": e_ok, "decode_sha256_ok": d_ok}
+    c = g["chunk_buffers"]
+    first = (lo + c - 1) // c
+    checked = 0
+    for k in range(first, (lo + nbuf) // c):
+        b0 = k * c - lo
+        got = hashlib.sha256(enc[b0 * Es:(b0 + c) * Es].cpu().numpy()).hexdigest()
+        if got != g["chunk_out_sha256"][k]:
+            raise SystemExit(f"{name}: chunk {k} digest mismatch on this rank")
+        checked += 1
+    return {"scope": f"{checked} chunks of {c} buffers held whole by the rank",
+            "encode_sha256_ok": True if checked else None}
 
 
 def bench_host_inclusive(args, b64):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define B64X_ABI_VERSION 2
+#define B64X_ABI_VERSION 3
 
 /* Alphabet descriptor.  (char) -1 selects the reference's defaults,
  * exactly like base64_encode()/base64_decode() (ref
@@ -112,11 +112,25 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * next; one workspace per stream), or NULL to use a library-owned one
  * per (device, stream) (allocated on the first such call for that stream:
  * that call is not capture-safe).  The library keeps at most 8 such
- * workspaces (about 12.7 MiB of HBM each): a call on a ninth stream waits
- * for the least recently used one's stream and frees its workspace. */
+ * workspaces (about 12.7 MiB of HBM each): a call on a ninth stream frees
+ * the least recently used idle one once the work queued on it has finished
+ * (-EBUSY if all eight are in use by calls being enqueued right then). */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);
+/* b64x_decode_dev, also returning in *seq (may be NULL) the sequence number
+ * the call drew: the `seq` its record holds once it has landed.  A caller
+ * that copies the record back (from any stream) checks it with
+ * b64x_result_check() and so never takes a stale, zero-filled or partly
+ * written record for this call's. */
+int b64x_decode_dev_seq(const void *d_in, uint64_t nchars, void *d_out,
+                        b64x_dec_result *d_res, const b64x_alphabet *abc,
+                        unsigned flags, void *d_workspace, void *stream, uint32_t *seq);
+/* 0 if *res (host memory) is the landed, self-consistent record of the
+ * decode of `nchars` characters with `flags` that drew `seq` (the rules of
+ * b64x_session_decode_result), -EAGAIN if it is not (yet). */
+int b64x_result_check(const b64x_dec_result *res, uint64_t nchars, unsigned flags,
+                      uint32_t seq);
 /* Free the library-owned decode workspace of `stream` on the current device,
  * if it has one (after waiting for the device); call it before destroying a
  * stream that decoded with d_workspace == NULL. */

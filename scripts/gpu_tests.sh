@@ -7,5 +7,5 @@ mkdir -p gpurun_out
 TAG=${TAG:-t}
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_smoke.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/${TAG}_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; tail -5 gpurun_out/${TAG}_pytest.log; exit $rc

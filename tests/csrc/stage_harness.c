@@ -9,20 +9,23 @@
  * Python calls these through ctypes (tests/test_stages_gpu.py).
  */
 #define _GNU_SOURCE
-#define _GNU_SOURCE
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <pthread.h>
+#include <unistd.h>
 
 #include "async.h"
 #include "base64decoder.h"
 #include "base64encoder.h"
 #include "blobstream.h"
 #include "chunkencoder.h"
+#include "fdsink.h"
 #include "fsalloc.h"
 #include "nicestream.h"
+#include "pipestream.h"
 #include "queuestream.h"
 
 /* ---- the reference runner's leak check: test/asynctest.c:108-147 ------ */
@@ -698,6 +701,197 @@ static int egress_mt(const uint8_t *in, const uint64_t *in_off, size_t nmsg, siz
     if (err_out)
         *err_out = err;
     return err ? -1 : 0;
+}
+
+/* ---- the fd ends of the path: pipe/socket -> decoder, encoder -> pipe ---
+ * (bench.py `host_fd`, tests/test_fd_*.py).  A
+ * writer (ingress) or reader (egress) thread sits on the other end of a
+ * pipe or an AF_UNIX socketpair, doing blocking write(2)/read(2), as a
+ * peer process would; the product's loop does the rest. */
+#include <fcntl.h>
+#include <sys/socket.h>
+
+static int make_channel(int fds[2], int sock)
+{
+    if (sock) {
+        if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, fds) < 0)
+            return -1;
+        int sz = 4 << 20;
+        (void) setsockopt(fds[0], SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
+        (void) setsockopt(fds[1], SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
+        return 0;
+    }
+    if (pipe2(fds, O_CLOEXEC) < 0)
+        return -1;
+    (void) fcntl(fds[1], F_SETPIPE_SZ, 1 << 20); /* the default pipe-max-size */
+    return 0;
+}
+
+typedef struct {
+    int fd;
+    const uint8_t *data;
+    size_t n, chunk;
+    uint8_t *out;
+    size_t cap, got;
+    int err;
+    double t_end;
+} peer;
+
+static void *peer_writer(void *arg)
+{
+    peer *p = arg;
+    size_t off = 0;
+    while (off < p->n) {
+        size_t k = p->n - off < p->chunk ? p->n - off : p->chunk;
+        ssize_t w = write(p->fd, p->data + off, k);
+        if (w < 0) {
+            if (errno == EINTR)
+                continue;
+            p->err = errno;
+            break;
+        }
+        off += (size_t) w;
+    }
+    close(p->fd);
+    return NULL;
+}
+
+static void *peer_reader(void *arg)
+{
+    peer *p = arg;
+    for (;;) {
+        size_t room = p->cap - p->got;
+        if (!room) { /* overlong: drain and flag */
+            uint8_t sink[4096];
+            ssize_t r = read(p->fd, sink, sizeof sink);
+            if (r > 0) {
+                p->err = ENOSPC;
+                continue;
+            }
+            break;
+        }
+        ssize_t r = read(p->fd, p->out + p->got, room);
+        if (r < 0) {
+            if (errno == EINTR)
+                continue;
+            p->err = errno;
+            break;
+        }
+        if (r == 0)
+            break;
+        p->got += (size_t) r;
+    }
+    p->t_end = now_s();
+    close(p->fd);
+    return NULL;
+}
+
+/* Ingress: `chars` written into a pipe (or socketpair) by a peer thread in
+ * `write_chunk` pieces -> pipestream -> base64_decode (GPU stage) ->
+ * consumer reading `read_size` at a time into out.  times[0] = wall time
+ * from the first byte written to the consumer's EOF.  Returns the decoded
+ * length or -1 + *err_out. */
+ssize_t h_fd_decode(const uint8_t *chars, size_t n, size_t write_chunk, size_t read_size,
+                    char pos62, char pos63, uint8_t *out, size_t cap, int sock,
+                    int *err_out, double *times)
+{
+    int fds[2];
+    if (make_channel(fds, sock) < 0) {
+        if (err_out)
+            *err_out = errno;
+        return -1;
+    }
+    async_t *async = make_async();
+    if (!async) {
+        close(fds[0]);
+        close(fds[1]);
+        return -1;
+    }
+    pipestream_t *ps = open_pipestream(async, fds[0]);
+    base64decoder_t *dec = base64_decode(async, pipestream_as_bytestream_1(ps), pos62, pos63);
+    peer w = { fds[1], chars, n, write_chunk ? write_chunk : (1 << 20), NULL, 0, 0, 0, 0 };
+    pthread_t th;
+    double t0 = now_s();
+    pthread_create(&th, NULL, peer_writer, &w);
+    ssize_t r = run(async, base64decoder_as_bytestream_1(dec), read_size, out, cap, err_out,
+                    NULL);
+    double t1 = now_s();
+    pthread_join(th, NULL);
+    if (times)
+        times[0] = t1 - t0;
+    if (r >= 0 && w.err) {
+        if (err_out)
+            *err_out = w.err;
+        return -1;
+    }
+    return r;
+}
+
+typedef struct {
+    async_t *async;
+    fdsink_t *sink;
+} sink_watch;
+
+static void sink_finished(sink_watch *sw)
+{
+    async_quit_loop(sw->async);
+}
+
+/* Egress: the `npieces` pieces of `in` (lens[i] bytes each) as blobstreams
+ * on one terminated queuestream -> base64_encode (GPU stage) ->
+ * chunk_encode(max_chunk) -> fdsink (10,240-byte pulls, write(2)) into a
+ * pipe (or socketpair) that a peer thread reads into out.  times[0] = wall
+ * time from the loop's start to the peer's EOF.  Returns the framed length
+ * or -1 + *err_out. */
+ssize_t h_fd_encode(const uint8_t *in, const size_t *lens, size_t npieces, size_t max_chunk,
+                    char pos62, char pos63, int pad, char padchar, uint8_t *out, size_t cap,
+                    int sock, int *err_out, double *times)
+{
+    int fds[2];
+    if (make_channel(fds, sock) < 0) {
+        if (err_out)
+            *err_out = errno;
+        return -1;
+    }
+    async_t *async = make_async();
+    if (!async) {
+        close(fds[0]);
+        close(fds[1]);
+        return -1;
+    }
+    queuestream_t *q = make_queuestream(async);
+    size_t off = 0;
+    for (size_t i = 0; i < npieces; i++) {
+        queuestream_enqueue(q, blobstream_as_bytestream_1(open_blobstream(async, in + off,
+                                                                          lens[i])));
+        off += lens[i];
+    }
+    queuestream_terminate(q);
+    base64encoder_t *e = base64_encode(async, queuestream_as_bytestream_1(q), pos62, pos63,
+                                       pad != 0, padchar);
+    chunkencoder_t *ch = chunk_encode(async, base64encoder_as_bytestream_1(e), max_chunk);
+    peer rd = { fds[0], NULL, 0, 0, out, cap, 0, 0, 0 };
+    pthread_t th;
+    double t0 = now_s();
+    pthread_create(&th, NULL, peer_reader, &rd);
+    sink_watch sw = { async, NULL };
+    sw.sink = open_fdsink(async, chunkencoder_as_bytestream_1(ch), fds[1]);
+    fdsink_register_callback(sw.sink, (action_1) { &sw, (act_1) sink_finished });
+    int rc = fdsink_done(sw.sink) ? 0 : async_loop(async);
+    int err = rc < 0 ? errno : fdsink_error(sw.sink);
+    uint64_t written = fdsink_bytes(sw.sink);
+    fdsink_close(sw.sink);
+    pthread_join(th, NULL);
+    if (times)
+        times[0] = rd.t_end - t0;
+    destroy_async(async);
+    if (!err && rd.err)
+        err = rd.err;
+    if (!err && written != rd.got)
+        err = EPIPE;
+    if (err_out)
+        *err_out = err;
+    return err ? -1 : (ssize_t) rd.got;
 }
 
 /* ---- a small sampling profiler (SIGPROF, process CPU time) ---------------

@@ -20,6 +20,7 @@ Independence: nothing here calls the oracle (oracle/) or the product
     Appendix B rows ``Q`` -> empty, ``QU`` -> ``A``, ``QUI`` -> ``AB``.
 
 Run:  python tests/golden/make_golden.py   (rewrites the JSON files)
+      python tests/golden/make_golden.py --batch   (batch_digests.json)
 """
 from __future__ import annotations
 
@@ -184,6 +185,69 @@ def digests():
     }
 
 
+# ---- configs 3 and 4: whole-output digests ----------------------------
+
+def splitmix64_np(seed: int, n: int, first_word: int = 0):
+    """splitmix64() above, vectorised (numpy), from word `first_word` on."""
+    import numpy as np
+    n8 = (n + 7) // 8
+    with np.errstate(over="ignore"):
+        i = np.arange(first_word + 1, first_word + n8 + 1, dtype=np.uint64)
+        z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").view(np.uint8)[:n]
+
+
+def batch_digests():
+    """SURVEY.md §8(d) configs 3 and 4 pinned by their whole outputs: buffer
+    i is bytes [i L, (i+1) L) of splitmix64(0x5EED), encoded on its own
+    (stdlib, standard alphabet, padded) and laid out back to back
+    (out_stride = E, as bench.py and the tests lay them out).  Recorded:
+      - the SHA-256 of the concatenated characters (the whole output);
+      - the SHA-256 of the concatenated per-buffer SHA-256 digests (each
+        buffer's own digest, checked without holding the whole output);
+      - the SHA-256 of each chunk of `chunk` consecutive buffers' characters
+        (a rank of a sharded run checks the chunks its index range holds);
+      - the input stream's SHA-256 (what every decode must give back);
+      - for config 4, the rows in RFC 2045 lines (76 characters + CRLF; a
+        1,368-character row is exactly 18 lines) and the SHA-256 of that
+        text: its decode is the input stream again.
+    The config-4 row decode in CRLF-76 lines (bench.py `mime_decode`,
+    tests) is checked against `in_sha256`."""
+    out = {}
+    for name, nbuf, L, chunk in (("cfg3", 1 << 16, 4096, 1 << 13),
+                                 ("cfg4", 1 << 20, 1024, 1 << 16)):
+        E = (L + 2) // 3 * 4
+        whole, per_buf, in_h = hashlib.sha256(), hashlib.sha256(), hashlib.sha256()
+        mime = hashlib.sha256() if name == "cfg4" else None
+        chunks = []
+        for c0 in range(0, nbuf, chunk):
+            raw = splitmix64_np(0x5EED, chunk * L, c0 * L // 8).tobytes()
+            in_h.update(raw)
+            ch = hashlib.sha256()
+            for i in range(chunk):
+                e = base64.b64encode(raw[i * L:(i + 1) * L])
+                assert len(e) == E
+                whole.update(e)
+                ch.update(e)
+                per_buf.update(hashlib.sha256(e).digest())
+                if mime is not None:
+                    assert E % 76 == 0
+                    mime.update(b"".join(e[k:k + 76] + b"\r\n" for k in range(0, E, 76)))
+            chunks.append(ch.hexdigest())
+        out[name] = {"nbuf": nbuf, "len": L, "out_len": E, "pattern": "splitmix64",
+                     "seed": 0x5EED, "in_sha256": in_h.hexdigest(),
+                     "out_sha256": whole.hexdigest(),
+                     "per_buffer_sha256_of_sha256": per_buf.hexdigest(),
+                     "chunk_buffers": chunk, "chunk_out_sha256": chunks}
+        if mime is not None:
+            out[name]["crlf76"] = {"row_bytes": E // 76 * 78, "text_sha256": mime.hexdigest(),
+                                   "dec_sha256": in_h.hexdigest()}
+    return out
+
+
 # ---- config 5: Zipf lengths, encoder read counts, chunk framing --------
 
 def zipf_lengths(n_msgs=16384, seed=0x2F, rmax=16384, s=1.1):
@@ -323,6 +387,11 @@ def chunk_fixtures():
 
 
 def main():
+    import sys
+    if "--batch" in sys.argv:  # ~1 minute: 1.25 GiB of synthetic input
+        with open(os.path.join(HERE, "batch_digests.json"), "w") as f:
+            json.dump(batch_digests(), f, indent=1)
+        return
     with open(os.path.join(HERE, "chunk.json"), "w") as f:
         json.dump(chunk_fixtures(), f, indent=1)
     rng = random.Random(0xB64)

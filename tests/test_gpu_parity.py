@@ -211,7 +211,7 @@ def test_g3_1gib_roundtrip():
     assert torch.equal(dd.out[: d["n"]], x)
 
 
-def _strided_check(nbuf, length, sample_idx, g4=None):
+def _strided_check(nbuf, length, sample_idx, g4=None, whole=None):
     qstride_out = b64.encoded_len(length)
     x = torch.empty(nbuf * length, dtype=torch.uint8, device=DEV)
     b64.fill_splitmix64(x, 0x5EED)
@@ -224,6 +224,16 @@ def _strided_check(nbuf, length, sample_idx, g4=None):
         assert ehost[i * qstride_out:(i + 1) * qstride_out].tobytes() == want, i
     if g4:
         assert hashlib.sha256(ehost[:qstride_out].tobytes()).hexdigest().startswith(g4)
+    if whole:
+        # the whole output, not samples: every buffer's characters, laid out
+        # back to back (tests/golden/batch_digests.json, make_golden.py)
+        assert hashlib.sha256(host).hexdigest() == whole["in_sha256"]
+        assert hashlib.sha256(ehost).hexdigest() == whole["out_sha256"]
+        per = hashlib.sha256()
+        rows = ehost.reshape(nbuf, qstride_out)
+        for i in range(nbuf):
+            per.update(hashlib.sha256(rows[i]).digest())
+        assert per.hexdigest() == whole["per_buffer_sha256_of_sha256"]
     # exact-capacity rows (per-slot kernel) and 16-byte rows (the uniform
     # row kernel needs out_stride >= 12 * ceil(E/16))
     for cap in (b64.decoded_cap(qstride_out), (b64.decoded_cap(qstride_out) + 15) // 16 * 16):
@@ -232,6 +242,11 @@ def _strided_check(nbuf, length, sample_idx, g4=None):
         b64.decode_strided(enc, qstride_out, qstride_out, nbuf, dec, cap, outlen)
         assert int(outlen.min()) == length and int(outlen.max()) == length
         assert torch.equal(dec.view(nbuf, cap)[:, :length], x.view(nbuf, length))
+        if whole:  # the decoded rows, whole, against the input stream's digest
+            got = dec.view(nbuf, cap)[:, :length].contiguous().cpu().numpy()
+            assert hashlib.sha256(got).hexdigest() == whole["in_sha256"]
+            del got
+        del dec
 
 
 def test_strided_small_shapes():
@@ -338,7 +353,8 @@ def test_strided_rows_last_slot_shapes(E):
 def test_strided_cfg3_full():
     """65,536 x 4 KiB (BASELINE config 3)."""
     d = util.golden("digests.json")
-    _strided_check(65536, 4096, [0, 1, 2, 31337, 65535], d["G4_4096"]["out_sha256_prefix"])
+    _strided_check(65536, 4096, [0, 1, 2, 31337, 65535], d["G4_4096"]["out_sha256_prefix"],
+                   util.golden("batch_digests.json")["cfg3"])
 
 
 @pytest.mark.slow
@@ -346,7 +362,32 @@ def test_strided_cfg4_full():
     """1,048,576 x 1 KiB (BASELINE config 4, one GPU's worth)."""
     d = util.golden("digests.json")
     _strided_check(1 << 20, 1024, [0, 1, 777777, (1 << 20) - 1],
-                   d["G4_1024"]["out_sha256_prefix"])
+                   d["G4_1024"]["out_sha256_prefix"], util.golden("batch_digests.json")["cfg4"])
+
+
+@pytest.mark.slow
+def test_strided_cfg4_crlf76_full():
+    """Config 4's rows in RFC 2045 lines (18 x (76 + CRLF) = 1,404 bytes per
+    row), decoded by the row kernel: the text and the decoded rows, whole,
+    against tests/golden/batch_digests.json."""
+    g = util.golden("batch_digests.json")["cfg4"]
+    nbuf, L, E = g["nbuf"], g["len"], g["out_len"]
+    D = g["crlf76"]["row_bytes"]
+    x = torch.empty(nbuf * L, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0x5EED)
+    enc = torch.empty(nbuf * E, dtype=torch.uint8, device=DEV)
+    b64.encode_strided(x, L, L, nbuf, enc, E)
+    crlf = torch.tensor([13, 10], dtype=torch.uint8, device=DEV).expand(nbuf, E // 76, 2)
+    text = torch.cat([enc.view(nbuf, E // 76, 76), crlf], dim=2).reshape(-1).contiguous()
+    del enc
+    assert hashlib.sha256(text.cpu().numpy()).hexdigest() == g["crlf76"]["text_sha256"]
+    cap = 12 * ((D + 15) // 16)
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    b64.decode_strided(text, D, D, nbuf, dec, cap, outlen)
+    assert int(outlen.min()) == L and int(outlen.max()) == L
+    got = dec.view(nbuf, cap)[:, :L].contiguous().cpu().numpy()
+    assert hashlib.sha256(got).hexdigest() == g["crlf76"]["dec_sha256"]
 
 
 def test_ragged_batch_vs_oracle():
@@ -871,3 +912,86 @@ def test_library_workspace_is_bounded():
         lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
     run(keep[5])  # a released stream gets a fresh workspace
     lib.b64x_release_stream(ctypes.c_void_p(keep[5].cuda_stream))
+
+
+def test_library_workspace_threads_past_the_cache():
+    """12 threads, each decoding on its own stream with d_workspace == NULL
+    (more streams than the 8 cached workspaces, so entries are evicted while
+    other threads are enqueuing): an entry handed out is pinned until its
+    call's kernels are queued and an event is recorded behind them, and
+    eviction waits on that event, not the device -- every decode stays
+    exact (the unpinned LRU could free a workspace between its
+    lookup and the launches that use it).  The threads make only C calls
+    (the library, hipStreamSynchronize, hipMemcpyAsync); buffers, streams
+    and the checks are the main thread's."""
+    import ctypes
+    import threading
+
+    from async_amd import _lib
+    lib = _lib.load()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_int, ctypes.c_void_p]
+    rng = np.random.default_rng(41)
+    jobs = []
+    for k in range(12):
+        raw = rng.integers(0, 256, 200000 + 977 * k, dtype=np.uint8)
+        text = _junk(rng, orc.encode(raw), 0.003) if k % 2 else \
+            b"\r\n".join(orc.encode(raw)[i:i + 76] for i in range(0, 300000, 76))
+        x = dev(text)
+        out = torch.zeros(b64.decoded_cap(x.numel()), dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+        jobs.append({"raw": raw, "x": x, "out": out, "res": res, "st": torch.cuda.Stream(),
+                     "ok": 0, "err": None})
+    torch.cuda.synchronize()
+    a = b64._abc(None)
+
+    def worker(j):
+        try:
+            st = ctypes.c_void_p(j["st"].cuda_stream)
+            rec = b64.DecResult()
+            for rep in range(6):
+                seq = ctypes.c_uint32(0)
+                rc = lib.b64x_decode_dev_seq(ctypes.c_void_p(j["x"].data_ptr()), j["x"].numel(),
+                                             ctypes.c_void_p(j["out"].data_ptr()),
+                                             ctypes.c_void_p(j["res"].data_ptr()),
+                                             ctypes.byref(a), 0, None, st, ctypes.byref(seq))
+                if rc == -16:  # -EBUSY: every cached entry mid-enqueue
+                    continue
+                assert rc == 0, rc
+                assert hip.hipMemcpyAsync(ctypes.addressof(rec), j["res"].data_ptr(),
+                                          b64.RES_BYTES, 2, st) == 0
+                assert hip.hipStreamSynchronize(st) == 0
+                assert lib.b64x_result_check(ctypes.byref(rec), j["x"].numel(), 0,
+                                             seq.value) == 0
+                assert rec.out_len == j["raw"].size
+                j["ok"] += 1
+            lib.b64x_release_stream(st)
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            j["err"] = e
+
+    th = [threading.Thread(target=worker, args=(j,), daemon=True) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th)
+    for j in jobs:
+        assert j["err"] is None, j["err"]
+        assert j["ok"] >= 1
+        assert np.array_equal(j["out"][:j["raw"].size].cpu().numpy(), j["raw"])
+
+
+def test_decoded_info_checks_the_record():
+    """Decoded.info() waits for the decode's own stream and refuses a record
+    that does not name the call."""
+    raw = np.arange(3000, dtype=np.uint8)
+    x = dev(orc.encode(raw))
+    st = torch.cuda.Stream()
+    d = b64.decode(x, stream=st)
+    assert d.seq != 0 and d.nchars == x.numel()
+    assert d.info().out_len == raw.size
+    stale = b64.Decoded(d.out, d.result, d.nchars, d.flags, d.seq + 1, st)
+    with pytest.raises(b64.B64xError):
+        stale.info()

@@ -152,3 +152,50 @@ def test_oracle_rows_match_stdlib():
         dec = np.zeros((37, (E + 3) // 4 * 3), np.uint8)
         assert pyoracle.decode_rows(np.ascontiguousarray(enc[:, :E]), dec) == 37 * L
         assert np.array_equal(dec[:, :L], rows)
+
+
+def _rows_parallel(fn, src, dst, threads=8):
+    """Run an oracle row function over slices of rows on `threads` threads
+    (ctypes drops the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = src.shape[0]
+    sl = [slice(i * n // threads, (i + 1) * n // threads) for i in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda q: fn(src[q], dst[q]), sl))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cfg", ["cfg3", "cfg4"])
+def test_batch_whole_output_digests(cfg):
+    """SURVEY.md §8(d) configs 3 and 4 pinned by their whole outputs: the
+    oracle (one reference encoder per buffer, read with one full read)
+    reproduces tests/golden/batch_digests.json -- the digest of all
+    characters, of the per-buffer digests and of every chunk -- and its
+    decoder gives the input back; for config 4 also from the rows in
+    CRLF-76 lines (decode digest = the input's)."""
+    import numpy as np
+    g = util.golden("batch_digests.json")[cfg]
+    nbuf, L, E = g["nbuf"], g["len"], g["out_len"]
+    x = util.splitmix64(g["seed"], nbuf * L).reshape(nbuf, L)
+    assert hashlib.sha256(x).hexdigest() == g["in_sha256"]
+    enc = np.empty((nbuf, E), dtype=np.uint8)
+    _rows_parallel(orc.encode_rows, x, enc)
+    assert hashlib.sha256(enc).hexdigest() == g["out_sha256"]
+    per = hashlib.sha256()
+    for i in range(nbuf):
+        per.update(hashlib.sha256(enc[i]).digest())
+    assert per.hexdigest() == g["per_buffer_sha256_of_sha256"]
+    c = g["chunk_buffers"]
+    assert [hashlib.sha256(enc[i:i + c]).hexdigest()
+            for i in range(0, nbuf, c)] == g["chunk_out_sha256"]
+    if "crlf76" in g:
+        lines = E // 76
+        crlf = np.broadcast_to(np.frombuffer(b"\r\n", np.uint8), (nbuf, lines, 2))
+        text = np.concatenate([enc.reshape(nbuf, lines, 76), crlf], axis=2).reshape(nbuf, -1)
+        del enc
+        assert text.shape[1] == g["crlf76"]["row_bytes"]
+        assert hashlib.sha256(text).hexdigest() == g["crlf76"]["text_sha256"]
+        enc = text
+    dec = np.empty((nbuf, (enc.shape[1] + 3) // 4 * 3), dtype=np.uint8)
+    _rows_parallel(orc.decode_rows, enc, dec)
+    assert hashlib.sha256(np.ascontiguousarray(dec[:, :L])).hexdigest() == g["in_sha256"]

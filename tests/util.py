@@ -131,6 +131,12 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_prof_stop.argtypes = [ctypes.c_char_p]
     L.h_device_count.argtypes = []
     L.h_device_count.restype = ctypes.c_int
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.h_fd_decode.argtypes = [vp, sz, sz, sz, ch, ch, vp, sz, ctypes.c_int, ip, dp]
+    L.h_fd_decode.restype = ssz
+    L.h_fd_encode.argtypes = [vp, vp, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ctypes.c_int,
+                              ip, dp]
+    L.h_fd_encode.restype = ssz
     return L
 
 
@@ -315,3 +321,57 @@ def ingress_stacks(msgs, read_size: int, pos62=-1, pos63=-1, times=None, lib=Non
         return None, err.value
     return [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
             for i in range(lens.size)], 0
+
+
+def fd_decode(chars, write_chunk=1 << 20, read_size=1 << 18, pos62=-1, pos63=-1, sock=False,
+              out=None, lib=None):
+    """Ingress through a real fd: a peer thread writes `chars` into a pipe
+    (or AF_UNIX socketpair) -> pipestream -> base64_decode stage -> consumer.
+    Returns (decoded bytes as a numpy view | None, errno, seconds)."""
+    src = np.frombuffer(chars, np.uint8) if isinstance(chars, (bytes, bytearray)) else \
+        np.ascontiguousarray(chars, dtype=np.uint8)
+    cap = src.size // 4 * 3 + 16
+    if out is None:
+        out = np.empty(cap, np.uint8)
+    err = ctypes.c_int(0)
+    t = (ctypes.c_double * 1)()
+    n = _lib_or_default(lib).h_fd_decode(src.ctypes.data if src.size else None, src.size,
+                                         write_chunk, read_size, cch(pos62), cch(pos63),
+                                         out.ctypes.data, out.size, int(bool(sock)),
+                                         ctypes.byref(err), t)
+    return (None if n < 0 else out[:n]), err.value, t[0]
+
+
+def fd_encode(data, pieces=None, max_chunk=1 << 20, pos62=-1, pos63=-1, pad=True, padchar=-1,
+              sock=False, out=None, lib=None):
+    """Egress through a real fd: `data` (split into `pieces` lengths) on a
+    queuestream -> base64_encode stage -> chunk_encode(max_chunk) -> fdsink
+    (10,240-byte pulls, write(2)) -> a pipe a peer thread drains.  Returns
+    (framed bytes as a numpy view | None, errno, seconds)."""
+    src = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else \
+        np.ascontiguousarray(data, dtype=np.uint8)
+    lens = np.asarray(pieces if pieces is not None else [src.size], dtype=np.uintp)
+    cap = framed_cap(src.size, max_chunk)
+    if out is None:
+        out = np.empty(cap, np.uint8)
+    err = ctypes.c_int(0)
+    t = (ctypes.c_double * 1)()
+    n = _lib_or_default(lib).h_fd_encode(src.ctypes.data if src.size else None,
+                                         lens.ctypes.data, lens.size, max_chunk, cch(pos62),
+                                         cch(pos63), int(bool(pad)), cch(padchar),
+                                         out.ctypes.data, out.size, int(bool(sock)),
+                                         ctypes.byref(err), t)
+    return (None if n < 0 else out[:n]), err.value, t[0]
+
+
+def dechunk(framed: bytes) -> bytes:
+    """The payload of an HTTP/1.1 chunked body (chunkencoder's framing)."""
+    out, pos = bytearray(), 0
+    while True:
+        eol = framed.index(b"\r\n", pos)
+        size = int(framed[pos:eol], 16)
+        pos = eol + 2
+        if size == 0:
+            return bytes(out)
+        out += framed[pos:pos + size]
+        pos += size + 2
