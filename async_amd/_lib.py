@@ -105,8 +105,9 @@ SIGNATURES = {
     "b64x_lane_release": (None, [_vp]),
     "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp, _vp]),
     "b64x_lane_encode_check": (_int, [_vp]),
-    "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _ap, _vp, _vp]),
-    "b64x_lane_decode_check": (_int, [_vp, _vp, _vp, _vp, _u32]),
+    "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ap,
+                                      _vp, _vp, ctypes.POINTER(_u32)]),
+    "b64x_lane_decode_check": (_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "b64x_lane_wait": (_int, [_vp]),
     "b64x_diag_counters": (None, [ctypes.POINTER(_u64)]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),

@@ -49,6 +49,9 @@ enum {
     HUB_JOBS = 1 << 16,     /* jobs per arena */
     HUB_DEPTH = 8,          /* reservations open at once (stages reading
                                through stages, see b64_hub_reserve) */
+    LANE_QUEUE = 4,         /* decode batches queued on one lane: a batch
+                               whose chained jobs continue streams of a batch
+                               in flight on that lane waits behind it there */
 };
 
 typedef enum { B_FREE, B_FILLING, B_READY, B_INFLIGHT, B_DONE } batch_state;
@@ -60,6 +63,15 @@ struct b64_batch {
     uint64_t *h_in_off, *h_out_off; /* pinned, HUB_JOBS + 1 each */
     uint8_t *h_flags;            /* pinned, HUB_JOBS: decode jobs' flags */
     b64x_dec_result *h_res;      /* pinned, HUB_JOBS: decode jobs' records */
+    b64x_dec_result *h_spell;    /* pinned, HUB_JOBS: chained jobs' spell logs */
+    const b64x_dec_result **h_prev; /* HUB_JOBS: chained jobs' predecessor records */
+    b64_batch *after;            /* a batch in flight (or ready) whose records
+                                    chained jobs of this one read: this one
+                                    runs behind it on its lane */
+    unsigned after_refs;         /* references this batch holds on `after` */
+    b64_batch *lane_next;        /* the lane's queue of batches in flight */
+    int lane;                    /* lane it runs on, -1 before launch */
+    uint32_t seq;                /* decode batches: the lane's sequence number */
     b64_hub_kind kind;
     b64_ticket **jobs;
     size_t in_cap, out_cap;
@@ -78,7 +90,8 @@ struct b64_hub {
     unsigned users;
     int efd;
     b64x_lane *lanes[HUB_LANES];
-    b64_batch *running[HUB_LANES];
+    b64_batch *lane_head[HUB_LANES], *lane_tail[HUB_LANES]; /* in flight, in order */
+    unsigned lane_depth[HUB_LANES];
     b64_batch *filling[HUB_DEPTH]; /* the open arena of each nesting level */
     unsigned depth;              /* reservations open (gathers in progress) */
     b64_batch *ready, *ready_tail;
@@ -146,6 +159,8 @@ static void batch_free(b64_batch *b)
     b64x_host_free(b->h_out_off);
     b64x_host_free(b->h_flags);
     b64x_host_free(b->h_res);
+    b64x_host_free(b->h_spell);
+    free(b->h_prev);
     free(b->jobs);
     free(b);
 }
@@ -165,9 +180,12 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     b->h_out_off = b64x_host_alloc((HUB_JOBS + 1) * sizeof(uint64_t));
     b->h_flags = b64x_host_alloc(HUB_JOBS);
     b->h_res = b64x_host_alloc(HUB_JOBS * sizeof(b64x_dec_result));
+    b->h_spell = b64x_host_alloc(HUB_JOBS * sizeof(b64x_dec_result));
+    b->h_prev = calloc(HUB_JOBS, sizeof *b->h_prev);
     b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
+    b->lane = -1;
     if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_flags || !b->h_res ||
-        !b->jobs) {
+        !b->h_spell || !b->h_prev || !b->jobs) {
         batch_free(b);
         errno = ENOMEM;
         return NULL;
@@ -185,6 +203,10 @@ static void batch_put(b64_batch *b)
     b->njobs = 0;
     b->err = 0;
     b->hub = NULL;
+    b->after = NULL;
+    b->after_refs = 0;
+    b->lane_next = NULL;
+    b->lane = -1;
     atomic_store_explicit(&b->done, 0, memory_order_relaxed);
     pthread_once(&pool_once, pool_init);
     pthread_mutex_lock(&pool_lock);
@@ -205,6 +227,20 @@ static void batch_recycle(b64_hub *h, b64_batch *b)
     h->live--;
     if (h->nwaiters)
         schedule_kick(h);
+}
+
+/* This batch no longer reads its `after` batch's records. */
+static void batch_drop_after(b64_hub *h, b64_batch *b)
+{
+    b64_batch *a = b->after;
+    if (!a)
+        return;
+    unsigned n = b->after_refs;
+    b->after = NULL;
+    b->after_refs = 0;
+    a->refs -= n;
+    if (a->refs == 0 && a->state == B_DONE)
+        batch_recycle(h, a);
 }
 
 static b64_batch *batch_get(b64_hub *h, size_t need)
@@ -265,18 +301,43 @@ static void seal(b64_hub *h, unsigned level)
     }
 }
 
+/* The lane a ready batch goes to: behind the batch its chained jobs read
+ * from while that one is in flight (its lane's queue has room), else an
+ * idle lane; -1 when it has to wait. */
+static int pick_lane(b64_hub *h, const b64_batch *b)
+{
+    if (b->after && b->after->state == B_INFLIGHT) {
+        int i = b->after->lane;
+        return h->lane_depth[i] < LANE_QUEUE ? i : -1;
+    }
+    for (int i = 0; i < HUB_LANES; i++)
+        if (!h->lane_depth[i])
+            return i;
+    return -1;
+}
+
 static void launch_ready(b64_hub *h)
 {
     double t0 = h->tr.on ? mono_s() : 0;
-    for (int i = 0; i < HUB_LANES && h->ready; i++) {
-        if (h->running[i])
-            continue;
+    /* in order: a batch that must wait keeps every later one waiting (a
+     * batch's `after` is always ahead of it) */
+    while (h->ready) {
         b64_batch *b = h->ready;
+        int i = pick_lane(h, b);
+        if (i < 0)
+            break;
         h->ready = b->next;
         if (!h->ready)
             h->ready_tail = NULL;
         b->state = B_INFLIGHT;
-        h->running[i] = b;
+        b->lane = i;
+        b->lane_next = NULL;
+        if (h->lane_tail[i])
+            h->lane_tail[i]->lane_next = b;
+        else
+            h->lane_head[i] = b;
+        h->lane_tail[i] = b;
+        h->lane_depth[i]++;
         h->inflight++;
         int rc = 0;
         if (!h->lanes[i] && !(h->lanes[i] = b64x_lane_acquire()))
@@ -285,7 +346,8 @@ static void launch_ready(b64_hub *h)
             rc = b->kind == B64_HUB_DECODE
                      ? b64x_lane_decode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
                                               b->h_out, b->h_out_off, b->h_flags, b->h_res,
-                                              &b->abc, batch_done, b)
+                                              b->h_prev, b->h_spell, &b->abc, batch_done, b,
+                                              &b->seq)
                      : b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
                                               b->h_out, b->h_out_off, &b->abc, batch_done, b);
         if (rc) { /* report through the normal completion path */
@@ -422,6 +484,7 @@ static void complete(b64_hub *h, b64_batch *b, bool collect)
             push_wake(h, t->wake);
     }
     b->state = B_DONE;
+    batch_drop_after(h, b);
     if (b->refs == 0)
         batch_recycle(h, b);
 }
@@ -442,18 +505,27 @@ static void hub_wake(b64_hub *h)
     h->in_wake = true;
     h->nwakes = 0;
     for (int i = 0; i < HUB_LANES; i++) {
-        b64_batch *b = h->running[i];
-        if (b && atomic_load_explicit(&b->done, memory_order_acquire)) {
-            h->running[i] = NULL;
+        /* a lane's batches finish in the order they were queued */
+        b64_batch *b;
+        while ((b = h->lane_head[i]) && atomic_load_explicit(&b->done, memory_order_acquire)) {
+            h->lane_head[i] = b->lane_next;
+            if (!h->lane_head[i])
+                h->lane_tail[i] = NULL;
+            h->lane_depth[i]--;
             h->inflight--;
             /* the batch's records or completion stamp, checked (and
              * waited for, should the callback have come early) before
              * anything of it is read */
             if (!b->err)
                 b->err = b->kind == B64_HUB_DECODE
-                             ? b64x_lane_decode_check(h->lanes[i], b->h_in_off, b->h_flags,
-                                                      b->h_res, b->njobs)
+                             ? b64x_lane_decode_check(h->lanes[i], b->seq, b->h_in_off,
+                                                      b->h_flags, b->h_res, b->h_prev,
+                                                      b->h_spell, b->njobs)
                              : b64x_lane_encode_check(h->lanes[i]);
+            if (b->err && b->kind == B64_HUB_DECODE) /* chained successors read its records */
+                for (b64_batch *q = h->lane_head[i]; q; q = q->lane_next)
+                    if (q->after == b && !q->err)
+                        q->err = b->err;
             complete(h, b, true);
         }
     }
@@ -507,6 +579,17 @@ b64_hub *b64_hub_acquire(async_t *async)
     return h;
 }
 
+/* Teardown: back to the pool, with the references it held on a finished
+ * batch (which nothing else holds any more: every stage is gone). */
+static void teardown_put(b64_batch *b)
+{
+    b64_batch *a = b->after;
+    unsigned n = b->after_refs;
+    batch_put(b);
+    if (a && a->state == B_DONE && (a->refs -= n) == 0)
+        batch_put(a);
+}
+
 static void hub_teardown(b64_hub *h)
 {
     h->dead = true;
@@ -527,20 +610,24 @@ static void hub_teardown(b64_hub *h)
     }
     pthread_mutex_unlock(&registry_lock);
     for (int i = 0; i < HUB_LANES; i++) {
-        if (h->running[i]) { /* teardown: wait, do not wake anyone */
+        if (h->lane_head[i]) /* teardown: wait, do not wake anyone */
             (void) b64x_lane_wait(h->lanes[i]);
-            batch_put(h->running[i]);
-            h->running[i] = NULL;
+        while (h->lane_head[i]) {
+            b64_batch *b = h->lane_head[i];
+            h->lane_head[i] = b->lane_next;
+            teardown_put(b);
         }
+        h->lane_tail[i] = NULL;
+        h->lane_depth[i] = 0;
         b64x_lane_release(h->lanes[i]);
     }
     for (unsigned l = 0; l < HUB_DEPTH; l++)
         if (h->filling[l])
-            batch_put(h->filling[l]);
+            teardown_put(h->filling[l]);
     while (h->ready) {
         b64_batch *b = h->ready;
         h->ready = b->next;
-        batch_put(b);
+        teardown_put(b);
     }
     (void) async_unregister(h->async, h->efd);
     close(h->efd);
@@ -639,12 +726,36 @@ uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc
     return b->h_in + b->in_used;
 }
 
+bool b64_hub_chainable(b64_hub *h, const b64_ticket *prev)
+{
+    const b64_batch *p = prev->batch;
+    if (!h->depth || !p || atomic_load_explicit(&prev->done, memory_order_acquire))
+        return false;
+    const b64_batch *b = h->filling[h->depth - 1];
+    if (p == b)
+        return true; /* earlier job of the same batch */
+    if (p->state != B_READY && p->state != B_INFLIGHT)
+        return false; /* filling at another nesting level */
+    return !b->after || b->after == p;
+}
+
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
-                    unsigned flags, action_1 wake)
+                    unsigned flags, const b64_ticket *prev, action_1 wake)
 {
     b64_batch *b = h->filling[--h->depth];
     uint32_t j = b->njobs++;
     b->h_flags[j] = (uint8_t) flags;
+    b->h_prev[j] = NULL;
+    if (prev) { /* b64_hub_chainable() said yes */
+        b64_batch *p = prev->batch;
+        b->h_flags[j] |= B64X_LANE_CHAINED;
+        b->h_prev[j] = p->h_res + prev->index;
+        if (p != b) { /* p's records must outlive b's kernels */
+            b->after = p;
+            b->after_refs++;
+            p->refs++;
+        }
+    }
     b->h_in_off[j] = b->in_used;
     b->in_used += n;
     b->h_in_off[j + 1] = b->in_used;

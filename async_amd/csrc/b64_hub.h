@@ -71,13 +71,24 @@ uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc
  * thousands of stages: scanning them on every close would be quadratic. */
 void b64_hub_forget(b64_hub *h, void *obj, bool waiting);
 /* Turn the reservation into a job of n bytes -> out_len characters
+ * (`prev`: NULL, or as b64_hub_chainable() allowed)
  * (encode) or of n characters -> at most out_len bytes (decode; `flags`
  * B64X_DEC_HOLD_TAIL when more of the stream follows: whole groups only,
  * the last V mod 4 sextets reported; 0 ends the stream: its final partial
  * group emitted).  A decode job's record lands in ticket->res, its byte
  * count in ticket->out_len. */
 void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
-                    unsigned flags, action_1 wake);
+                    unsigned flags, const b64_ticket *prev, action_1 wake);
+/* Decoder streams in blocks (the stage's carry): while
+ * a reservation is open, may the job about to be committed take its 0-3
+ * carried sextets on the device from `prev`, a job of the same stream whose
+ * record the host has not seen yet?  Yes when `prev` is an earlier job of
+ * the arena being filled, or of a batch that is ready or in flight (this
+ * arena's batch then runs behind it on its lane; it can follow one such
+ * batch only).  The job is then committed with `prev` (a 4-character head
+ * of non-alphabet characters first): the device spells prev's held-back
+ * sextets into the head between prev's decode and its own. */
+bool b64_hub_chainable(b64_hub *h, const b64_ticket *prev);
 void b64_hub_cancel(b64_hub *h);
 /* The stage is done with the ticket (consumed, or closing before the
  * batch finished: its output is then discarded). */

@@ -29,12 +29,13 @@
  *    :61-99);
  *  - decoder: blocks are decoded with B64X_DEC_HOLD_TAIL; the device
  *    reports the 0-3 sextets a block leaves over (its result record), and
- *    the stage spells them as alphabet characters in a 4-byte head in
- *    front of the stream's next block (the reference keeps those bits in
- *    decoder->bits across reads, :64-76).  So a decoder stream has one
- *    block on the GPU at a time; finished blocks still queue up for the
- *    consumer.  At EOF the last block (or a head alone) is decoded without
- *    HOLD_TAIL, giving the reference's floor(6V/8) bytes overall.
+ *    they are spelled as alphabet characters in a 4-byte head in front of
+ *    the stream's next block (the reference keeps those bits in
+ *    decoder->bits across reads, :64-76) -- by the host when the block
+ *    before has finished, by the device (a chained job, b64_hub.h) while
+ *    it is still in flight, so a decoder stream keeps up to NSLOTS blocks
+ *    on the GPU.  At EOF the last block (or a head alone) is decoded
+ *    without HOLD_TAIL, giving the reference's floor(6V/8) bytes overall.
  *
  * The byte stream each stage produces is the reference's, byte for byte,
  * and the encoder's per-read counts are too whenever upstream keeps up
@@ -91,6 +92,8 @@ typedef struct {
     stage *owner;
     b64_ticket ticket;  /* this slot's job in a hub batch */
     bool hold;          /* decoder: more of the stream follows this block */
+    bool carry_out;     /* decoder: the next block took this one's held-back
+                           sextets on the device (b64_hub_chainable) */
     bool resolved;      /* out_len/body_end valid (decoder: after done) */
     size_t out_pos;
     size_t body_end;    /* encoder: end of the full sextets; the finalize
@@ -296,6 +299,7 @@ static void slot_arm(stage *st, slot *sl)
 {
     sl->resolved = false;
     sl->hold = false;
+    sl->carry_out = false;
     sl->out_pos = sl->body_end = sl->out_len = 0;
     st->nbusy++;
 }
@@ -382,7 +386,7 @@ static int top_up_encoder(stage *st)
         }
         slot_arm(st, sl);
         sl->out_len = (size_t) b64x_encoded_len(total, st->abc.pad);
-        b64_hub_commit(st->hub, &sl->ticket, total, sl->out_len, 0,
+        b64_hub_commit(st->hub, &sl->ticket, total, sl->out_len, 0, NULL,
                        (action_1) { st, (act_1) stage_notify });
         sl->out_pos = skip;
         sl->body_end = total * 8 / 6;
@@ -399,15 +403,22 @@ static int top_up_encoder(stage *st)
 
 static bool slot_ready(slot *sl);
 
-/* Decoder blocks: each one a hub job of DEC_HEAD + n characters, the head
- * spelling the sextets the previous block held back (skip characters when
- * none), so a block is launched once the one before it has finished. */
+/* Decoder blocks: each one a hub job of DEC_HEAD + n characters whose head
+ * carries the 0-3 sextets the previous block held back (the reference keeps
+ * them in decoder->bits across reads, base64decoder.c:64-76).  When the
+ * previous block has finished, the host spells them into the head.  While
+ * it is still queued or on the GPU, the block is chained to it
+ * (b64_hub_chainable): the device spells them between the two decodes, in
+ * stream order on one lane, so a stream keeps up to NSLOTS blocks in
+ * flight.  A block that cannot be chained (its predecessor is filling at
+ * another nesting level, or the arena follows another batch) waits for the
+ * predecessor's completion. */
 static int top_up_decoder(stage *st)
 {
     slot *sl;
     while ((sl = next_launch_slot(st))) {
-        if (st->nbusy && !slot_ready(&st->slots[(st->head + st->nbusy - 1) % NSLOTS]))
-            return 0; /* its completion brings us back */
+        slot *last = st->nbusy ? &st->slots[(st->head + st->nbusy - 1) % NSLOTS] : NULL;
+        const bool pending = last && !slot_ready(last); /* its carry is not known here */
         size_t room;
         action_1 waiter = hub_waiter(st);
         size_t want = DEC_HEAD + st->cap;
@@ -416,12 +427,16 @@ static int top_up_decoder(stage *st)
                                       waiter);
         if (!in)
             return reserve_failed(st, waiter);
+        if (pending && !b64_hub_chainable(st->hub, &last->ticket)) {
+            b64_hub_cancel(st->hub);
+            return 0; /* its completion brings us back */
+        }
         bool eof;
         int uerr;
         size_t got = gather(st, in + DEC_HEAD, room - DEC_HEAD, &eof, &uerr);
         if (eof) {
             st->final_queued = true;
-            if (got == 0 && st->ncarry == 0) { /* nothing held back: done */
+            if (got == 0 && !pending && st->ncarry == 0) { /* nothing held back: done */
                 b64_hub_cancel(st->hub);
                 return 0;
             }
@@ -435,9 +450,12 @@ static int top_up_decoder(stage *st)
         st->ncarry = 0;
         slot_arm(st, sl);
         sl->hold = !eof;
+        if (pending)
+            last->carry_out = true;
         b64_hub_commit(st->hub, &sl->ticket, DEC_HEAD + got,
                        (size_t) b64x_decoded_cap(DEC_HEAD + got),
-                       eof ? 0u : B64X_DEC_HOLD_TAIL, (action_1) { st, (act_1) stage_notify });
+                       eof ? 0u : B64X_DEC_HOLD_TAIL, pending ? &last->ticket : NULL,
+                       (action_1) { st, (act_1) stage_notify });
         if (uerr)
             return uerr;
     }
@@ -460,7 +478,7 @@ static bool slot_ready(slot *sl)
         sl->out_len = sl->ticket.err ? 0 : sl->ticket.out_len;
         sl->body_end = sl->out_len;
         sl->resolved = true;
-        if (sl->hold && !sl->ticket.err) {
+        if (sl->hold && !sl->carry_out && !sl->ticket.err) {
             st->ncarry = sl->ticket.res.tail_n < 4 ? sl->ticket.res.tail_n : 0;
             memcpy(st->carry, sl->ticket.res.tail, st->ncarry);
         }

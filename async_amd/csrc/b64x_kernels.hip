@@ -2760,6 +2760,7 @@ struct BatchLayout {
     const uint64_t *out_off;  // nbuf offsets, or null
     uint64_t in_stride, out_stride, len;
     uint64_t big;             // ragged: jobs of >= big characters are skipped (0: none)
+    const uint8_t *flags;     // ragged: jobs flagged B64X_LANE_CHAINED are skipped too
 };
 
 DEV void batch_buf(const BatchLayout &L, uint32_t b, uint64_t &beg, uint64_t &len,
@@ -2769,7 +2770,8 @@ DEV void batch_buf(const BatchLayout &L, uint32_t b, uint64_t &beg, uint64_t &le
         beg = L.in_off[b];
         len = L.in_off[b + 1] - beg;
         obeg = L.out_off[b];
-        if (L.big && len >= L.big) len = 0;  // decoded by the single-buffer pipeline
+        // decoded by the single-buffer pipeline: big and chained jobs
+        if ((L.big && len >= L.big) || (L.flags && (L.flags[b] & B64X_LANE_CHAINED))) len = 0;
     } else {
         beg = (uint64_t) b * L.in_stride;
         len = L.len;
@@ -3652,7 +3654,8 @@ __global__ __launch_bounds__(kThreads) void k_batch_finish(
     for (uint32_t j = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
          j < njobs; j += nw) {
         const uint64_t beg = in_off[j], n = in_off[j + 1] - beg, V = vcount[j];
-        if (big && n >= big) continue;  // its pipeline wrote the record
+        if ((big && n >= big) || (flags[j] & B64X_LANE_CHAINED))
+            continue;  // its pipeline wrote the record
         const bool hold = flags[j] & 1;
         int need = hold ? (int) (V & 3) : 0;
         uint8_t got[4] = {0, 0, 0, 0};
@@ -3687,6 +3690,41 @@ __global__ __launch_bounds__(kThreads) void k_batch_finish(
 __global__ void __launch_bounds__(64) k_stamp(uint64_t *h_stamp, uint64_t v)
 {
     if (threadIdx.x == 0) *(volatile uint64_t *) h_stamp = v;
+}
+
+// A chained lane job's head (the reference keeps these
+// bits in decoder->bits across reads, src/base64decoder.c:64-76): the
+// held-back sextets of the stream's previous block, read from its record
+// (host memory, written by an earlier kernel of this stream), spelled as
+// alphabet characters into the last tail_n of the 4 head bytes (the rest
+// stay outside the alphabet).  What it read is logged, for the host to
+// compare with the record it checked (b64x_spell_ok).
+__global__ void __launch_bounds__(64) k_spell_head(uint8_t *head, const b64x_dec_result *prev,
+                                                   b64x_dec_result *log, DecAlpha a)
+{
+    if (threadIdx.x != 0) return;
+    const volatile b64x_dec_result *v = prev;
+    b64x_dec_result r;
+    r.out_len = v->out_len;
+    r.valid = v->valid;
+    r.tail_n = v->tail_n;
+    for (int k = 0; k < 4; k++) r.tail[k] = v->tail[k];
+    r.nchars = v->nchars;
+    r.seq = v->seq;
+    r.flags = v->flags;
+    volatile b64x_dec_result *w = log;
+    w->out_len = r.out_len;
+    w->valid = r.valid;
+    w->tail_n = r.tail_n;
+    for (int k = 0; k < 4; k++) w->tail[k] = r.tail[k];
+    w->nchars = r.nchars;
+    w->seq = r.seq;
+    w->flags = r.flags;
+    const uint32_t n = r.tail_n <= 3 ? r.tail_n : 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t s = r.tail[k];
+        if (s < 64) head[4 - n + k] = (uint8_t) (s < 62 ? enc_char(s, EncAlpha{}) : s == 62 ? a.p62 : a.p63);
+    }
 }
 
 // ------------------------------------------------------------ utilities --
@@ -4736,7 +4774,6 @@ struct b64x_lane {
     uint64_t in_cap, offs_cap, flags_cap;  // bytes allocated
     b64x_dec_result *d_res;  // big decode jobs: the pipeline's record ...
     void *d_ws;              // ... and workspace (allocated at the first)
-    uint32_t dseq;           // the last decode batch's sequence number
 };
 
 b64x_lane *b64x_lane_open(void)
@@ -4883,17 +4920,22 @@ static constexpr uint64_t kBigJob = 128u << 10;
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const uint8_t *h_flags,
-                           b64x_dec_result *h_res, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg)
+                           b64x_dec_result *h_res, const b64x_dec_result *const *h_prev,
+                           b64x_dec_result *h_spell, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg, uint32_t *seq)
 {
-    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off || !h_flags || !h_res)))
+    if (!l || !seq || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off || !h_flags || !h_res)))
         return -EINVAL;
+    for (uint32_t j = 0; j < njobs; j++)
+        if ((h_flags[j] & B64X_LANE_CHAINED) &&
+            (!h_prev || !h_prev[j] || !h_spell || h_in_off[j + 1] - h_in_off[j] < 4))
+            return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(l->device)))) return err;
+    *seq = next_seq();
     if (njobs) {
         const uint64_t words = (uint64_t) njobs + 1;
         for (uint32_t j = 0; j < njobs; j++) b64x_poison_result(h_res + j);
-        l->dseq = next_seq();
         if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, words))) return err;
         if ((err = lane_grow(l, (void **) &l->d_flags, &l->flags_cap, njobs))) return err;
         if ((err = hip_err(hipMemcpyAsync(l->d_flags, h_flags, njobs, hipMemcpyHostToDevice,
@@ -4904,12 +4946,16 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
         // Jobs of kBigJob characters or more (whole stage blocks) would each
         // keep one wave of the batch kernel busy for hundreds of us: they
         // take the single-buffer pipeline instead, in job order on the lane's
-        // stream, which writes their records itself; the batch kernels skip them.
-        uint32_t nbig = 0;
-        for (uint32_t j = 0; j < njobs; j++) nbig += h_in_off[j + 1] - h_in_off[j] >= kBigJob;
-        const BatchLayout L{d_in_off, d_out_off, 0, 0, 0, nbig ? kBigJob : 0};
+        // stream, which writes their records itself; so do chained jobs,
+        // whose heads are spelled between their predecessor's decode and
+        // their own.  The batch kernels skip both.
+        uint32_t npiped = 0;
+        for (uint32_t j = 0; j < njobs; j++)
+            npiped += h_in_off[j + 1] - h_in_off[j] >= kBigJob || (h_flags[j] & B64X_LANE_CHAINED);
+        const BatchLayout L{d_in_off, d_out_off, 0, 0, 0, kBigJob, (const uint8_t *) l->d_flags};
         const uint8_t *src = h_in_off[njobs] ? l->d_in : (const uint8_t *) l->d_offs;
-        if (nbig < njobs) {
+        const DecAlpha da = dec_alpha(abc);
+        if (npiped < njobs) {
             if ((err = launch_batch_decode(src, L, njobs, h_out, d_vcount, abc, l->stream, true)))
                 return err;
             const DeviceInfo *d = device_info();
@@ -4917,11 +4963,10 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                                            (uint64_t) d->cus * 8);
             hipLaunchKernelGGL(k_batch_finish, dim3(grid), dim3(kThreads), 0, l->stream, src,
                                d_in_off, (const uint8_t *) l->d_flags,
-                               (const uint64_t *) d_vcount, njobs, L.big, dec_alpha(abc), h_res,
-                               l->dseq);
+                               (const uint64_t *) d_vcount, njobs, kBigJob, da, h_res, *seq);
             if ((err = launch_status())) return err;
         }
-        if (nbig && !l->d_ws) {
+        if (npiped && !l->d_ws) {
             const uint64_t wsz = b64x_decode_workspace_size(0);
             if (!l->d_res && hipMalloc(&l->d_res, sizeof *l->d_res) != hipSuccess) {
                 l->d_res = nullptr;
@@ -4933,12 +4978,18 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
             }
             if ((err = hip_err(hipMemsetAsync(l->d_ws, 0, wsz, l->stream)))) return err;
         }
-        for (uint32_t j = 0; nbig && j < njobs; j++) {
+        for (uint32_t j = 0; npiped && j < njobs; j++) {
             const uint64_t n = h_in_off[j + 1] - h_in_off[j];
-            if (n < kBigJob) continue;
+            const bool chained = h_flags[j] & B64X_LANE_CHAINED;
+            if (n < kBigJob && !chained) continue;
+            if (chained) {
+                hipLaunchKernelGGL(k_spell_head, dim3(1), dim3(64), 0, l->stream,
+                                   l->d_in + h_in_off[j], h_prev[j], h_spell + j, da);
+                if ((err = launch_status())) return err;
+            }
             if ((err = decode_dev_impl(l->d_in + h_in_off[j], n, h_out + h_out_off[j], l->d_res,
                                        h_res + j, abc, h_flags[j] & 1 ? B64X_DEC_HOLD_TAIL : 0,
-                                       l->d_ws, l->stream, l->dseq)))
+                                       l->d_ws, l->stream, *seq)))
                 return err;
         }
     }
@@ -4952,25 +5003,34 @@ int b64x_lane_wait(b64x_lane *l)
     return hip_err(hipStreamSynchronize(l->stream));
 }
 
+// Every record is this batch's and consistent; every chained job's head was
+// spelled from its predecessor's finished record (checked before it: the
+// predecessor is an earlier job of this batch or of a batch before it).
 static bool jobs_ok(const uint64_t *h_in_off, const uint8_t *h_flags,
-                    const b64x_dec_result *h_res, uint32_t njobs, uint32_t seq)
+                    const b64x_dec_result *h_res, const b64x_dec_result *const *h_prev,
+                    const b64x_dec_result *h_spell, uint32_t njobs, uint32_t seq)
 {
-    for (uint32_t j = 0; j < njobs; j++)
+    for (uint32_t j = 0; j < njobs; j++) {
         if (!b64x_result_ok(h_res + j, h_in_off[j + 1] - h_in_off[j], h_flags[j] & 1, seq,
                             nullptr))
             return false;
+        if ((h_flags[j] & B64X_LANE_CHAINED) && !b64x_spell_ok(h_spell + j, h_prev[j]))
+            return false;
+    }
     return true;
 }
 
-int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t *h_flags,
-                           const b64x_dec_result *h_res, uint32_t njobs)
+int b64x_lane_decode_check(b64x_lane *l, uint32_t seq, const uint64_t *h_in_off,
+                           const uint8_t *h_flags, const b64x_dec_result *h_res,
+                           const b64x_dec_result *const *h_prev,
+                           const b64x_dec_result *h_spell, uint32_t njobs)
 {
     if (!l || (njobs && (!h_in_off || !h_flags || !h_res))) return -EINVAL;
-    if (jobs_ok(h_in_off, h_flags, h_res, njobs, l->dseq)) return 0;
+    if (jobs_ok(h_in_off, h_flags, h_res, h_prev, h_spell, njobs, seq)) return 0;
     g_early_lane.fetch_add(1, std::memory_order_relaxed);
     int err = b64x_lane_wait(l);
     if (err) return err;
-    return jobs_ok(h_in_off, h_flags, h_res, njobs, l->dseq) ? 0 : -EIO;
+    return jobs_ok(h_in_off, h_flags, h_res, h_prev, h_spell, njobs, seq) ? 0 : -EIO;
 }
 
 #ifdef B64X_TEST_HOOKS

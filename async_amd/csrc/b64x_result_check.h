@@ -69,4 +69,20 @@ static inline bool b64x_result_ok(const b64x_dec_result *r, uint64_t len, unsign
     return c.out_len == (hold ? c.valid / 4 * 3 : c.valid * 6 / 8);
 }
 
+/* A chained lane job's spell log (what the device spelled its head from)
+ * against the predecessor's record as checked on the host: the same call
+ * (seq, nchars, flags) and the same held-back sextets.  A log taken from a
+ * record that had not landed yet (poison, or an older call's) fails. */
+static inline bool b64x_spell_ok(const b64x_dec_result *log, const b64x_dec_result *prev)
+{
+    const volatile b64x_dec_result *v = log;
+    if (v->seq != prev->seq || v->nchars != prev->nchars || v->flags != prev->flags ||
+        v->tail_n != prev->tail_n || v->valid != prev->valid)
+        return false;
+    for (int j = 0; j < 4; j++)
+        if (v->tail[j] != prev->tail[j])
+            return false;
+    return true;
+}
+
 #endif /* ASYNC_AMD_B64X_RESULT_CHECK_H */

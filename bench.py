@@ -32,6 +32,10 @@ Also reported on the same JSON line:
                 timed beside it (rank 0 at N=1; skipped with --no-cpu);
   root_scatter  N > 1: rank 0 scatters config 4's 1 GiB to the ranks (reported,
                 not used by the primary metric: SURVEY.md §8(e));
+  host_fd       the path's real ends: config 2 through a pipe / socket
+                read() by the event loop's pipestream into the GPU decoder
+                stage, and the encoder stack drained by fdsink into write(2)
+                on a pipe (rank 0, N=1); never `value`;
   host_inclusive  the same 1 GiB round trip starting and ending in pinned
                 host memory (rank 0): the kernels read and write the pinned
                 buffers in place over PCIe (the sessions' zero-copy path),
@@ -437,6 +441,109 @@ def bench_host_inclusive(args, b64):
     for p in (p_src, p_chr, p_dst):
         L.b64x_host_free(p)
     return out
+
+
+def bench_host_fd(args, b64):
+    """The path's real ends: bytes crossing a pipe
+    or socket through read(2)/write(2) on the product's event loop.
+      ingress  a peer thread writes config 2's characters (clean, and in
+               CRLF-76 lines) into a pipe (and, clean, an AF_UNIX
+               socketpair) in 1 MiB writes -> pipestream -> base64_decode
+               stage (GPU) -> consumer reading 256 KiB at a time;
+      egress   config 2's bytes on a queuestream -> base64_encode stage (GPU)
+               -> chunk_encode(1 MiB) -> fdsink (10,240-byte pulls, the
+               reference's tcp_connection.c:22, write(2)) -> a pipe a peer
+               thread drains.
+    One stream each way, one loop thread; payload GiB/s (N bytes), wall time
+    from the first byte to the last, bit-checked (ingress: == the input;
+    egress: de-chunked == G3's digest, every chunk but the last full)."""
+    import hashlib
+
+    import numpy as np
+
+    from tests import util
+
+    N = args.size
+    x = torch.empty(N, dtype=torch.uint8, device="cuda")
+    b64.fill_splitmix64(x, 0x5EED)
+    chars_d = b64.encode(x)
+    xh = x.cpu().numpy()
+    out = np.empty(N + 16, np.uint8)
+    out.fill(0)  # fault in outside the timed region
+    res = {"workload": f"cfg2 ({N >> 20} MiB) through a pipe/socket and the event loop, one "
+                       "stream each way", "unit": "GiB/s of payload"}
+    # the same stream from memory (blobstream -> decoder stage -> consumer):
+    # the loop and the GPU stage without the pipe's copies
+    import ctypes
+    H = util.harness()
+    ch = chars_d.cpu().numpy()
+    best = None
+    for _ in range(2):
+        err = ctypes.c_int(0)
+        t0 = time.perf_counter()
+        n = H.h_decode_stream(ch.ctypes.data, ch.size, 0, 1 << 18, util.cch(-1), util.cch(-1),
+                              out.ctypes.data, out.size, ctypes.byref(err))
+        dt = time.perf_counter() - t0
+        if n != N or not np.array_equal(out[:N], xh):
+            raise SystemExit(f"host_fd blob stream: decode mismatch (errno {err.value})")
+        best = dt if best is None else min(best, dt)
+    res["ingress_blob_clean"] = {"GiB_s": N / best / 2**30, "seconds": best,
+                                 "bytes_in": int(ch.size)}
+    del ch
+    legs = [("ingress_pipe_clean", chars_d, False), ("ingress_socket_clean", chars_d, True),
+            ("ingress_pipe_crlf76", None, False)]
+    for name, text_d, sock in legs:
+        if text_d is None:
+            text_d = crlf76(chars_d)
+        text = text_d.cpu().numpy()
+        if name == "ingress_pipe_crlf76":
+            del text_d
+        best = None
+        for _ in range(2):  # the first pass also pools the hub's arenas and lanes
+            got, err, dt = util.fd_decode(text, write_chunk=1 << 20, read_size=1 << 18,
+                                          sock=sock, out=out)
+            if got is None or got.size != N or not np.array_equal(got, xh):
+                raise SystemExit(f"host_fd {name}: decode mismatch (errno {err})")
+            best = dt if best is None else min(best, dt)
+        res[name] = {"GiB_s": N / best / 2**30, "seconds": best,
+                     "bytes_in": int(text.size)}
+        del text
+    del out
+    chunk = 1 << 20
+    framed = np.empty(util.framed_cap(N, chunk), np.uint8)
+    framed.fill(0)
+    g3 = _g3_digest()
+    best = None
+    for _ in range(2):
+        got, err, dt = util.fd_encode(xh, max_chunk=chunk, out=framed)
+        if got is None:
+            raise SystemExit(f"host_fd egress failed (errno {err})")
+        best = dt if best is None else min(best, dt)
+    body = got.tobytes()
+    h, pos, sizes = hashlib.sha256(), 0, []
+    while True:
+        eol = body.index(b"\r\n", pos)
+        size = int(body[pos:eol], 16)
+        pos = eol + 2
+        if size == 0:
+            break
+        h.update(memoryview(body)[pos:pos + size])
+        sizes.append(size)
+        pos += size + 2
+    ok = (g3 is None or h.hexdigest() == g3) and all(k == chunk for k in sizes[:-1])
+    if not ok:
+        raise SystemExit("host_fd egress: framed output mismatch")
+    res["egress_pipe"] = {"GiB_s": N / best / 2**30, "seconds": best,
+                          "framed_bytes": int(got.size), "chunks": len(sizes)}
+    return res
+
+
+def _g3_digest():
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+            return json.load(f)["G3"]["out_sha256"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def crlf76(chars: torch.Tensor) -> torch.Tensor:
@@ -922,6 +1029,9 @@ def main():
     host = None
     if rank == 0 and not args.no_host:
         host = bench_host_inclusive(args, b64)
+    hostfd = None
+    if rank == 0 and world == 1 and not args.no_host:
+        hostfd = bench_host_fd(args, b64)
     mime = None
     if rank == 0 and world == 1 and not args.no_mime and args.size == 1 << 30:
         mime = bench_mime(args, b64)
@@ -999,6 +1109,7 @@ def main():
             "batch_cfg4": batch,
             "batch_cfg3": batch3,
             "host_inclusive": host,
+            "host_fd": hostfd,
             "root_scatter": scatter,
             "mime_decode": mime,
             "cfg5_egress": cfg5,

@@ -270,6 +270,10 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
  * stamp (written by a kernel queued behind the encode) is there; if not,
  * counted (b64x_diag_counters), waited for and checked again.  0 or -EIO. */
 int b64x_lane_encode_check(b64x_lane *l);
+/* Lane decode job flag (h_flags): the job is chained -- h_prev[i] names the
+ * record whose held-back sextets complete its 4-byte head (below). */
+#define B64X_LANE_CHAINED 4u
+
 /* Decode njobs character buffers: job i is h_in[h_in_off[i] ..
  * h_in_off[i+1]), its bytes go to h_out + h_out_off[i] (capacity
  * >= b64x_decoded_cap(len)) and its result record to h_res[i].  h_flags[i]
@@ -277,18 +281,40 @@ int b64x_lane_encode_check(b64x_lane *l);
  * groups are emitted and the last V mod 4 sextets are reported in the
  * record (b64x_decode_dev's HOLD_TAIL); otherwise the job ends its stream
  * and its final partial group is emitted.  Pinned host buffers, as for
- * b64x_lane_encode_async; the records are poisoned here. */
+ * b64x_lane_encode_async; the records are poisoned here.  *seq receives
+ * the batch's sequence number (its records' `seq`; pass it to
+ * b64x_lane_decode_check).
+ *
+ * Chained jobs (one stream decoded in blocks without waiting for each
+ * block's record on the host): h_flags[i] & B64X_LANE_CHAINED and h_prev[i]
+ * (h_prev may be NULL when no job is chained) points at the pinned host
+ * record of an earlier HOLD_TAIL job of the same stream -- in this batch or
+ * in a batch queued before it on this lane.  Job i's first 4 characters are
+ * a head of characters outside the alphabet; on the device, after that
+ * record has been written and before job i is decoded, its last tail_n
+ * head bytes are replaced by the record's held-back sextets spelled as
+ * alphabet characters, and what was spelled from is logged to h_spell[i]
+ * (pinned), which b64x_lane_decode_check compares with the record.
+ * Chained jobs and jobs of 128 KiB or more are decoded one after another
+ * in job order; the rest in one batch launch before them.
+ *
+ * Several decode batches may be queued on one lane; they run in order.
+ * Encode batches only go to an idle lane. */
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const uint8_t *h_flags,
-                           b64x_dec_result *h_res, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg);
+                           b64x_dec_result *h_res, const b64x_dec_result *const *h_prev,
+                           b64x_dec_result *h_spell, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg, uint32_t *seq);
 /* Checks a finished decode batch's records (see b64x_session_decode_result
- * for what is checked): one still poisoned or inconsistent is counted, the
- * lane is waited for and the records are checked again.  0 or -EIO. */
-int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off,
+ * for what is checked) and, for chained jobs, that the head was spelled
+ * from the finished predecessor record: one still poisoned or inconsistent
+ * is counted, the lane is waited for and the records are checked again.  0
+ * or -EIO. */
+int b64x_lane_decode_check(b64x_lane *l, uint32_t seq, const uint64_t *h_in_off,
                            const uint8_t *h_flags, const b64x_dec_result *h_res,
-                           uint32_t njobs);
+                           const b64x_dec_result *const *h_prev,
+                           const b64x_dec_result *h_spell, uint32_t njobs);
 /* Wait for everything queued on the lane. */
 int b64x_lane_wait(b64x_lane *l);
 

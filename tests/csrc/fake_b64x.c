@@ -65,6 +65,8 @@ struct fjob {
     b64x_dec_result res;
     b64x_dec_result *recs_dst; /* publish: per-job records */
     b64x_dec_result *recs;
+    b64x_dec_result *spells_dst; /* publish: chained jobs' spell logs */
+    b64x_dec_result *spells;
     uint32_t njobs;
     uint64_t *stamp_dst;     /* publish: a lane's completion stamp */
     uint64_t stamp;
@@ -96,7 +98,7 @@ static uint32_t next_seq(void)
     while (v == 0);
     return v;
 }
-static atomic_ulong n_early, n_jobs;
+static atomic_ulong n_early, n_jobs, n_chained;
 
 static uint64_t rnd(void) /* splitmix64, under mu */
 {
@@ -138,6 +140,8 @@ static void publish(fjob *j)
         *j->res_dst = j->res;
     if (j->recs_dst)
         memcpy(j->recs_dst, j->recs, (size_t) j->njobs * sizeof *j->recs);
+    if (j->spells_dst)
+        memcpy(j->spells_dst, j->spells, (size_t) j->njobs * sizeof *j->spells);
     if (j->stamp_dst)
         *(volatile uint64_t *) j->stamp_dst = j->stamp;
 }
@@ -146,6 +150,7 @@ static void job_free(fjob *j)
 {
     free(j->out_src);
     free(j->recs);
+    free(j->spells);
     free(j);
 }
 
@@ -296,6 +301,12 @@ void fake_configure(uint64_t seed, unsigned pct, int mode)
     raw_mode = mode == MODE_RAW;
     fake_mode = mode;
     pthread_mutex_unlock(&mu);
+}
+
+/* chained lane jobs (heads spelled "on the device") since load */
+uint64_t fake_chained(void)
+{
+    return atomic_load(&n_chained);
 }
 
 /* jobs queued and early ones since load */
@@ -521,7 +532,6 @@ int b64x_session_decode_result(b64x_session *s, b64x_dec_result *res)
 struct b64x_lane {
     uint64_t stamp; /* the "host memory" stamp, published with a batch */
     uint64_t seq;   /* the last encode batch queued */
-    uint32_t dseq;  /* the last decode batch's sequence number */
 };
 
 b64x_lane *b64x_lane_acquire(void)
@@ -576,26 +586,92 @@ int b64x_lane_encode_check(b64x_lane *l)
     return *(volatile uint64_t *) &l->stamp == l->seq ? 0 : -EIO;
 }
 
+/* The records the device has computed, by the host address they will be
+ * published to: a chained job reads its predecessor's record on the
+ * device after that one has been decoded, whether or not the host has it
+ * yet (ordered on the lane).  Open addressing, overwritten on reuse. */
+enum { REG_SIZE = 1 << 18 };
+static struct {
+    const b64x_dec_result *addr;
+    b64x_dec_result rec;
+} reg[REG_SIZE];
+static pthread_mutex_t reg_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t reg_slot(const b64x_dec_result *addr)
+{
+    size_t i = ((uintptr_t) addr >> 3) * 0x9E3779B97F4A7C15ull >> 46;
+    while (reg[i].addr && reg[i].addr != addr)
+        i = (i + 1) & (REG_SIZE - 1);
+    return i;
+}
+
+static void reg_put(const b64x_dec_result *addr, const b64x_dec_result *r)
+{
+    pthread_mutex_lock(&reg_mu);
+    size_t i = reg_slot(addr);
+    reg[i].addr = addr;
+    reg[i].rec = *r;
+    pthread_mutex_unlock(&reg_mu);
+}
+
+static bool reg_get(const b64x_dec_result *addr, b64x_dec_result *r)
+{
+    pthread_mutex_lock(&reg_mu);
+    size_t i = reg_slot(addr);
+    bool ok = reg[i].addr == addr;
+    if (ok)
+        *r = reg[i].rec;
+    pthread_mutex_unlock(&reg_mu);
+    return ok;
+}
+
 int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
                            const uint64_t *h_out_off, const uint8_t *h_flags,
-                           b64x_dec_result *h_res, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg)
+                           b64x_dec_result *h_res, const b64x_dec_result *const *h_prev,
+                           b64x_dec_result *h_spell, const b64x_alphabet *abc,
+                           b64x_done_fn done, void *arg, uint32_t *seq)
 {
     fjob *j = calloc(1, sizeof *j);
     j->owner = l;
     size_t total = njobs ? h_out_off[njobs] : 0;
     j->out_src = malloc(total + 16);
     j->recs = calloc(njobs ? njobs : 1, sizeof *j->recs);
-    l->dseq = next_seq();
+    j->spells = calloc(njobs ? njobs : 1, sizeof *j->spells);
+    *seq = next_seq();
+    bool chained_any = false;
     for (uint32_t k = 0; k < njobs; k++) {
         size_t n = h_in_off[k + 1] - h_in_off[k];
-        j->recs[k] = decode_bits(h_in + h_in_off[k], n, abc, h_flags[k] & B64X_DEC_HOLD_TAIL,
-                                 l->dseq, j->out_src + h_out_off[k]);
+        const uint8_t *src = h_in + h_in_off[k];
+        uint8_t *tmp = NULL;
+        if (h_flags[k] & B64X_LANE_CHAINED) {
+            /* the device spells the predecessor's held-back sextets into
+             * the head (k_spell_head) after that one's decode */
+            chained_any = true;
+            atomic_fetch_add(&n_chained, 1);
+            b64x_dec_result p;
+            if (!h_prev || !h_prev[k] || n < 4 || !reg_get(h_prev[k], &p))
+                return -EINVAL;
+            j->spells[k] = p;
+            tmp = malloc(n);
+            memcpy(tmp, src, n);
+            const char *p62 = abc->pos62 == (char) -1 ? "+" : &abc->pos62;
+            const char *p63 = abc->pos63 == (char) -1 ? "/" : &abc->pos63;
+            for (uint32_t i = 0; i < p.tail_n && i < 4; i++) {
+                uint8_t v = p.tail[i];
+                tmp[4 - p.tail_n + i] = v < 62 ? (uint8_t) kStd[v] : (uint8_t) (v == 62 ? *p62 : *p63);
+            }
+            src = tmp;
+        }
+        j->recs[k] = decode_bits(src, n, abc, h_flags[k] & B64X_DEC_HOLD_TAIL, *seq,
+                                 j->out_src + h_out_off[k]);
+        reg_put(h_res + k, &j->recs[k]);
+        free(tmp);
     }
     j->out_dst = h_out;
     j->out_n = total;
     j->recs_dst = h_res;
+    j->spells_dst = chained_any ? h_spell : NULL;
     j->njobs = njobs;
     j->done = done;
     j->arg = arg;
@@ -606,20 +682,29 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     return 0;
 }
 
-int b64x_lane_decode_check(b64x_lane *l, const uint64_t *h_in_off, const uint8_t *h_flags,
-                           const b64x_dec_result *h_res, uint32_t njobs)
+static bool jobs_ok(uint32_t seq, const uint64_t *h_in_off, const uint8_t *h_flags,
+                    const b64x_dec_result *h_res, const b64x_dec_result *const *h_prev,
+                    const b64x_dec_result *h_spell, uint32_t njobs)
 {
-    bool ok = true;
-    for (uint32_t k = 0; k < njobs && ok && !raw_mode; k++)
-        ok = b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], l->dseq, NULL);
-    if (ok)
+    for (uint32_t k = 0; k < njobs; k++) {
+        if (!b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], seq, NULL))
+            return false;
+        if ((h_flags[k] & B64X_LANE_CHAINED) && !b64x_spell_ok(h_spell + k, h_prev[k]))
+            return false;
+    }
+    return true;
+}
+
+int b64x_lane_decode_check(b64x_lane *l, uint32_t seq, const uint64_t *h_in_off,
+                           const uint8_t *h_flags, const b64x_dec_result *h_res,
+                           const b64x_dec_result *const *h_prev,
+                           const b64x_dec_result *h_spell, uint32_t njobs)
+{
+    if (raw_mode || jobs_ok(seq, h_in_off, h_flags, h_res, h_prev, h_spell, njobs))
         return 0;
     atomic_fetch_add(&g_early_lane, 1);
     owner_wait(l);
-    for (uint32_t k = 0; k < njobs; k++)
-        if (!b64x_result_ok(h_res + k, h_in_off[k + 1] - h_in_off[k], h_flags[k], l->dseq, NULL))
-            return -EIO;
-    return 0;
+    return jobs_ok(seq, h_in_off, h_flags, h_res, h_prev, h_spell, njobs) ? 0 : -EIO;
 }
 
 /* The product's record check on a caller's record (tests/test_stage_fake.py

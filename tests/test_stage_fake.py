@@ -36,6 +36,11 @@ def counters(L):
     return int(out[0]), int(out[1])
 
 
+def chained(L):
+    L.fake_chained.restype = ctypes.c_uint64
+    return int(L.fake_chained())
+
+
 def stats(L):
     out = (ctypes.c_uint64 * 2)()
     L.fake_stats(out)
@@ -62,8 +67,8 @@ def bad_streams(msgs, got):
 
 @pytest.fixture
 def small_blocks(monkeypatch):
-    # 1 KiB staging: every stream outgrows its first block and continues on
-    # chained sessions, 2-7 blocks each (the round-1 stress shape)
+    # 1 KiB staging: every stream outgrows its first block, 2-7 blocks each
+    # (the round-1 stress shape), chained on the lanes while in flight
     monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", "1024")
 
 
@@ -77,12 +82,16 @@ def test_long_decoder_streams_adversarial_orders(small_blocks, seed, pct):
     L.fake_configure(seed, pct, 0)
     e0 = counters(L)
     j0 = stats(L)
+    c0 = chained(L)
     msgs = long_msgs(seed)
     got, err = util.ingress_stacks(msgs, 4096, lib=L)
     assert err == 0
     assert bad_streams(msgs, got) == []
     batches, early = (a - b for a, b in zip(stats(L), j0))
-    assert batches >= 4  # 2-7 blocks a stream, one on the GPU at a time
+    # blocks 2..7 of a stream are chained to the one before while it is in
+    # flight (the device spells the carry), so a stream is not one batch
+    # round trip per block
+    assert batches >= 2 and chained(L) > c0
     if pct == 100:
         assert early == batches and counters(L)[1] - e0[1] == batches
 

@@ -160,3 +160,20 @@ def test_decoder_streams_big_and_small_jobs_in_one_batch(monkeypatch):
     assert err == 0
     for i, m in enumerate(msgs):
         assert got[i] == orc.decode_stream(m, 0, 0, 200), i
+
+
+@pytest.mark.parametrize("cap", [4096, 65536])
+def test_decoder_stage_chained_blocks(monkeypatch, cap):
+    """One long stream in many small blocks: every block after the first is
+    committed while its predecessor is still queued or on the GPU, so its
+    carried sextets are spelled into its head on the device (k_spell_head,
+    chained lane jobs, across batches queued on one lane) -- the stream's
+    bytes equal the oracle's, carries at every block edge included."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    monkeypatch.setenv("ASYNC_B64_MIN_PULL", str(cap))
+    rng = np.random.default_rng(cap)
+    dirty = _dirty(rng, 3_000_000)
+    for read_size in (1000, 1 << 20):
+        got, err = util.stage_decode(dirty, 0, read_size)
+        assert err == 0
+        assert got == orc.decode_stream(dirty, 0, 0, 200)
