@@ -230,28 +230,6 @@ DEV uint4 enc_quad(const uint8_t *tab, uint32_t a, uint32_t b, uint32_t c)
     return o;
 }
 
-// enc_quad with the alphabet held one character per lane (lane i: the
-// character of sextet i) and read across lanes with ds_bpermute -- no LDS
-// table, so no block barrier before the first lookup.
-DEV uint32_t enc_group_bp(uint32_t lc, uint32_t g)
-{
-    const uint32_t c0 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 16) & 0xFCu), (int) lc);
-    const uint32_t c1 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 10) & 0xFCu), (int) lc);
-    const uint32_t c2 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g >> 4) & 0xFCu), (int) lc);
-    const uint32_t c3 = (uint32_t) __builtin_amdgcn_ds_bpermute((int) ((g << 2) & 0xFCu), (int) lc);
-    return c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
-}
-
-DEV uint4 enc_quad_bp(uint32_t lc, uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t g0 = __builtin_amdgcn_perm(0u, a, 0x0c000102u);
-    uint32_t g1 = __builtin_amdgcn_perm(b, a, 0x0c030405u);
-    uint32_t g2 = __builtin_amdgcn_perm(c, b, 0x0c020304u);
-    uint32_t g3 = __builtin_amdgcn_perm(0u, c, 0x0c010203u);
-    return make_uint4(enc_group_bp(lc, g0), enc_group_bp(lc, g1), enc_group_bp(lc, g2),
-                      enc_group_bp(lc, g3));
-}
-
 // Encode r (1..12) bytes at `src` byte by byte; `last` = these are the
 // final bytes of the stream (finalize(), src/base64encoder.c:61-99:
 // a trailing 1 or 2 bytes give 2 or 3 characters, then padding).
@@ -428,99 +406,40 @@ DEV u32x3a4 ld12(const uint8_t *p)
     return *(const u32x3a4 *) p;
 }
 
-// One dword-aligned device buffer (the BASELINE config-2 hot path).  The
-// n/12 full quads form tiles of kFlatU quads per lane (kFlatU x 768 B in
-// per wave); a block takes whole tiles with no per-lane guards, so loads
-// and stores are never exec-masked and the compiler can wait on loads with
-// counted vmcnt instead of draining the stores (vmcnt counts both).  Loads
-// and stores are non-temporal.  Launched with one block per tile (a
+// One dword-aligned device buffer (the BASELINE config-2 hot path): one
+// quad (12 bytes in, 16 characters out) per lane, the n/12 full quads in
+// tiles of one 256-lane block each; a block takes whole tiles with no
+// per-lane guards, so loads and stores are never exec-masked and the
+// compiler can wait on loads with counted vmcnt instead of draining the
+// stores (vmcnt counts both).  Loads and stores are non-temporal, the
+// 64-character alphabet an LDS table.  Launched with one block per tile (a
 // non-persistent grid streams fastest here: tests/tools/copy_sweep.hip; the
 // loop only matters past 2^31 tiles).  The last, partial tile and the final
-// n mod 12 bytes (with padding) are done by the last block.  One quad per
-// lane with the LDS table (round 3, profiles/r03_ab_enc*.jsonl: 406 -> 397
-// us per 1 GiB; the copy with encode's 12 -> 16 mix is also fastest at one
-// load per lane); round 1's A/B of software pipelining and cached loads
-// still holds (profiles/r01_v6_*).
-#ifndef B64X_FLAT_U  // A/B builds only (scripts/ab_variants.sh)
-#define B64X_FLAT_U 1
-#endif
-constexpr int kFlatU = B64X_FLAT_U;
-#ifndef B64X_ENC_NTL  // A/B builds only: non-temporal loads / stores
-#define B64X_ENC_NTL true
-#endif
-#ifndef B64X_ENC_NTS
-#define B64X_ENC_NTS true
-#endif
-
-// The per-lane alphabet character of enc_quad_bp (lane v: sextet v's),
-// branch-free: the ternary chain of enc_char compiled to three nested
-// exec-masked branches, each waiting on the kernel arguments, ahead of
-// the first load.
-DEV uint32_t enc_lane_char(uint32_t v, uint32_t p62, uint32_t p63)
-{
-    // 'A' + v, + 6 past 'Z' (v > 25), - 75 past 'z' (v > 51): v in [0, 64)
-    uint32_t c = v + 65 + 6 * ((v + 230) >> 8) - 75 * ((v + 204) >> 8);
-    c = v == 62 ? p62 : c;
-    return v == 63 ? p63 : c;
-}
-
-// A/B builds only (scripts/ab_variants.sh): block size, a wave's quads
-// contiguous instead of a block's, an LDS alphabet table, and a pricing
-// form that stores the loaded bytes instead of encoding them (wrong output)
-#ifndef B64X_ENC_TH
-#define B64X_ENC_TH 256
-#endif
-#ifndef B64X_ENC_WS
-#define B64X_ENC_WS 0
-#endif
-#ifndef B64X_ENC_LDS
-#define B64X_ENC_LDS 1
-#endif
-#ifndef B64X_ENC_PRICE
-#define B64X_ENC_PRICE 0
-#endif
-constexpr uint32_t kEncTH = B64X_ENC_TH;
+// n mod 12 bytes (with padding) are done by the last block.  Measured forms
+// (DESIGN.md §5): one quad per lane with the LDS table 397 us per 1 GiB
+// (profiles/r03_ab_enc*.jsonl); the alphabet read across lanes by
+// ds_bpermute 445 us; two quads per lane 405; 512- and 1,024-lane blocks
+// +20 / +120 us; software pipelining and cached loads slower (r01_v6_*).
+constexpr uint32_t kEncTH = 256;
 
 __global__ __launch_bounds__(kEncTH) void k_encode_flat(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t full, uint64_t n,
     EncAlpha a)
 {
-    // `full` (the whole tiles of kFlatU quads per lane) comes from the host,
-    // so a wave issues its loads without a 64-bit division by 12 first.
+    // `full` (the whole tiles) comes from the host, so a wave issues its
+    // load without a 64-bit division by 12 first.
     __shared__ uint8_t tab[64];
-    const uint64_t tile = (uint64_t) kEncTH * kFlatU;
     const uint32_t tid = threadIdx.x;
-    // the lane's first quad in its tile and the step between its quads
-    const uint32_t q0 = B64X_ENC_WS ? (tid & ~63u) * kFlatU + (tid & 63u) : tid;
-    constexpr uint32_t qs = B64X_ENC_WS ? 64u : kEncTH;
-    if (B64X_ENC_LDS) {
-        build_enc_table(tab, a);
-        __syncthreads();
-    }
+    build_enc_table(tab, a);
+    __syncthreads();
     for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
-        u32x3a4 cur[kFlatU];
-        const uint8_t *src = in + (t * tile + q0) * 12;
-#pragma unroll
-        for (int u = 0; u < kFlatU; u++) cur[u] = ld12<B64X_ENC_NTL>(src + u * qs * 12);
-        // B64X_ENC_LDS = 0: the alphabet one character per lane, read across
-        // lanes (enc_quad_bp, round 2's form): no LDS table and no barrier,
-        // but 16 cross-lane permutes per quad (445 vs 397 us at one quad
-        // per lane, profiles/r03_ab_enc2.jsonl)
-        const uint32_t lc = enc_lane_char(tid & 63u, a.p62, a.p63);
-        uint8_t *dst = out + (t * tile + q0) * 16;
-#pragma unroll
-        for (int u = 0; u < kFlatU; u++) {
-            const uint4 o = B64X_ENC_PRICE ? make_uint4(cur[u].x, cur[u].y, cur[u].z, cur[u].x ^ cur[u].z)
-                          : B64X_ENC_LDS   ? enc_quad(tab, cur[u].x, cur[u].y, cur[u].z)
-                                           : enc_quad_bp(lc, cur[u].x, cur[u].y, cur[u].z);
-            store16<B64X_ENC_NTS>(dst + u * qs * 16, o);
-        }
+        const uint64_t q = t * kEncTH + tid;
+        const u32x3a4 v = ld12<true>(in + q * 12);
+        store16<true>(out + q * 16, enc_quad(tab, v.x, v.y, v.z));
     }
     if (blockIdx.x == gridDim.x - 1) {
         const uint64_t nq = n / 12;
-        build_enc_table(tab, a);
-        __syncthreads();
-        for (uint64_t q = full * tile + tid; q < nq; q += kEncTH) {
+        for (uint64_t q = full * kEncTH + tid; q < nq; q += kEncTH) {
             const u32x3a4 v = *(const u32x3a4 *) (in + q * 12);
             store16<true>(out + q * 16, enc_quad(tab, v.x, v.y, v.z));
         }
@@ -711,20 +630,6 @@ DEV void wave_lds_order()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// The 256-entry decode table in the wave's own LDS slice (one dword of four
-// entries per lane): no block barrier, so a wave never waits for the
-// block's other waves before its lookups.
-[[maybe_unused]] DEV const uint8_t *wave_dec_table(uint32_t *slice, const DecAlpha &a)
-{
-    const uint32_t l = lane_id();
-    uint32_t v = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) v |= dec_value(4 * l + j, a) << (8 * j);
-    slice[l] = v;
-    wave_lds_order();
-    return (const uint8_t *) slice;
 }
 
 // Four groups -> 12 output bytes as three little-endian dwords.
@@ -986,19 +891,14 @@ struct DecodeWs {
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
+// Ranges per wave of a single-pass decode tile (k_decode_suffix): each is
+// decoded into its own LDS window before the tile's prefix is known, so a
+// block holds kFusePer x 4 windows of ~1.6 KB (6 blocks per CU).
 #ifndef B64X_FUSE_PER  // A/B builds only
-#define B64X_FUSE_PER 8
+#define B64X_FUSE_PER 4
 #endif
-// ranges per wave tile in the single-pass decode: with the group-sum prefix
-// and the count run one tile ahead, small tiles win (1 GiB at junk density
-// 0.05, single pass: 2: 1,195 us, 4: 758, 8: 766, 16: 841, 32: 885;
-// profiles/r03_ab_sfx_tiles*.jsonl); 8 keeps the ticket atomics at half of 4's
-// (round 2's chained look-back was best at 16)
 constexpr uint32_t kFusePer = B64X_FUSE_PER;
-constexpr uint32_t kFuseLoad = kFusePer < 4 ? kFusePer : 4;  // of them loaded at once for counting
-static_assert(kFuseLoad % 2 == 0, "counts are reduced two ranges at a time");
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
-
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsStatus = 64;                                        // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
@@ -1451,11 +1351,6 @@ DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
     }
 }
 
-DEV uint32_t lane_valid_count(const uint32_t P[4])
-{
-    return 16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
-           __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
-}
 
 // ---- pass 2, bit-stream form ----------------------------------------------
 //
@@ -1605,8 +1500,8 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
 // sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
 // up to 18 bits past the window's byte 4: skipped sextets land in its
 // head).  Returns the step's alphabet characters.
-template <bool BE = false>
-DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
+template <bool BE = false, class SM = P2dSmem>
+DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
     // per dword: table values, the v_perm compaction selector (by the
@@ -1672,13 +1567,7 @@ DEV uint32_t bits_step(const P2dSmem &sm, uint32_t *bits, const uint4 c[2],
 //
 // Reference: the per-character loop of decoder_read(), src/base64decoder.c:
 // 52-80 (skip non-alphabet bytes, 8 bits out per 4 characters' 24).
-#ifndef B64X_LINES_U  // A/B builds only (scripts/ab_variants.sh)
-#define B64X_LINES_U 4
-#endif
-#ifndef B64X_LINES_NTL  // A/B builds only: non-temporal window loads on line-structured text
-#define B64X_LINES_NTL false
-#endif
-constexpr uint32_t kLinesU = B64X_LINES_U;          // slots per lane (2: +1-3 %, 8: +7 %)
+constexpr uint32_t kLinesU = 4;                     // slots per lane (2: +1-3 %, 8: +7 %)
 constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
 constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
 
@@ -1884,14 +1773,8 @@ DEV bool sep_ok_s(const uint8_t *tab, uint32_t sep, uint32_t s)
 // matters for the result (k_decode_lines takes slots [0, T) exactly or
 // publishes their failure; k_decode_suffix takes the rest), only for speed.
 constexpr uint32_t kProbeThreads = 256;
-#ifndef B64X_PROBE_SAMPLES  // A/B builds only: 0 = the first window only
-#define B64X_PROBE_SAMPLES 1
-#endif
-constexpr uint64_t kProbeSampleMin = B64X_PROBE_SAMPLES ? 1u << 18 : ~0ull;  // shorter streams: the first window only
-#ifndef B64X_PROBE_NS  // A/B builds only: sampling threads (<= kProbeThreads)
-#define B64X_PROBE_NS 256
-#endif
-constexpr uint32_t kProbeNS = B64X_PROBE_NS;
+constexpr uint64_t kProbeSampleMin = 1u << 18;  // shorter streams: the first window only
+constexpr uint32_t kProbeNS = 256;              // sampling threads
 constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
 
 __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
@@ -1993,33 +1876,21 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
 
 // At least 6 waves per SIMD (80 VGPRs): unconstrained, the rarely taken
 // generic and tail paths pushed the kernel to 81 VGPRs and 5 waves, which
-// cost the clean path 5 us per 1 GiB; 8 waves (64 VGPRs) spill.
-#ifndef B64X_LINES_WPE  // A/B builds only: minimum waves per SIMD
-#define B64X_LINES_WPE 6
-#endif
-#ifndef B64X_LINES_WTAB  // A/B builds only: 1 = each wave builds its own table, no block barrier
-#define B64X_LINES_WTAB 0
-#endif
-#ifndef B64X_LINES_TH  // A/B builds only: lanes per block of k_decode_lines
-#define B64X_LINES_TH 256
-#endif
-constexpr uint32_t kLinesTH = B64X_LINES_TH, kLinesWaves = kLinesTH / 64;
-__global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(B64X_LINES_WPE)))
+// cost the clean path 5 us per 1 GiB; 8 waves (64 VGPRs) spill.  256-lane
+// blocks with one block-wide table (per-wave tables without the barrier:
+// neutral, profiles/r03_ab_probe_wtab.jsonl).
+constexpr uint32_t kLinesTH = 256, kLinesWaves = kLinesTH / 64;
+__global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, uint32_t seq)
 {
-#if B64X_LINES_WTAB
-    __shared__ uint32_t tabw[kLinesWaves][64];
-#else
     __shared__ uint8_t tab[256];
-#endif
     __shared__ uint8_t s_tail[64];
     // the scalar loads of the model overlap the table build
     const uint64_t *mp = (const uint64_t *) ws_view(ws, nranges).model;
     const uint64_t mw0 = scalar_load_u64(mp), mw1 = scalar_load_u64(mp + 1),
                    mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
-#if !B64X_LINES_WTAB
     build_dec_table(tab, a);
     // a block wholly past slot T (the probe cut the model's slots at junk)
     // leaves before the barrier: on junk-laden input nearly every block of
@@ -2027,7 +1898,6 @@ void k_decode_lines(
     // no longer overlapped the build: MIME text +2 %.)
     if (blockIdx.x * kLinesWaves * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
     __syncthreads();
-#endif
     LineModel m;
     m.L = (uint32_t) mw0;
     m.s = (uint32_t) (mw0 >> 32);
@@ -2045,9 +1915,6 @@ void k_decode_lines(
     const uint32_t wv = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
     const uint32_t t0 = (blockIdx.x * kLinesWaves + wv) * kLinesSlots;
     if (t0 > T) return;
-#if B64X_LINES_WTAB
-    const uint8_t *tab = wave_dec_table(tabw[wv], a);
-#endif
     const uint32_t ns = T - t0 >= kLinesSlots ? kLinesSlots : T - t0;  // interior slots here
     const bool full = ns == kLinesSlots;
     const bool oal = (((uintptr_t) out) & 3) == 0;
@@ -2074,16 +1941,7 @@ void k_decode_lines(
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
             uint32_t G[4], bad;
-#ifndef B64X_LINES_PRICE  // A/B builds only: store the loaded bytes (wrong output)
-#define B64X_LINES_PRICE 0
-#endif
-            if (B64X_LINES_PRICE) {
-                G[0] = c[u].x & 0xFFFFFFu, G[1] = c[u].y & 0xFFFFFFu;
-                G[2] = c[u].z & 0xFFFFFFu, G[3] = c[u].w & 0xFFFFFFu;
-                bad = 0;
-            } else {
-                map_fast(tab, c[u], 16, G, bad);
-            }
+            map_fast(tab, c[u], 16, G, bad);
             const uint64_t fb = __ballot(bad != 0);
             if (fb && fail_u == kLinesU) {
                 fail_u = u;
@@ -2112,7 +1970,7 @@ void k_decode_lines(
             cc[u] = hs[u] ? L - col : 16u;
             oo[u] = pos & 3u;
             const uint8_t *ab = in + (pos & ~3u);
-            win[u] = ld16<B64X_LINES_NTL>(ab);
+            win[u] = ld16<false>(ab);  // (non-temporal: neutral, r02_ab_lines_ntl.jsonl)
             const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
             wx[u] = make_uint2(v.x, v.y);
         }
@@ -2250,33 +2108,9 @@ void k_decode_lines(
 // flushed between steps and its partial dword carried to the front (as
 // decode_buf_bits does); the bytes flushed early are final and never reach
 // the next range's output.
-// One wave copies 64 x 16 bytes from gsrc (per lane) to LDS at lds_dst +
-// 16 x lane, straight into LDS (global_load_lds_dwordx4: no VGPR holds the
-// data).  Issued as inline asm so that the compiler does not track the copy:
-// it cannot tell the copy's destination from the decode's other LDS traffic
-// (the window's atomic ORs go through a pointer) and waited for every copy
-// in flight (vmcnt(0)) at the first of them, right after the copy was
-// issued.  The reader waits itself (vm_wait_all) before it reads the copy.
-DEV void lds_dma16(const void *gsrc, void *lds_dst)
-{
-    const uint32_t l = (uint32_t) (uintptr_t) (__attribute__((address_space(3))) void *) lds_dst;
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
-}
-
-DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// la_lds (optional): where the lookahead bytes sit in LDS (the next range,
-// prefetched there by k_decode_suffix); read only when the range's last
-// group needs them, so the prefetch has the whole range's time to land.
-// la_late: the lookahead bytes are read from `in` only when needed (la
-// and la_ok are ignored), so no global load is in flight during the range.
 DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ in, uint64_t n,
                       uint64_t start, uint64_t re, int T0, uint8_t *ob, const uint4 c[2],
-                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold,
-                      const uint8_t *la_lds = nullptr, bool la_late = false)
+                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold)
 {
     const uint32_t lane = lane_id();
     uint32_t *bits = (uint32_t *) bq;
@@ -2328,14 +2162,6 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     if (!last && T > 0 && (T & 3)) {
         // complete the range's last group from the characters after it
         bool ok = la_ok;
-        if (la_lds) {
-            vm_wait_all();  // the next range's copy, issued when this range began
-            ok = true;      // (the next range is whole)
-            la = la_lds[lane_id()];
-        } else if (la_late) {
-            ok = re + lane_id() < n;
-            la = ok ? in[re + lane_id()] : 0u;
-        }
         for (uint64_t q = re;;) {
             const uint32_t t = ok ? sm.tab[la] : 0xFFu;
             const bool v = t < 64u;
@@ -2477,31 +2303,37 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
 // tiles of kFuseTile ranges (kFusePer per wave) from a ticket in the order
 // they start, so a tile's predecessors are running or done whatever else
-// shares the GPU.  A block counts its tile and publishes the count, then
-// draws and counts its NEXT tile before it takes the first one's prefix, and
-// decodes the first one with decode_range (re-reading it).  The prefix is not
-// a chained look-back: it is the counts of the tiles before it in its group
-// of 64 tiles (one status word per lane) plus the sums of the earlier groups
-// (every tile adds its count into its group's word), all loaded at once, so
-// it takes one memory round trip at any depth and waits only for tiles drawn
-// before this one to be counted -- which, counted one tile ahead, they are.
-// (Round 2's chained look-back -- back over predecessors' aggregates 64 at a
-// time to the first inclusive prefix, right after the count, three waves
-// idle at a barrier -- cost 157 of 945 us on 1 GiB at junk density 0.05,
-// profiles/r03_ab_sfx_breakdown.jsonl.)  Every block counts itself out in
-// `wdone` when it leaves; the block that decodes the last tile writes the
-// record, waits until every block has left (so no prefix read is in
-// flight), then clears the status and group words, the ticket, `wdone` and
-// the failure words.
-// At least 6 waves per SIMD (80 VGPRs).
-#ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD
+// shares the GPU.  Decode first, place later: each wave decodes each of its
+// ranges into an LDS window of its own as the bit stream of the range's
+// sextets from sextet 0 at a fixed window bit (bits_step: what a range
+// decodes to depends on where it starts only through a shift), which also
+// counts them; the tile's count is published, its prefix taken (the counts
+// of the tiles before it in its group of 64 tiles, one status word per lane,
+// plus the sums of the earlier groups: one memory round trip at any depth),
+// and each range's bytes are stored from its window with the shift its
+// start's group phase needs, its last group completed from the characters
+// after it.  Every character is read from HBM once and looked up once.
+// (Round 3's form counted a tile one tile ahead, then read and looked up
+// every range again to decode it: 2.0x the input read from HBM, twice the
+// table work -- profiles/r03_g_pmc_junk005.txt.)  Every block counts itself
+// out in `wdone` when it leaves; the block that decodes the last tile
+// writes the record, waits until every block has left (so no prefix read
+// is in flight), then clears the status and group words, the ticket,
+// `wdone` and the failure words.
+#ifndef B64X_SFX_WPE  // minimum waves per SIMD (80 VGPRs)
 #define B64X_SFX_WPE 6
 #endif
 
-#ifndef B64X_SFX_DMA  // A/B builds only: read ranges ahead into LDS (global_load_lds)
-#define B64X_SFX_DMA 1
-#endif
-constexpr bool kSfxDma = B64X_SFX_DMA;
+// A range's window: relative sextet 0 at window bit kSfxP0 (16 zero bytes
+// before it absorb the store shift), 2,048 characters' 1,536 bytes, up to 3
+// completing sextets, and the shift's read-ahead.
+constexpr uint32_t kSfxP0 = 128;
+constexpr uint32_t kSfxWin = 100;  // uint4 per window
+struct __attribute__((aligned(16))) SfxSmem {
+    uint8_t tab[256];
+    uint32_t sel[16];
+    uint4 win[kWavesPerBlock][kFusePer][kSfxWin];
+};
 
 // The idle test of k_decode_suffix<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
@@ -2544,6 +2376,55 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
     return true;
 }
 
+// 32 stream bits from window bit x (big-endian dwords, or_field<true>).
+DEV uint32_t win_bits32(const uint32_t *wd, uint32_t x)
+{
+    const uint32_t d = x >> 5, q = x & 31u;
+    return q ? __builtin_amdgcn_alignbit(wd[d], wd[d + 1], 32u - q) : wd[d];
+}
+
+// Store stream bytes [0, nbytes) of a window whose byte 0 starts at window
+// bit x_start, to ob: aligned 16-byte blocks of output (lane k the k-th:
+// five dwords read, four funnel shifts by the same amount, one non-temporal
+// dwordx4), the partial head and tail blocks by byte stores (up to 15
+// each, one store of up to 30 lanes).
+DEV void store_shifted(const uint4 *win, uint32_t x_start, uint32_t nbytes, uint8_t *ob)
+{
+    if (!nbytes) return;
+    const uint32_t lane = lane_id();
+    const uint32_t *wd = (const uint32_t *) win;
+    const uint32_t a = (uint32_t) ((uintptr_t) ob & 15);
+    uint8_t *base = ob - a;              // byte k of the output sits at base + a + k
+    const uint32_t x0 = x_start - 8 * a; // window bit of base's byte (x_start >= 8 * 15)
+    const uint32_t end = a + nbytes;
+    const uint32_t klo = (a + 15) >> 4, khi = end >> 4;  // whole blocks [klo, khi)
+    const uint32_t q = x0 & 31u, dq = x0 >> 5;
+    for (uint32_t k = klo + lane; k < khi; k += 64) {
+        const uint32_t d = dq + 4 * k;
+        const uint32_t w0 = wd[d], w1 = wd[d + 1], w2 = wd[d + 2], w3 = wd[d + 3], w4 = wd[d + 4];
+        uint32_t o0 = w0, o1 = w1, o2 = w2, o3 = w3;
+        if (q) {
+            o0 = __builtin_amdgcn_alignbit(w0, w1, 32u - q);
+            o1 = __builtin_amdgcn_alignbit(w1, w2, 32u - q);
+            o2 = __builtin_amdgcn_alignbit(w2, w3, 32u - q);
+            o3 = __builtin_amdgcn_alignbit(w3, w4, 32u - q);
+        }
+        __builtin_nontemporal_store(u32x4a16{bswap32(o0), bswap32(o1), bswap32(o2), bswap32(o3)},
+                                    (u32x4a16 *) (base + 16 * (uint64_t) k));
+    }
+    const uint32_t hend = 16 * klo < end ? 16 * klo : end;  // head bytes [a, hend)
+    uint32_t i = 0;
+    bool act = false;
+    if (lane < 16) {
+        i = a + lane;
+        act = i < hend;
+    } else if (lane < 32) {
+        i = 16 * khi + (lane - 16);  // tail bytes [max(16 khi, hend), end)
+        act = i < end && i >= hend;
+    }
+    if (act) base[i] = (uint8_t) (win_bits32(wd, x0 + 8 * i) >> 24);
+}
+
 template <bool WHOLE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
 void k_decode_suffix(
@@ -2559,73 +2440,15 @@ void k_decode_suffix(
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
     if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
-    const bool dma = (((uintptr_t) in) & 15) == 0;
-    __shared__ P2dSmem sm;
-    // per wave: two ranges read ahead (an LDS object of its own, so that the
-    // compiler sees table and window reads cannot alias the copies in flight)
-    __shared__ uint4 s_rng[kWavesPerBlock][2][kSfxDma ? 128 : 1];
-    __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_cnt[2][kFuseTile];
+    __shared__ SfxSmem sm;
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_cnt[kFuseTile];
     __shared__ uint32_t s_excl;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint4 *bq = sm.bits[wv];
 
-    // Count tile t into s_cnt[b] (each wave its kFusePer ranges; every
-    // wave's loads issued before any is counted).  Block-uniform call.
-    auto count_tile = [&](uint32_t t, uint32_t b) {
-        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
-        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
-            uint4 c[kFuseLoad][2];
-            uint32_t nin[kFuseLoad][2];
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                const uint32_t r = rw + j0 + jj;
-                const uint64_t rb = (uint64_t) r * R;
-                const uint64_t beg = rb > S ? rb : S;
-                const uint64_t re = rb + R < n ? rb + R : n;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
-                    nin[jj][h] = r >= nranges || p >= re
-                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                    c[jj][h] = nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
-                }
-            }
-            // two ranges' counts (each <= 2,048) share one packed DPP scan
-            // (a shuffle reduction per range cost 25 VALU and 6 LDS ops)
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
-                uint32_t cnt = 0;
-#pragma unroll
-                for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        uint32_t P[4];
-                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
-                        cnt += lane_valid_count(P) << (16 * e);
-                    }
-                }
-                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
-                    (int) wave_incl_scan_dpp(cnt), 63);
-                if (lane == 0) {
-                    s_cnt[b][wv * kFusePer + j0 + jj] = tot & 0xFFFFu;
-                    s_cnt[b][wv * kFusePer + j0 + jj + 1] = tot >> 16;
-                }
-            }
-        }
-    };
-    // Publish tile t's count (s_cnt[b] complete): its status word and its
-    // group's sum.  Thread 0.
-    auto publish = [&](uint32_t t, uint32_t b) {
-        uint32_t agg = 0;
-        for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[b][i];
-        st_store(&w.fstatus[t], kStAgg | agg);
-        __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    };
     // The alphabet characters of the suffix before tile t.  Wave 0.
     auto prefix = [&](uint32_t t) -> uint32_t {
         const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
@@ -2645,94 +2468,150 @@ void k_decode_suffix(
         }
     };
 
-    __syncthreads();  // the tables
-    if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
-    __syncthreads();
-    uint32_t tA = s_tile[0], bA = 0;
-    if (tA < ntiles) {
-        count_tile(tA, 0);
-        __syncthreads();
-        if (threadIdx.x == 0) publish(tA, 0);
-    }
     bool owner = false;  // this block decoded the last tile
     uint32_t Vs = 0;     // then: the suffix's alphabet characters
-    while (tA < ntiles) {
-        const uint32_t bB = bA ^ 1u;
-        if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
-        __syncthreads();  // also: s_cnt[bB] of two tiles back is consumed
-        const uint32_t tB = s_tile[bB];
-        if (tB < ntiles) count_tile(tB, bB);
+    __syncthreads();     // the tables
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(w.fticket, 1u);
+        __syncthreads();  // also: the last tile's s_cnt and s_excl are consumed
+        const uint32_t t = s_tile;
+        if (t >= ntiles) break;
+        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
+        // Range j's characters (this lane's 16 of each 1,024-character chunk).
+        auto load = [&](uint32_t j, uint4 c[2], uint32_t nin[2]) {
+            const uint32_t r = rw + j;
+            const uint64_t rb = (uint64_t) r * R;
+            const uint64_t beg = rb > S ? rb : S;
+            const uint64_t re = rb + R < n ? rb + R : n;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
+                nin[h] = r >= nranges || p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+            }
+        };
+        // Count first -- the table values' bit 7s, two ranges per packed DPP
+        // reduction -- and publish the tile's count at once, so the tiles
+        // after it find it published when they take their prefix (counted by
+        // the decode itself, every tile waited for its predecessors' whole
+        // decode: 1.9x slower).  The decode below reads the ranges again,
+        // from L2: a few microseconds later, not a whole tile's time later as
+        // round 3's count-ahead did (whose second read came from HBM).
+#pragma unroll
+        for (uint32_t j = 0; j < kFusePer; j += 2) {
+            uint4 c[2][2];
+            uint32_t nin[2][2];
+            load(j, c[0], nin[0]);
+            load(j + 1, c[1], nin[1]);
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < 2; e++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    uint32_t P[4];
+                    lane_values(sm.tab, c[e][h], nin[e][h], P);
+                    cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
+                            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
+                           << (16 * e);
+                }
+            }
+            const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
+            if (lane == 0) {
+                s_cnt[wv * kFusePer + j] = tot & 0xFFFFu;
+                s_cnt[wv * kFusePer + j + 1] = tot >> 16;
+            }
+        }
         __syncthreads();
-        if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
+        if (threadIdx.x == 0) {  // publish the tile's count: its status word, its group's sum
+            uint32_t agg = 0;
+            for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
+            st_store(&w.fstatus[t], kStAgg | agg);
+            __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // then the decode of each range into its window (sextet 0 at kSfxP0)
+#pragma unroll
+        for (uint32_t j = 0; j < kFusePer; j++) {
+            uint4 *win = sm.win[wv][j];
+            win[lane] = make_uint4(0, 0, 0, 0);
+            if (lane + 64 < kSfxWin) win[lane + 64] = make_uint4(0, 0, 0, 0);
+        }
+        wave_lds_order();
+        uint32_t T[kFusePer];
+#pragma unroll
+        for (uint32_t j = 0; j < kFusePer; j++) {
+            uint4 c[2];
+            uint32_t nin[2];
+            load(j, c, nin);
+            T[j] = rw + j < nranges
+                       ? bits_step<true>(sm, (uint32_t *) sm.win[wv][j], c, nin, (int) kSfxP0)
+                       : 0u;
+        }
         if (wv == 0) {
-            const uint32_t ex = tA ? prefix(tA) : 0u;
+            const uint32_t ex = t ? prefix(t) : 0u;
             if (lane == 0) s_excl = ex;
         }
         __syncthreads();
         uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
-        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
-        const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
-        // A whole range (2,048 characters from its aligned start) of a
-        // 16-byte aligned input is read ahead into LDS by two direct
-        // global->LDS copies (no VGPRs held) while the range before it
-        // decodes; the others (the first, from S; the stream's last) load
-        // as they decode.
-        auto whole = [&](uint32_t r) {
-            return kSfxDma && dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
-        };
-        auto fetch = [&](uint32_t r, uint32_t buf) {
-            const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
-            lds_dma16(src, &s_rng[wv][buf][0]);
-            lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
-        };
-        if (whole(rw)) fetch(rw, 0);
+        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
+        wave_lds_order();  // the windows, written by this wave's own ORs
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
-            const uint64_t rb = (uint64_t) r * R;
-            const uint64_t re = rb + R < n ? rb + R : n;
-            const bool first = r == r0, last = r + 1 == nranges;
-            const uint64_t start = first ? S : rb;
-            const bool next_dma = j + 1 < kFusePer && whole(r + 1);
-            uint4 *buf = s_rng[wv][j & 1];
-            uint32_t nin[2] = {16u, 16u};
-            // Every range goes through the LDS buffer, so that one code path
-            // decodes them all: a joined path made the compiler wait for the
-            // register path's loads (vmcnt(0), draining the copy in flight)
-            // on the copied path too.  A whole range waits for its copy; any
-            // other is loaded here (and waited for) and written there.
-            if (whole(r)) {
-                vm_wait_all();
-            } else {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                    buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+            const uint64_t re = (uint64_t) r * R + R < n ? (uint64_t) r * R + R : n;
+            const bool last = r + 1 == nranges;
+            uint32_t *bits = (uint32_t *) sm.win[wv][j];
+            // the range owns the groups that start in it: its first `skip`
+            // sextets end the group the range before it started (which took
+            // them by look-ahead), and it takes the sextets that end its own
+            // last group from the characters after it
+            const int skip = (int) ((4u - (B & 3u)) & 3u);
+            int Tp = (int) T[j] - skip;
+            bool at_end = last;
+            if (!last && Tp > 0 && (Tp & 3)) {
+                for (uint64_t q = re;;) {
+                    const bool ok = q + lane < n;
+                    const uint32_t tv = ok ? sm.tab[in[q + lane]] : 0xFFu;
+                    const bool v = tv < 64u;
+                    const uint64_t m = __ballot(v);
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                    const int need = 4 - (Tp & 3);
+                    if (v && (int) rank < need)  // after the sextets taken so far
+                        or_field<true>(bits, kSfxP0 + 6u * ((uint32_t) (Tp + skip) + rank),
+                                       tv << 18);
+                    const int got = __popcll(m);
+                    if (got >= need) {
+                        Tp += need;
+                        break;
+                    }
+                    Tp += got;
+                    q += 64;
+                    if (q >= n) {
+                        at_end = true;  // the stream's final, incomplete group
+                        break;
+                    }
                 }
+                wave_lds_order();
             }
-            uint4 c[2];
-            c[0] = buf[lane];
-            c[1] = buf[64 + lane];
-            // then the next range's copy: in flight while this one decodes
-            // (no global load of the compiler's is outstanding from here on)
-            if (next_dma) fetch(r + 1, (j + 1) & 1);
-            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
-                         base_out + (B + 3) / 4 * 3, c, nin, 0u, !last, last, hold,
-                         next_dma ? (const uint8_t *) s_rng[wv][(j + 1) & 1] : nullptr, true);
-            B += s_cnt[bA][wv * kFusePer + j];
+            if (Tp > 0) {
+                const uint32_t ng = (uint32_t) Tp >> 2, rem = (uint32_t) Tp & 3u;
+                // the final partial group: 2 sextets -> 1 byte, 3 -> 2
+                // (floor(6r/8), src/base64decoder.c:59-62,71-76)
+                const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
+                store_shifted(sm.win[wv][j], kSfxP0 + 6u * (uint32_t) skip, 3 * ng + tail,
+                              base_out + (B + 3) / 4 * 3);
+            }
+            B += T[j];
         }
-        if (tA == ntiles - 1) {
+        if (t == ntiles - 1) {
             owner = true;
             Vs = s_excl;
-            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[bA][i];
+            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[i];
         }
-        tA = tB;
-        bA = bB;
     }
     // every prefix read of this block is over (relaxed: the loads have
     // returned -- their values decided the loop -- and a release at agent
     // scope would write back the L2)
-    __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!owner || wv != 0) return;
     const uint64_t V = Vb + Vs;
@@ -2797,11 +2676,8 @@ DEV uint4 load_lane(const uint8_t *src, uint64_t p, uint64_t len, bool aligned, 
 // latency.  A buffer any of whose chunks needs the exact path is marked in
 // outlen[] for the fix-up.  RV: outlen[] receives the alphabet count V
 // instead of floor(6V/8) bytes (the hub's jobs, k_batch_finish).
-#ifndef B64X_BF_WPE  // A/B builds only: minimum waves per SIMD
-#define B64X_BF_WPE 1
-#endif
 template <bool RV>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_BF_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1)))
 void k_decode_batch_fast(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
     uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a)
@@ -3040,6 +2916,7 @@ struct RowModel {
     uint32_t rg;            // 1: the mapping applies
 };
 static_assert(sizeof(RowModel) == 96, "RowModel layout");
+static_assert(kFusePer % 2 == 0, "suffix counts are reduced two ranges at a time");
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the model, in the region pass 1
@@ -3786,30 +3663,36 @@ DeviceInfo g_info[kMaxDevices];
 bool g_info_done[kMaxDevices];
 // Library-owned decode workspaces, one per (device, stream): a workspace
 // carries state from one kernel of a decode to the next, so streams must
-// not share one.  At most kWsCache of them are kept (about 12.7 MiB of HBM
-// each); the least recently used idle one goes when another stream needs
-// one, or when its stream is released (b64x_release_stream).
+// not share one at the same time.  At most kWsCache of them exist (about
+// 12.7 MiB of HBM each), allocated on first need and then kept: a stream
+// that needs one takes a free slot, or rebinds the least recently used
+// idle workspace of its device, and never frees memory on the way.
 //  - A call pins its entry from the lookup until its kernels are enqueued
-//    and an event is recorded behind them (`pins`), so no other thread can
-//    free a workspace between handing it out and enqueuing on it; an entry
-//    that is pinned is never evicted (a call on a ninth stream while all
-//    eight are mid-enqueue gets -EBUSY).
-//  - Eviction unlinks the entry under g_ws_mu and frees it outside the lock,
-//    after waiting on the event recorded behind its last use (the stream
-//    itself may be gone by then): no device-wide synchronisation, and no
-//    lock held while waiting, so a host callback on any stream that calls
-//    back into the library cannot deadlock on it.
+//    and the entry's event is recorded behind them (`pins`), so no other
+//    thread can rebind a workspace between handing it out and enqueuing on
+//    it; when all kWsCache entries are pinned the call gets -EBUSY.
+//  - Rebinding makes the new stream wait on the device for the event
+//    recorded behind the workspace's last use (hipStreamWaitEvent): no host
+//    wait, no device-wide synchronisation, no hipFree, and no lock held
+//    across a HIP call that waits, so a host callback on any stream that
+//    calls back into the library cannot deadlock on it.  (Round 3 freed the
+//    LRU workspace after a hipDeviceSynchronize under the library's lock;
+//    a first fix that freed it with hipFree outside the lock hung a 12-thread
+//    test on the MI355X: hipFree waits for the whole device.)
+//  - Each call leaves the workspace zeroed for the next (re-armed by the
+//    kernels), so a rebound workspace needs no clearing.
 struct WsEntry {
     int dev;
-    void *stream;
-    void *ws;
+    void *stream;       // bound stream; nullptr = idle (reusable)
+    void *ws;           // nullptr: slot not allocated yet
     hipEvent_t last;    // recorded after the entry's last enqueued use
+    bool recorded;      // `last` has been recorded at least once
     uint64_t used;      // last use (g_ws_tick)
     int pins;           // calls between lookup and their event record
-    bool release;       // b64x_release_stream while pinned: free at unpin
+    bool release;       // b64x_release_stream while pinned: unbind at unpin
 };
 constexpr int kWsCache = 8;
-std::mutex g_ws_mu;     // g_ws, g_ws_tick (never held while waiting on HIP)
+std::mutex g_ws_mu;     // g_ws, g_ws_tick (never held across a waiting HIP call)
 WsEntry g_ws[kWsCache];
 uint64_t g_ws_tick;
 
@@ -3946,7 +3829,7 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
     if (((((uintptr_t) d_in) | ((uintptr_t) d_out)) & 3) == 0) {
-        const uint64_t tiles = n / 12 / ((uint64_t) kEncTH * kFlatU);
+        const uint64_t tiles = n / 12 / kEncTH;
         hipLaunchKernelGGL(k_encode_flat, dim3(cap_grid(tiles, (uint64_t) 1 << 31)),
                            dim3(kEncTH), 0, (hipStream_t) stream, (const uint8_t *) d_in,
                            (uint8_t *) d_out, tiles, n, enc_alpha(abc));
@@ -3977,10 +3860,7 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (slots > 0xFFFFFFFFull - 4096) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-#ifndef B64X_TIGHT_U  // A/B builds only: output slots per lane of k_encode_tight2
-#define B64X_TIGHT_U 2
-#endif
-    constexpr int U = B64X_TIGHT_U;
+    constexpr int U = 2;  // output slots per lane of k_encode_tight2
     const EncAlpha ea = enc_alpha(abc);
     const uint64_t E = b64x_encoded_len(len, ea.pad);
     const uint32_t r = (uint32_t) (len % 3);
@@ -4029,26 +3909,8 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
     return launch_status();
 }
 
-// Free an unlinked workspace (outside g_ws_mu): wait for the work queued
-// behind its last use, then release it on its device.
-static void ws_free(const WsEntry &e)
-{
-    if (!e.ws) return;
-    int prev = 0;
-    (void) hipGetDevice(&prev);
-    (void) hipSetDevice(e.dev);
-    if (e.last) {
-        (void) hipEventSynchronize(e.last);
-        (void) hipEventDestroy(e.last);
-    }
-    (void) hipFree(e.ws);
-    (void) hipSetDevice(prev);
-}
-
 // The workspace of (current device, stream), pinned; *slot receives its
-// entry for ws_unpin().  A new stream takes a free entry or the least
-// recently used idle one (freed outside the lock); -EBUSY when every entry
-// is pinned by a call in progress.
+// entry for ws_unpin().
 static void *library_workspace(void *stream, int *slot, int *err)
 {
     int dev = 0;
@@ -4056,8 +3918,9 @@ static void *library_workspace(void *stream, int *slot, int *err)
         *err = -ENODEV;
         return nullptr;
     }
-    WsEntry victim{};
     int v = -1;
+    bool fresh = false, wait = false;
+    hipEvent_t after = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_ws_mu);
         for (int i = 0; i < kWsCache; i++) {
@@ -4070,82 +3933,90 @@ static void *library_workspace(void *stream, int *slot, int *err)
                 return e.ws;
             }
         }
-        // a free entry (no workspace and not reserved by a call that is
-        // allocating one: such an entry is pinned), else the LRU idle one
-        for (int i = 0; i < kWsCache && v < 0; i++)
-            if (!g_ws[i].ws && !g_ws[i].pins) v = i;
-        for (int i = 0; i < kWsCache && v < 0; i++)
-            if (!g_ws[i].pins) v = i;
+        // the least recently used idle workspace of this device, else a
+        // slot never allocated
+        for (int i = 0; i < kWsCache; i++) {
+            const WsEntry &e = g_ws[i];
+            if (e.ws && e.dev == dev && !e.pins && (v < 0 || e.used < g_ws[v].used)) v = i;
+        }
+        if (v < 0)
+            for (int i = 0; i < kWsCache && v < 0; i++)
+                if (!g_ws[i].ws && !g_ws[i].pins) v = i;
         if (v < 0) {
-            *err = -EBUSY;
+            *err = -EBUSY;  // every workspace is in use by a call, or on another device
             return nullptr;
         }
-        if (g_ws[v].ws)
-            for (int i = 0; i < kWsCache; i++)
-                if (g_ws[i].ws && !g_ws[i].pins && g_ws[i].used < g_ws[v].used) v = i;
-        victim = g_ws[v];
-        // reserve the slot (no ws yet: nobody else looks it up) while the
-        // old workspace is freed and the new one allocated
-        g_ws[v] = WsEntry{dev, stream, nullptr, nullptr, ++g_ws_tick, 1, false};
+        WsEntry &e = g_ws[v];
+        fresh = !e.ws;
+        wait = !fresh && e.recorded;
+        after = e.last;
+        if (fresh) e = WsEntry{};
+        e.dev = dev;
+        e.stream = stream;
+        e.used = ++g_ws_tick;
+        e.pins = 1;  // reserved: nobody else takes this slot
+        e.release = false;
     }
-    ws_free(victim);
-    void *p = nullptr;
-    hipEvent_t ev = nullptr;
-    hipError_t e = hipMalloc(&p, b64x_decode_workspace_size(0));
-    if (e == hipSuccess) e = hipMemset(p, 0, b64x_decode_workspace_size(0));
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    int rc = 0;
+    if (fresh) {
+        void *p = nullptr;
+        hipEvent_t ev = nullptr;
+        const uint64_t wsz = b64x_decode_workspace_size(0);
+        hipError_t he = hipMalloc(&p, wsz);
+        if (he == hipSuccess) he = hipMemsetAsync(p, 0, wsz, (hipStream_t) stream);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        if (he != hipSuccess) {
+            if (p) (void) hipFree(p);
+            if (ev) (void) hipEventDestroy(ev);
+            g_ws[v] = WsEntry{};
+            *err = hip_err(he);
+            return nullptr;
+        }
+        g_ws[v].ws = p;
+        g_ws[v].last = ev;
+    } else if (wait) {
+        // the previous stream's last use of it finishes first, on the device
+        rc = hip_err(hipStreamWaitEvent((hipStream_t) stream, after, 0));
+    }
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    if (e != hipSuccess) {
-        if (p) (void) hipFree(p);
-        if (ev) (void) hipEventDestroy(ev);
-        g_ws[v] = WsEntry{};
-        *err = hip_err(e);
+    if (rc) {
+        g_ws[v].stream = nullptr;  // idle again, its event still guards it
+        g_ws[v].pins = 0;
+        *err = rc;
         return nullptr;
     }
-    g_ws[v].ws = p;
-    g_ws[v].last = ev;
     *slot = v;
     *err = 0;
-    return p;
+    return g_ws[v].ws;
 }
 
 // The call that pinned entry `slot` has enqueued its kernels on `stream`:
 // record the entry's last-use event behind them and unpin it.
 static void ws_unpin(int slot, void *stream)
 {
-    WsEntry doomed{};
-    {
-        std::lock_guard<std::mutex> lk(g_ws_mu);
-        WsEntry &e = g_ws[slot];
-        (void) hipEventRecord(e.last, (hipStream_t) stream);
-        if (--e.pins == 0 && e.release) {
-            doomed = e;
-            e = WsEntry{};
-        }
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    WsEntry &e = g_ws[slot];
+    if (hipEventRecord(e.last, (hipStream_t) stream) == hipSuccess) e.recorded = true;
+    if (--e.pins == 0 && e.release) {
+        e.stream = nullptr;
+        e.release = false;
     }
-    ws_free(doomed);
 }
 
 void b64x_release_stream(void *stream)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
-    WsEntry doomed[kWsCache];
-    int n = 0;
-    {
-        std::lock_guard<std::mutex> lk(g_ws_mu);
-        for (int i = 0; i < kWsCache; i++) {
-            WsEntry &e = g_ws[i];
-            if (!e.ws || e.dev != dev || e.stream != stream) continue;
-            if (e.pins) {
-                e.release = true;  // the last unpin frees it
-            } else {
-                doomed[n++] = e;
-                e = WsEntry{};
-            }
-        }
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (int i = 0; i < kWsCache; i++) {
+        WsEntry &e = g_ws[i];
+        if (!e.ws || e.dev != dev || e.stream != stream) continue;
+        if (e.pins)
+            e.release = true;  // the last unpin unbinds it
+        else
+            e.stream = nullptr;  // idle: the next stream waits on its event
     }
-    for (int i = 0; i < n; i++) ws_free(doomed[i]);
 }
 
 __global__ void __launch_bounds__(64) k_result_zero(b64x_dec_result *res, b64x_dec_result *hres,
@@ -4189,10 +4060,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
         static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
-#ifndef B64X_SFX_OCC  // A/B builds only: blocks per CU of the suffix grid (0: occupancy)
-#define B64X_SFX_OCC 0
-#endif
-        const uint32_t sfx_grid = (uint32_t) d->cus * (B64X_SFX_OCC ? B64X_SFX_OCC : occ_sfx);
+        const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
         if (flags & B64X_DEC_EXPECT_JUNK) {
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
@@ -5159,9 +5027,12 @@ uint64_t b64x__test_range_chunks(uint64_t chunks)
 
 const char *b64x_build_info(void)
 {
-    return "b64x abi=2 arch=gfx950 enc:quad12->16 lds-alphabet 1 quad/lane; "
-           "dec:probe+line-model single pass (4 slots/lane) + exact suffix (group sums); "
-           "rows:line model in row bands";
+#define B64X_STR2(x) #x
+#define B64X_STR(x) B64X_STR2(x)
+    return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
+           "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
+           "(count first, decode into LDS windows, shifted stores); rows:line model in row "
+           "bands; lanes:chained decoder blocks";
 }
 
 const char *b64x_strerror(int err)

@@ -563,7 +563,7 @@ def crlf76(chars: torch.Tensor) -> torch.Tensor:
     return out.contiguous()
 
 
-def bench_mime(args, b64, steps=10):
+def bench_mime(args, b64, steps=20):
     """MIME-formatted decode (SURVEY.md §8(d) dirty input): config 2's
     characters and config 4's rows in 76-character CRLF lines, decoded back
     and checked; device-resident, HIP events around each call.  Algorithmic
@@ -577,7 +577,9 @@ def bench_mime(args, b64, steps=10):
     res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
-    def timed(fn):
+    spread = {}
+
+    def timed(fn, name):
         fn()
         torch.cuda.synchronize()
         ts = []
@@ -588,9 +590,11 @@ def bench_mime(args, b64, steps=10):
             e1.record(stream)
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
+        spread[name] = {"ms_min": min(ts), "ms_median": statistics.median(ts), "ms_max": max(ts)}
         return statistics.median(ts)
 
-    ms = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream))
+    ms = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream),
+               "cfg2_crlf76")
     info = b64.Decoded(out, res).info()
     if info.out_len != N or not torch.equal(out[:N], x):
         raise SystemExit("mime decode mismatch")
@@ -614,7 +618,8 @@ def bench_mime(args, b64, steps=10):
         del mask, idx
         out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device="cuda")
         ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device="cuda")
-        ms_j = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream))
+        ms_j = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream),
+                     f"cfg2_junk{d:g}")
         info = b64.Decoded(out, res).info()
         if info.out_len != N or not torch.equal(out[:N], x):
             raise SystemExit(f"junk {d} decode mismatch")
@@ -645,7 +650,8 @@ def bench_mime(args, b64, steps=10):
     cap = 12 * ((D + 15) // 16)
     dec = torch.empty(nbuf * cap, dtype=torch.uint8, device="cuda")
     outlen = torch.zeros(nbuf, dtype=torch.int64, device="cuda")
-    ms4 = timed(lambda: b64.decode_strided(mime, D, D, nbuf, dec, cap, outlen, stream=stream))
+    ms4 = timed(lambda: b64.decode_strided(mime, D, D, nbuf, dec, cap, outlen, stream=stream),
+                "cfg4_crlf76")
     if not (bool((outlen == L).all()) and
             bool(torch.equal(dec.view(nbuf, cap)[:, :L], xr.view(nbuf, L)))):
         raise SystemExit("mime batch decode mismatch")
@@ -654,7 +660,10 @@ def bench_mime(args, b64, steps=10):
              "ms": ms4, "GiB_s": nbuf * L / (ms4 * 1e-3) / 2**30,
              "alg_GBps": alg4 / (ms4 * 1e-3) / 1e9,
              "roofline_frac": alg4 / (ms4 * 1e-3) / (HBM_PEAK_GBS * 1e9)}
-    return {"cfg2_crlf76": single, "cfg4_crlf76": batch, **junk, "unit": "ms, GiB/s payload"}
+    for k, v in (("cfg2_crlf76", single), ("cfg4_crlf76", batch), *junk.items()):
+        v.update(spread[k])
+    return {"cfg2_crlf76": single, "cfg4_crlf76": batch, **junk, "unit": "ms, GiB/s payload",
+            "steps": steps}
 
 
 def bench_cfg5(args, world=1, rank=0):
@@ -1075,6 +1084,11 @@ def main():
             "decode_GBps": per_launch / (r["dec_ms"] * 1e-3) / 1e9,
             "roundtrip_hbm_frac": 2 * per_launch / ((r["enc_ms"] + r["dec_ms"]) * 1e-3)
                                   / (HBM_PEAK_GBS * 1e9),
+            # the headline fraction: both legs' algorithmic bytes over the
+            # timed region's own GPU time per step (HIP events around the K
+            # steps, nothing between them)
+            "timed_region_frac": 2 * per_launch / (r["gpu_ms_per_step"] * 1e-3)
+                                 / (HBM_PEAK_GBS * 1e9),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "+".join(knames),

@@ -110,11 +110,12 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * d_workspace: b64x_decode_workspace_size(nchars) bytes of device memory,
  * zero-filled before its first use (each call leaves it ready for the
  * next; one workspace per stream), or NULL to use a library-owned one
- * per (device, stream) (allocated on the first such call for that stream:
- * that call is not capture-safe).  The library keeps at most 8 such
- * workspaces (about 12.7 MiB of HBM each): a call on a ninth stream frees
- * the least recently used idle one once the work queued on it has finished
- * (-EBUSY if all eight are in use by calls being enqueued right then). */
+ * per (device, stream).  The library keeps at most 8 such workspaces
+ * (about 12.7 MiB of HBM each), allocated on first need and never freed: a
+ * call on a stream without one takes an idle one (its stream made to wait
+ * on the device for the workspace's last use), or -EBUSY if all eight are
+ * in use by calls being enqueued right then.  A call that allocates one is
+ * not capture-safe. */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);
@@ -131,9 +132,9 @@ int b64x_decode_dev_seq(const void *d_in, uint64_t nchars, void *d_out,
  * b64x_session_decode_result), -EAGAIN if it is not (yet). */
 int b64x_result_check(const b64x_dec_result *res, uint64_t nchars, unsigned flags,
                       uint32_t seq);
-/* Free the library-owned decode workspace of `stream` on the current device,
- * if it has one (after waiting for the device); call it before destroying a
- * stream that decoded with d_workspace == NULL. */
+/* Unbind the library-owned decode workspace of `stream` on the current
+ * device, if it has one, so another stream can take it; call it before
+ * destroying a stream that decoded with d_workspace == NULL. */
 void b64x_release_stream(void *stream);
 
 /* ---- batches of independent buffers ----------------------------------- */

@@ -878,7 +878,8 @@ def test_strided_mime_rows_bands_vs_oracle(n, L, sep, nbuf):
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
-    b64x_release_stream frees a stream's one; every result stays exact."""
+    b64x_release_stream unbinds a stream's one for the next; every result
+    stays exact."""
     import ctypes
 
     from async_amd import _lib
@@ -943,14 +944,14 @@ def test_library_workspace_threads_past_the_cache():
         out = torch.zeros(b64.decoded_cap(x.numel()), dtype=torch.uint8, device=DEV)
         res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
         jobs.append({"raw": raw, "x": x, "out": out, "res": res, "st": torch.cuda.Stream(),
-                     "ok": 0, "err": None})
+                     "pinned": lib.b64x_host_alloc(b64.RES_BYTES), "ok": 0, "err": None})
     torch.cuda.synchronize()
     a = b64._abc(None)
 
     def worker(j):
         try:
             st = ctypes.c_void_p(j["st"].cuda_stream)
-            rec = b64.DecResult()
+            rec = b64.DecResult.from_address(j["pinned"])  # pinned: an async D2H
             for rep in range(6):
                 seq = ctypes.c_uint32(0)
                 rc = lib.b64x_decode_dev_seq(ctypes.c_void_p(j["x"].data_ptr()), j["x"].numel(),
@@ -960,7 +961,7 @@ def test_library_workspace_threads_past_the_cache():
                 if rc == -16:  # -EBUSY: every cached entry mid-enqueue
                     continue
                 assert rc == 0, rc
-                assert hip.hipMemcpyAsync(ctypes.addressof(rec), j["res"].data_ptr(),
+                assert hip.hipMemcpyAsync(j["pinned"], j["res"].data_ptr(),
                                           b64.RES_BYTES, 2, st) == 0
                 assert hip.hipStreamSynchronize(st) == 0
                 assert lib.b64x_result_check(ctypes.byref(rec), j["x"].numel(), 0,
@@ -981,6 +982,7 @@ def test_library_workspace_threads_past_the_cache():
         assert j["err"] is None, j["err"]
         assert j["ok"] >= 1
         assert np.array_equal(j["out"][:j["raw"].size].cpu().numpy(), j["raw"])
+        lib.b64x_host_free(j["pinned"])
 
 
 def test_decoded_info_checks_the_record():
