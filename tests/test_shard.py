@@ -150,3 +150,37 @@ def test_bench_refuses_a_mismatched_world():
     line: `--gpus 8` can never report an n_gpus=1 measurement."""
     rc, lines, _ = _bench("--gpus", "2", "--dry-run", env_extra={"WORLD_SIZE": "1"})
     assert rc != 0 and lines == []
+
+
+@pytest.mark.parametrize("world,rank", [(8, 3), (2, 1), (3, 1)])
+def test_batch_digest_check_on_a_share(world, rank):
+    """bench.py's whole-output check of a sharded batch leg (config 3):
+    a rank's share of the buffers, filled from the splitmix64 stream at its
+    own offset (the seed shifted by the share's first word), encoded, and
+    every digested chunk it holds whole compared with
+    tests/golden/batch_digests.json; a corrupted byte is caught.  CPU
+    tensors stand in for the device ones (the check copies to the host)."""
+    import base64
+
+    import numpy as np
+
+    import bench
+    lo, nbuf = shard.by_index(1 << 16, world, rank)
+    L, E = 4096, 5464
+    seed = (0x5EED + (lo * L // 8) * 0x9E3779B97F4A7C15) % (1 << 64)
+    x = util.splitmix64(seed, nbuf * L)
+    assert (x[:L] == util.splitmix64(0x5EED, (lo + 1) * L)[lo * L:]).all()
+    enc = np.frombuffer(b"".join(base64.b64encode(x[i * L:(i + 1) * L].tobytes())
+                                 for i in range(nbuf)), np.uint8).copy()
+    t_enc = torch.from_numpy(enc)
+    got = bench._batch_digest_check("cfg3", lo, nbuf, L, E, None, t_enc, None, 0)
+    c = 1 << 13
+    whole = (lo + nbuf) // c - (lo + c - 1) // c
+    assert got["encode_sha256_ok"] is (True if whole else None)
+    assert got["scope"].startswith(f"{whole} chunks")
+    if whole:
+        b0 = ((lo + c - 1) // c) * c - lo
+        enc[b0 * E + 77] ^= 1
+        with pytest.raises(SystemExit):
+            bench._batch_digest_check("cfg3", lo, nbuf, L, E, None, torch.from_numpy(enc),
+                                      None, 0)
