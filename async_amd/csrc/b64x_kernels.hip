@@ -2320,8 +2320,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // writes the record, waits until every block has left (so no prefix read
 // is in flight), then clears the status and group words, the ticket,
 // `wdone` and the failure words.
-#ifndef B64X_SFX_WPE  // minimum waves per SIMD (80 VGPRs)
-#define B64X_SFX_WPE 6
+#ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD (96 VGPRs)
+#define B64X_SFX_WPE 5
 #endif
 
 // A range's window: relative sextet 0 at window bit kSfxP0 (16 zero bytes
@@ -2494,31 +2494,41 @@ void k_decode_suffix(
         // reduction -- and publish the tile's count at once, so the tiles
         // after it find it published when they take their prefix (counted by
         // the decode itself, every tile waited for its predecessors' whole
-        // decode: 1.9x slower).  The decode below reads the ranges again,
-        // from L2: a few microseconds later, not a whole tile's time later as
-        // round 3's count-ahead did (whose second read came from HBM).
+        // decode: 1.9x slower).  Every range's characters are in flight at
+        // once; the decode below reads them again, from L2, a few
+        // microseconds later (round 3's count-ahead read them again a whole
+        // tile later, from HBM).  The 64 bytes after each range (its last
+        // group's look-ahead) come in with them.
+        uint32_t la[kFusePer];
+        {
+            uint4 c[kFusePer][2];
+            uint32_t nin[kFusePer][2];
 #pragma unroll
-        for (uint32_t j = 0; j < kFusePer; j += 2) {
-            uint4 c[2][2];
-            uint32_t nin[2][2];
-            load(j, c[0], nin[0]);
-            load(j + 1, c[1], nin[1]);
-            uint32_t cnt = 0;
-#pragma unroll
-            for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    uint32_t P[4];
-                    lane_values(sm.tab, c[e][h], nin[e][h], P);
-                    cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
-                            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
-                           << (16 * e);
-                }
+            for (uint32_t j = 0; j < kFusePer; j++) {
+                load(j, c[j], nin[j]);
+                const uint64_t q = (uint64_t) (rw + j + 1) * R + lane;
+                la[j] = rw + j + 1 < nranges && q < n ? in[q] : 0u;
             }
-            const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
-            if (lane == 0) {
-                s_cnt[wv * kFusePer + j] = tot & 0xFFFFu;
-                s_cnt[wv * kFusePer + j + 1] = tot >> 16;
+#pragma unroll
+            for (uint32_t j = 0; j < kFusePer; j += 2) {
+                uint32_t cnt = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < 2; e++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        uint32_t P[4];
+                        lane_values(sm.tab, c[j + e][h], nin[j + e][h], P);
+                        cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
+                                __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
+                               << (16 * e);
+                    }
+                }
+                const uint32_t tot =
+                    (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
+                if (lane == 0) {
+                    s_cnt[wv * kFusePer + j] = tot & 0xFFFFu;
+                    s_cnt[wv * kFusePer + j + 1] = tot >> 16;
+                }
             }
         }
         __syncthreads();
@@ -2538,14 +2548,21 @@ void k_decode_suffix(
         }
         wave_lds_order();
         uint32_t T[kFusePer];
+        {
+            uint4 c[2], cn[2];
+            uint32_t nin[2], nn[2];
+            load(0, c, nin);
 #pragma unroll
-        for (uint32_t j = 0; j < kFusePer; j++) {
-            uint4 c[2];
-            uint32_t nin[2];
-            load(j, c, nin);
-            T[j] = rw + j < nranges
-                       ? bits_step<true>(sm, (uint32_t *) sm.win[wv][j], c, nin, (int) kSfxP0)
-                       : 0u;
+            for (uint32_t j = 0; j < kFusePer; j++) {
+                if (j + 1 < kFusePer) load(j + 1, cn, nn);  // in flight during this decode
+                T[j] = rw + j < nranges
+                           ? bits_step<true>(sm, (uint32_t *) sm.win[wv][j], c, nin, (int) kSfxP0)
+                           : 0u;
+                c[0] = cn[0];
+                c[1] = cn[1];
+                nin[0] = nn[0];
+                nin[1] = nn[1];
+            }
         }
         if (wv == 0) {
             const uint32_t ex = t ? prefix(t) : 0u;
@@ -2570,7 +2587,8 @@ void k_decode_suffix(
             if (!last && Tp > 0 && (Tp & 3)) {
                 for (uint64_t q = re;;) {
                     const bool ok = q + lane < n;
-                    const uint32_t tv = ok ? sm.tab[in[q + lane]] : 0xFFu;
+                    // the first 64 bytes came in with the count's loads
+                    const uint32_t tv = !ok ? 0xFFu : sm.tab[q == re ? la[j] : in[q + lane]];
                     const bool v = tv < 64u;
                     const uint64_t m = __ballot(v);
                     const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -2906,8 +2924,8 @@ struct RowModel {
                             // only filler, so consecutive rows' writes are contiguous)
     uint32_t pad;
     uint64_t m64x;          // ceil(2^64 / Sx)
-    // Row-group mapping of the line-structured hot path (k_decode_rows_lines,
-    // B64X_ROWS_RG): a lane keeps one row slot q for all its U slots, which
+    // Row-group mapping of the line-structured hot path (k_decode_rows_lines):
+    // a lane keeps one row slot q for all its U slots, which
     // lie in rows Ru apart; NB blocks of kThreads lanes cover Ru rows' Sx
     // slots (NB kThreads = Ru Sx = lcm(kThreads, Sx)), so the line position
     // of q is computed once per lane, not once per slot.
@@ -2928,10 +2946,7 @@ DEV unsigned long long *row_fail(void *ws)
     return (unsigned long long *) ((uint8_t *) ws + kWsScratch + sizeof(RowModel));
 }
 
-#ifndef B64X_ROWS_U  // A/B builds only
-#define B64X_ROWS_U 4
-#endif
-constexpr uint32_t kRowsU = B64X_ROWS_U;  // slots per lane of the row kernels
+constexpr uint32_t kRowsU = 4;  // slots per lane of the row kernels
 
 // One slot of a line-structured row: its 16 model characters from the
 // window at its span, checked strictly (interior) or by the prefix rule
@@ -3045,10 +3060,7 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
     // slots, the hot path takes that many per row (at most the launcher's)
     // and fills the slack, so no row leaves a hole between its bytes and the
     // next row's (a hole makes every row's last line a partial write).
-#ifndef B64X_ROWS_SLACK  // A/B builds only: fill each row's slack (0: leave holes)
-#define B64X_ROWS_SLACK 1
-#endif
-    r.Sx = B64X_ROWS_SLACK && r.L && out_stride % 12 == 0
+    r.Sx = r.L && out_stride % 12 == 0
                ? (out_stride / 12 < S ? (uint32_t) (out_stride / 12) : S) : Sr;
     const uint32_t Sq = r.L ? r.Sx : Sr;
     r.m64x = ~0ull / r.Sx + 1;
@@ -3087,9 +3099,6 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
 // (k_rows_finish); nothing else is written per row.  Blocks that touch the
 // last row ("tail", block-uniform) read page-safely and store only decoded
 // bytes, so one launch covers the batch.
-#ifndef B64X_ROWS_WPE  // A/B builds only: minimum waves per SIMD
-#define B64X_ROWS_WPE 1
-#endif
 
 // Mark the rows of this u-step's failing lanes: the first failing lane of
 // each row among the wave's lanes (rows are contiguous runs of lanes: lane
@@ -3103,11 +3112,8 @@ DEV void mark_failed_rows(unsigned long long *bm, uint64_t junk, uint32_t q, uin
         atomicOr(bm + (row >> 6), 1ull << (row & 63));
 }
 
-#ifndef B64X_ROWS_SEPBR  // A/B builds only: 0 = branch-free separator check
-#define B64X_ROWS_SEPBR 1
-#endif
 template <int U, bool O32>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_ROWS_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1)))
 void k_decode_rows_lines(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
     uint8_t *__restrict__ out, uint64_t out_stride, uint32_t S, uint32_t magic, uint64_t m64,
@@ -3139,11 +3145,8 @@ void k_decode_rows_lines(
         const uint32_t Sm = rm.S;
         const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
         const uint32_t Sx = (uint32_t) scalar_load_u64(rmw + 8);
-#ifndef B64X_ROWS_RG  // A/B builds only: 0 = every MIME batch through the general path
-#define B64X_ROWS_RG 1
-#endif
         const uint64_t r10 = scalar_load_u64(rmw + 10), r11 = scalar_load_u64(rmw + 11);
-        if (B64X_ROWS_RG && O32 && rcpS && (rm.L & 3) == 0 && (uint32_t) (r11 >> 32)) {
+        if (O32 && rcpS && (rm.L & 3) == 0 && (uint32_t) (r11 >> 32)) {
             const uint32_t NB = (uint32_t) r10, Ru = (uint32_t) (r10 >> 32), mx = (uint32_t) r11;
             const uint32_t st = blockIdx.x / NB, bi = blockIdx.x - st * NB;  // scalar
             const uint64_t row_st = (uint64_t) st * (U * Ru);  // the block's first row
@@ -3159,7 +3162,7 @@ void k_decode_rows_lines(
             const uint32_t spanL = len - (dL * rm.P + colL);
             const uint32_t nsepL = rm.L - colL > 16 || cL > kq ? 0u
                                  : (spanL - cL < rm.s ? spanL - cL : rm.s);
-            const uint32_t need_L = sep_need(nsepL), need_s = sep_need(rm.s);
+            const uint32_t need_L = sep_need(nsepL);
             const uint32_t kmask = 128u * (kq >= 16 ? 0xFFFFu : (1u << kq) - 1u);
             const uint32_t expm = j0 == kNoRowShape ? 1u : kmask & ~(128u * ((1u << j0) - 1u));
             // the lane's slot q and row in the band, once for its U slots
@@ -3174,7 +3177,6 @@ void k_decode_rows_lines(
             const bool last = q == Sm - 1;
             const bool hs = rm.L - col <= 16;
             const uint32_t c = hs ? rm.L - col : 16u;
-            const uint32_t need = last ? need_L : hs ? need_s : 0u;  // separator bytes to check
             const uint32_t ioff = __umul24(rin, (uint32_t) in_stride) + (pos & ~3u);
             const uint32_t ooff = __umul24(rin, (uint32_t) out_stride) + __umul24(q, 12u);
             // one 64-bit base per block; every lane offset is 32-bit (the
@@ -3219,13 +3221,11 @@ void k_decode_rows_lines(
                     m128 += (g & 2) ? part << 8 : part;
                 }
                 uint32_t bad = last ? (m128 & kmask) ^ expm : m128;
-                if (B64X_ROWS_SEPBR) {
-                    if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
-                             : (hs && !sep_ok_s(tab, sep, rm.s)))
-                        bad |= 1u;
-                } else {
-                    bad |= (sep_nonalpha(tab, sep) & need) ^ need;  // need: per lane, above
-                }
+                // separator bytes outside the alphabet (a branch per kind of
+                // slot: the branch-free form checked every lane's 4 bytes)
+                if (last ? (need_L && (sep_nonalpha(tab, sep) & need_L) != need_L)
+                         : (hs && !sep_ok_s(tab, sep, rm.s)))
+                    bad |= 1u;
                 if (q >= Sm || !live) bad = 0;  // slack filler: the bytes are scratch
                 uint32_t o0, o1, o2;
                 groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);

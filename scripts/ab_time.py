@@ -87,6 +87,9 @@ def child(lib, steps, only=()):
     timeit("crlf_ej", lambda: b64.decode(dirty, out=out, workspace=ws, result=rr,
                                          expect_junk=True))
     ok = chk("crlf_ej", torch.equal(out[:n], x))
+    timeit("clean_ej", lambda: b64.decode(enc, out=out, workspace=ws, result=rr,
+                                          expect_junk=True))
+    ok = chk("clean_ej", torch.equal(out[:n], x))
     # config 4: 1 M x 1 KiB rows, strided decode (clean)
     del dirty, junk, junk1, enc, out, x
     if only and not ({"rows_enc", "rows_dec", "rows_crlf", "ragged_dec"} & set(only)):
@@ -170,7 +173,7 @@ def main():
                 sys.exit(p.returncode or 1)
             d = json.loads(line[-1])
             print(json.dumps(d), flush=True)
-            for k in ("copy_enc", "copy_dec", "encode", "decode", "crlf", "junk", "junk1", "junk_ej", "crlf_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
+            for k in ("copy_enc", "copy_dec", "encode", "decode", "crlf", "junk", "junk1", "junk_ej", "crlf_ej", "clean_ej", "rows_enc", "rows_dec", "rows_crlf", "ragged_dec"):
                 agg[lib].setdefault(k, []).append(d[k][0])
     for lib in a.libs:
         print(json.dumps({"summary": lib, **{k: round(statistics.median(v), 1)
