@@ -39,7 +39,7 @@ OBJDIR   = build
 KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
 HOST_SRC   = async_amd/csrc/fsalloc.c async_amd/csrc/loop.c async_amd/csrc/streams.c \
              async_amd/csrc/framing.c async_amd/csrc/fdstreams.c async_amd/csrc/b64_hub.c \
-             async_amd/csrc/b64_stages.c
+             async_amd/csrc/b64_stages.c async_amd/csrc/b64_pin.c
 HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
@@ -60,7 +60,7 @@ $(OBJDIR):
 $(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h | $(OBJDIR)
+$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h async_amd/csrc/b64_pin.h | $(OBJDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(OBJDIR)/b64x_kernels_hooks.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)

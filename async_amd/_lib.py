@@ -103,7 +103,7 @@ SIGNATURES = {
     "b64x_lane_close": (None, [_vp]),
     "b64x_lane_acquire": (_vp, []),
     "b64x_lane_release": (None, [_vp]),
-    "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _ap, _vp, _vp]),
+    "b64x_lane_encode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _ap, _vp, _vp]),
     "b64x_lane_encode_check": (_int, [_vp]),
     "b64x_lane_decode_async": (_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ap,
                                       _vp, _vp, ctypes.POINTER(_u32)]),

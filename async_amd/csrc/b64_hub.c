@@ -24,6 +24,7 @@
  */
 #define _GNU_SOURCE
 #include "b64_hub.h"
+#include "b64_pin.h"
 #include "fsalloc.h"
 
 #include <errno.h>
@@ -49,6 +50,7 @@ enum {
     HUB_JOBS = 1 << 16,     /* jobs per arena */
     HUB_DEPTH = 8,          /* reservations open at once (stages reading
                                through stages, see b64_hub_reserve) */
+    HUB_SEGS = 1 << 14,     /* lent segments per arena (more are copied) */
     LANE_QUEUE = 4,         /* decode batches queued on one lane: a batch
                                whose chained jobs continue streams of a batch
                                in flight on that lane waits behind it there */
@@ -65,6 +67,10 @@ struct b64_batch {
     b64x_dec_result *h_res;      /* pinned, HUB_JOBS: decode jobs' records */
     b64x_dec_result *h_spell;    /* pinned, HUB_JOBS: chained jobs' spell logs */
     const b64x_dec_result **h_prev; /* HUB_JOBS: chained jobs' predecessor records */
+    b64x_seg *h_seg;             /* pinned, HUB_SEGS: encode input lent from pinned
+                                    messages (b64_hub_lend), by device offset */
+    b64_pin_slab **pins;         /* HUB_SEGS: the slab each segment holds */
+    uint32_t nseg;
     b64_batch *after;            /* a batch in flight (or ready) whose records
                                     chained jobs of this one read: this one
                                     runs behind it on its lane */
@@ -111,8 +117,11 @@ struct b64_hub {
     struct {                     /* ASYNC_B64_HUB_TRACE=1: printed at teardown */
         bool on;
         unsigned long batches, jobs, allocs, wake_calls, max_ready;
-        unsigned long long in_bytes, out_bytes;
+        unsigned long long in_bytes, out_bytes, gather_bytes;
+        unsigned long reserves, lent_jobs;
+        unsigned long long lent_bytes;
         double wake_s, launch_s, t_first, t_last;
+        double gather_s, reserve_s; /* the stages' upstream reads; arena reservations */
     } tr;
 };
 
@@ -160,6 +169,8 @@ static void batch_free(b64_batch *b)
     b64x_host_free(b->h_flags);
     b64x_host_free(b->h_res);
     b64x_host_free(b->h_spell);
+    b64x_host_free(b->h_seg);
+    free(b->pins);
     free(b->h_prev);
     free(b->jobs);
     free(b);
@@ -182,10 +193,12 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     b->h_res = b64x_host_alloc(HUB_JOBS * sizeof(b64x_dec_result));
     b->h_spell = b64x_host_alloc(HUB_JOBS * sizeof(b64x_dec_result));
     b->h_prev = calloc(HUB_JOBS, sizeof *b->h_prev);
+    b->h_seg = b64x_host_alloc(HUB_SEGS * sizeof *b->h_seg);
+    b->pins = calloc(HUB_SEGS, sizeof *b->pins);
     b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
     b->lane = -1;
     if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_flags || !b->h_res ||
-        !b->h_spell || !b->h_prev || !b->jobs) {
+        !b->h_spell || !b->h_prev || !b->h_seg || !b->pins || !b->jobs) {
         batch_free(b);
         errno = ENOMEM;
         return NULL;
@@ -198,6 +211,9 @@ static void schedule_kick(b64_hub *h);
 /* Back to the process pool (or freed); wakes stages waiting for room. */
 static void batch_put(b64_batch *b)
 {
+    for (uint32_t i = 0; i < b->nseg; i++) /* the GPU has read them (or never will) */
+        b64_pin_unref(b->pins[i]);
+    b->nseg = 0;
     b->state = B_FREE;
     b->in_used = b->out_used = 0;
     b->njobs = 0;
@@ -349,7 +365,8 @@ static void launch_ready(b64_hub *h)
                                               b->h_prev, b->h_spell, &b->abc, batch_done, b,
                                               &b->seq)
                      : b64x_lane_encode_async(h->lanes[i], b->h_in, b->njobs, b->h_in_off,
-                                              b->h_out, b->h_out_off, &b->abc, batch_done, b);
+                                              b->h_out, b->h_out_off, b->h_seg, b->nseg,
+                                              &b->abc, batch_done, b);
         if (rc) { /* report through the normal completion path */
             /* work queued before the failure may still write into the
              * arena: wait for it, so the arena is idle when it is recycled */
@@ -597,10 +614,13 @@ static void hub_teardown(b64_hub *h)
         fprintf(stderr,
                 "b64_hub: batches %lu jobs %lu in %llu out %llu allocs %lu "
                 "max_ready %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f "
-                "first %.6f last %.6f\n",
+                "first %.6f last %.6f gather_s %.4f gather_bytes %llu reserve_s %.4f "
+                "reserves %lu lent_segs %lu lent_bytes %llu\n",
                 h->tr.batches, h->tr.jobs, h->tr.in_bytes, h->tr.out_bytes,
                 h->tr.allocs, h->tr.max_ready, h->tr.wake_calls, h->tr.wake_s,
-                h->tr.launch_s, h->tr.t_last - h->tr.t_first, h->tr.t_first, h->tr.t_last);
+                h->tr.launch_s, h->tr.t_last - h->tr.t_first, h->tr.t_first, h->tr.t_last,
+                h->tr.gather_s, h->tr.gather_bytes, h->tr.reserve_s, h->tr.reserves,
+                h->tr.lent_jobs, h->tr.lent_bytes);
     pthread_mutex_lock(&registry_lock);
     for (b64_hub **p = &registry; *p; p = &(*p)->next_hub) {
         if (*p == h) {
@@ -673,8 +693,8 @@ void b64_hub_forget(b64_hub *h, void *obj, bool waiting)
  * 123-151).  Each open reservation has its own arena (filling[depth]), so
  * an inner reservation never moves, seals or recycles an outer one.
  */
-uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
-                         size_t room, size_t min_room, size_t *granted, action_1 waiter)
+static uint8_t *reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
+                        size_t room, size_t min_room, size_t *granted, action_1 waiter)
 {
     if (h->depth == HUB_DEPTH) {
         errno = ELOOP; /* stages nested deeper than HUB_DEPTH */
@@ -726,6 +746,29 @@ uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc
     return b->h_in + b->in_used;
 }
 
+uint8_t *b64_hub_reserve(b64_hub *h, b64_hub_kind kind, const b64x_alphabet *abc,
+                         size_t room, size_t min_room, size_t *granted, action_1 waiter)
+{
+    if (!h->tr.on)
+        return reserve(h, kind, abc, room, min_room, granted, waiter);
+    double t0 = mono_s(); /* includes the launches of the batches it seals */
+    uint8_t *p = reserve(h, kind, abc, room, min_room, granted, waiter);
+    h->tr.reserve_s += mono_s() - t0;
+    h->tr.reserves++;
+    return p;
+}
+
+bool b64_hub_tracing(const b64_hub *h)
+{
+    return h->tr.on;
+}
+
+void b64_hub_trace_gather(b64_hub *h, double secs, size_t bytes)
+{
+    h->tr.gather_s += secs;
+    h->tr.gather_bytes += bytes;
+}
+
 bool b64_hub_chainable(b64_hub *h, const b64_ticket *prev)
 {
     const b64_batch *p = prev->batch;
@@ -774,9 +817,39 @@ void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
     schedule_flush(h);
 }
 
+static atomic_ulong lent_total; /* segments lent, process-wide (tests) */
+
+unsigned long b64_hub_lent_total(void)
+{
+    return atomic_load_explicit(&lent_total, memory_order_relaxed);
+}
+
+bool b64_hub_lend(b64_hub *h, size_t pos, const uint8_t *src, size_t n, b64_pin_slab *slab)
+{
+    b64_batch *b = h->depth ? h->filling[h->depth - 1] : NULL;
+    if (!b || b->kind != B64_HUB_ENCODE || b->nseg == HUB_SEGS || !n)
+        return false;
+    const uint64_t off = b->in_used + pos;
+    if (b->nseg && b->h_seg[b->nseg - 1].off + b->h_seg[b->nseg - 1].len > off)
+        return false; /* out of order: never, for one gather */
+    b->h_seg[b->nseg] = (b64x_seg) { off, n, src };
+    b->pins[b->nseg++] = slab;
+    b64_pin_ref(slab);
+    atomic_fetch_add_explicit(&lent_total, 1, memory_order_relaxed);
+    if (h->tr.on) {
+        h->tr.lent_jobs++;
+        h->tr.lent_bytes += n;
+    }
+    return true;
+}
+
 void b64_hub_cancel(b64_hub *h)
 {
-    h->depth--; /* nothing was recorded */
+    b64_batch *b = h->filling[--h->depth];
+    /* segments lent into the cancelled reservation (none in practice: a
+     * block that took bytes is committed) */
+    while (b && b->nseg && b->h_seg[b->nseg - 1].off >= b->in_used)
+        b64_pin_unref(b->pins[--b->nseg]);
 }
 
 void b64_ticket_release(b64_ticket *t)

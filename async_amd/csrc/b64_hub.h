@@ -30,6 +30,7 @@
 
 typedef struct b64_hub b64_hub;
 typedef struct b64_batch b64_batch;
+struct b64_pin_slab;
 
 /* One committed block, owned by the stage. */
 typedef struct {
@@ -89,7 +90,21 @@ void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
  * of non-alphabet characters first): the device spells prev's held-back
  * sextets into the head between prev's decode and its own. */
 bool b64_hub_chainable(b64_hub *h, const b64_ticket *prev);
+/* While a reservation of an encode block is open: its bytes [pos, pos+n)
+ * are not written into the arena but lent -- they are at `src`, in a pinned
+ * message of `slab` (b64_pin.h).  The batch holds a reference on the slab
+ * until it has finished, and its lane reads the bytes straight from there
+ * (b64x_lane_encode_async, h_seg).  False (nothing recorded: copy them
+ * instead) when the arena's segment table is full. */
+bool b64_hub_lend(b64_hub *h, size_t pos, const uint8_t *src, size_t n,
+                  struct b64_pin_slab *slab);
+/* Segments lent so far in this process (tests). */
+unsigned long b64_hub_lent_total(void);
 void b64_hub_cancel(b64_hub *h);
+/* ASYNC_B64_HUB_TRACE=1: the stages add the time of their upstream reads
+ * (the copies into the arenas) to the hub's trace line. */
+bool b64_hub_tracing(const b64_hub *h);
+void b64_hub_trace_gather(b64_hub *h, double secs, size_t bytes);
 /* The stage is done with the ticket (consumed, or closing before the
  * batch finished: its output is then discarded). */
 void b64_ticket_release(b64_ticket *t);

@@ -63,6 +63,11 @@
  *   ASYNC_B64_MIN_PULL        gather at least this much from upstream
  *                             before launching, unless it runs dry
  *                             (default 64 KiB)
+ *   ASYNC_B64_LEND_MIN        encoder: a queued message of at least this
+ *                             many unread bytes (copied into pinned memory
+ *                             by queuestream_enqueue_bytes, b64_pin.h) is
+ *                             taken without copying (default 4 KiB; shorter
+ *                             ones are gathered into a block together)
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -70,11 +75,13 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "async.h"
 #include "b64_hub.h"
 #include "b64_lend.h"
+#include "b64_pin.h"
 #include "b64_trace.h"
 #include "b64x.h"
 #include "base64decoder.h"
@@ -111,6 +118,7 @@ struct stage {
     direction dir;
     b64x_alphabet abc;
     size_t cap, min_pull, max_cap;
+    size_t lend_min;    /* encoder: pinned messages this long are lent */
     b64_hub *hub;       /* the loop's batching hub */
     unsigned hub_waits; /* entries on the hub's waiter list (room for a block) */
     bool started;       /* the hub is held */
@@ -129,6 +137,7 @@ struct stage {
     uint8_t *spill;     /* lent copy of reads that span blocks (no fallback) */
     size_t spill_cap;
     const uint8_t *lent;/* what the last read lent, until returned */
+    uint8_t tail[2];    /* encoder: the last two bytes of the block being gathered */
 };
 
 static size_t env_size(const char *name, size_t dflt, size_t lo)
@@ -191,6 +200,7 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->abc = abc;
     st->cap = env_size("ASYNC_B64_STAGE_CAPACITY", (size_t) 1 << 20, 64);
     st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
+    st->lend_min = env_size("ASYNC_B64_LEND_MIN", 4096, 1);
     st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
     st->skip = skip_char(&abc);
     for (int i = 0; i < NSLOTS; i++)
@@ -253,37 +263,94 @@ static void stage_stop(stage *st)
     st->started = false;
 }
 
-/* Pull from upstream into dst until at least min_pull bytes have come
- * in, or EOF, EAGAIN or an error; after a short read it asks once more,
- * so the EOF of a finite upstream lands in the same block.  Returns bytes
- * gathered; *eof / *err report why it stopped. */
+/* Pull from upstream into the reservation `in` from offset `at` on, until
+ * at least min_pull bytes have come in, or EOF, EAGAIN or an error; after
+ * a short read it asks once more, so the EOF of a finite upstream lands in
+ * the same block.  Returns bytes gathered; *eof / *err report why it
+ * stopped.  Encoder: a queued message with at least lend_min unread bytes
+ * in pinned memory (queuestream_enqueue_bytes, b64_pin.h) is not copied --
+ * its bytes become a segment of the block that the GPU reads from where
+ * they are (b64_hub_lend) -- when the hub has room for the segment; and
+ * st->tail gets the block's last two bytes wherever they came from. */
 FSTRACE_DECL(ASYNC_BASE64DECODER_READ_INPUT_DUMP, "UID=%64u DATA=%A");
 
-static size_t gather(stage *st, uint8_t *dst, size_t room, bool *eof,
-                     int *err)
+static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, int *err)
 {
+    uint8_t *dst = in + at;
     size_t got = 0;
     size_t want = st->min_pull < room ? st->min_pull : room;
     *eof = false;
     *err = 0;
+    struct timespec t0 = { 0, 0 };
+    const bool tr = b64_hub_tracing(st->hub);
+    if (tr)
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (st->dir == DIR_ENCODE) /* the block so far: the carry */
+        for (size_t i = 0; i < at; i++)
+            st->tail[0] = st->tail[1], st->tail[1] = in[i];
+    bool lent_last = false; /* the last bytes came by lending */
     while (got < room) {
         size_t ask = room - got;
+        const uint8_t *lp;
+        size_t ln;
+        struct b64_pin_slab *ls;
+        if (st->dir == DIR_ENCODE && b64_src_peek(st->up, &lp, &ln, &ls) && ln >= st->lend_min) {
+            size_t n = ln < ask ? ln : ask;
+            if (b64_hub_lend(st->hub, at + got, lp, n, ls)) {
+                b64_src_take(st->up, n);
+                if (n >= 2) {
+                    st->tail[0] = lp[n - 2];
+                    st->tail[1] = lp[n - 1];
+                } else {
+                    st->tail[0] = st->tail[1];
+                    st->tail[1] = lp[0];
+                }
+                got += n;
+                lent_last = true;
+                if (got >= want)
+                    break;
+                continue;
+            }
+        }
+        if (st->dir == DIR_ENCODE) {
+            ask = b64_src_plain(st->up, st->lend_min, ask);
+            if (!ask) /* a lendable message comes next, but the hub is full */
+                ask = room - got;
+        }
         ssize_t n = bytestream_1_read(st->up, dst + got, ask);
         if (st->dir == DIR_DECODE)
             FSTRACE(ASYNC_BASE64DECODER_READ_INPUT_DUMP, st->uid, dst + got, n);
         if (n < 0) {
             *err = errno ? errno : EIO;
+            /* after lent bytes, the queue's own read would have returned
+             * them as a short count (ref src/queuestream.c read loop) */
+            if (lent_last && *err == EAGAIN)
+                st->short_seen = true;
             break;
         }
         if (n == 0) {
             *eof = true;
             break;
         }
+        lent_last = false;
+        if (n >= 2) {
+            st->tail[0] = dst[got + (size_t) n - 2];
+            st->tail[1] = dst[got + (size_t) n - 1];
+        } else {
+            st->tail[0] = st->tail[1];
+            st->tail[1] = dst[got];
+        }
         got += (size_t) n;
         if ((size_t) n < ask)
             st->short_seen = true;
         else if (got >= want)
             break;
+    }
+    if (tr) {
+        struct timespec t1;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        b64_hub_trace_gather(st->hub, (double) (t1.tv_sec - t0.tv_sec) +
+                                          1e-9 * (double) (t1.tv_nsec - t0.tv_nsec), got);
     }
     return got;
 }
@@ -359,8 +426,7 @@ static int top_up_encoder(stage *st)
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;
-        size_t got = gather(st, in + st->ncarry, room - st->ncarry, &eof,
-                            &uerr);
+        size_t got = gather(st, in, st->ncarry, room - st->ncarry, &eof, &uerr);
         size_t total = st->ncarry + got;
         /* The block encodes all `total` bytes.  Its full sextets,
          * floor(8*total/6) characters, are served now -- the reference
@@ -382,7 +448,8 @@ static int top_up_encoder(stage *st)
                 return uerr ? uerr : EAGAIN;
             }
             st->ncarry = total % 3;
-            memcpy(st->carry, in + total - st->ncarry, st->ncarry);
+            /* the block's last bytes (lent ones are not in the arena) */
+            memcpy(st->carry, st->tail + 2 - st->ncarry, st->ncarry);
         }
         slot_arm(st, sl);
         sl->out_len = (size_t) b64x_encoded_len(total, st->abc.pad);
@@ -433,7 +500,7 @@ static int top_up_decoder(stage *st)
         }
         bool eof;
         int uerr;
-        size_t got = gather(st, in + DEC_HEAD, room - DEC_HEAD, &eof, &uerr);
+        size_t got = gather(st, in, DEC_HEAD, room - DEC_HEAD, &eof, &uerr);
         if (eof) {
             st->final_queued = true;
             if (got == 0 && !pending && st->ncarry == 0) { /* nothing held back: done */
@@ -638,8 +705,12 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
                 return stage_fail(st, rc);
             return (ssize_t) n;
         }
-        if (blocked) {
-            errno = EAGAIN; /* the completion brings the consumer back */
+        if (blocked || staged) {
+            /* blocked: the completion brings the consumer back; staged but
+             * short of `count` while upstream answered EAGAIN: so does
+             * upstream's callback (a full-or-EAGAIN upstream makes the
+             * reference return EAGAIN here too, never a short count) */
+            errno = EAGAIN;
             return -1;
         }
         if (st->nbusy) { /* finished slots with nothing left to serve */

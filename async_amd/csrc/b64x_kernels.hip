@@ -891,11 +891,10 @@ struct DecodeWs {
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
-// Ranges per wave of a single-pass decode tile (k_decode_suffix): each is
-// decoded into its own LDS window before the tile's prefix is known, so a
-// block holds kFusePer x 4 windows of ~1.6 KB (6 blocks per CU).
+// Ranges per wave of a single-pass decode tile (k_decode_suffix): a block
+// holds two tiles' characters in LDS, 2 KiB per range.
 #ifndef B64X_FUSE_PER  // A/B builds only
-#define B64X_FUSE_PER 4
+#define B64X_FUSE_PER 2
 #endif
 constexpr uint32_t kFusePer = B64X_FUSE_PER;
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
@@ -1500,7 +1499,9 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
 // sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
 // up to 18 bits past the window's byte 4: skipped sextets land in its
 // head).  Returns the step's alphabet characters.
-template <bool BE = false, class SM = P2dSmem>
+// VALS: c[] already holds the table values (lane_values, beyond-end bytes
+// marked), as k_decode_suffix's count leaves them in LDS.
+template <bool BE = false, class SM = P2dSmem, bool VALS = false>
 DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
@@ -1511,7 +1512,14 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
     uint32_t P[2][4], sel[2][4], six[2][4], cnt = 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        lane_values(sm.tab, c[h], nin[h], P[h]);
+        if (VALS) {
+            P[h][0] = c[h].x;
+            P[h][1] = c[h].y;
+            P[h][2] = c[h].z;
+            P[h][3] = c[h].w;
+        } else {
+            lane_values(sm.tab, c[h], nin[h], P[h]);
+        }
         uint32_t nb6 = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -2108,9 +2116,12 @@ void k_decode_lines(
 // flushed between steps and its partial dword carried to the front (as
 // decode_buf_bits does); the bytes flushed early are final and never reach
 // the next range's output.
+// VALS: c[] and la_lds hold table values (k_decode_suffix), not characters.
+template <bool VALS = false>
 DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ in, uint64_t n,
                       uint64_t start, uint64_t re, int T0, uint8_t *ob, const uint4 c[2],
-                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold)
+                      const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold,
+                      const uint8_t *la_lds = nullptr, bool la_late = false)
 {
     const uint32_t lane = lane_id();
     uint32_t *bits = (uint32_t *) bq;
@@ -2128,7 +2139,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     // the first step from the chunks given (its own code: joined with the
     // loads of the later steps, the compiler waited for every load in
     // flight before the step, ranges read ahead included)
-    T += (int) bits_step<true>(sm, bits, c, nin, pb0 + 6 * T);
+    T += (int) bits_step<true, P2dSmem, VALS>(sm, bits, c, nin, pb0 + 6 * T);
     for (uint64_t pos = start + 2 * kChunk; pos < re; pos += 2 * kChunk) {
         // more of this range: flush the window's whole blocks and carry the
         // partial one to the front
@@ -2160,10 +2171,18 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     }
     bool at_end = last;
     if (!last && T > 0 && (T & 3)) {
-        // complete the range's last group from the characters after it
+        // complete the range's last group from the characters after it:
+        // given (la, la_ok), in LDS at la_lds (the next range's first
+        // characters, k_decode_suffix), or read from `in` only now (la_late)
         bool ok = la_ok;
+        bool val = false;  // la is a table value
+        if (la_lds || la_late) {
+            ok = re + lane < n;
+            la = !ok ? 0u : la_lds ? la_lds[lane] : in[re + lane];
+            val = VALS && la_lds;
+        }
         for (uint64_t q = re;;) {
-            const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+            const uint32_t t = !ok ? 0xFFu : val ? la : sm.tab[la];
             const bool v = t < 64u;
             const uint64_t m = __ballot(v);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -2184,6 +2203,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
             }
             ok = q + lane < n;
             la = ok ? in[q + lane] : 0u;
+            val = false;
         }
     }
     wave_lds_order();
@@ -2303,37 +2323,28 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
 // tiles of kFuseTile ranges (kFusePer per wave) from a ticket in the order
 // they start, so a tile's predecessors are running or done whatever else
-// shares the GPU.  Decode first, place later: each wave decodes each of its
-// ranges into an LDS window of its own as the bit stream of the range's
-// sextets from sextet 0 at a fixed window bit (bits_step: what a range
-// decodes to depends on where it starts only through a shift), which also
-// counts them; the tile's count is published, its prefix taken (the counts
-// of the tiles before it in its group of 64 tiles, one status word per lane,
-// plus the sums of the earlier groups: one memory round trip at any depth),
-// and each range's bytes are stored from its window with the shift its
-// start's group phase needs, its last group completed from the characters
-// after it.  Every character is read from HBM once and looked up once.
-// (Round 3's form counted a tile one tile ahead, then read and looked up
-// every range again to decode it: 2.0x the input read from HBM, twice the
-// table work -- profiles/r03_g_pmc_junk005.txt.)  Every block counts itself
-// out in `wdone` when it leaves; the block that decodes the last tile
-// writes the record, waits until every block has left (so no prefix read
-// is in flight), then clears the status and group words, the ticket,
-// `wdone` and the failure words.
-#ifndef B64X_SFX_WPE  // A/B builds only: minimum waves per SIMD (96 VGPRs)
-#define B64X_SFX_WPE 5
-#endif
-
-// A range's window: relative sextet 0 at window bit kSfxP0 (16 zero bytes
-// before it absorb the store shift), 2,048 characters' 1,536 bytes, up to 3
-// completing sextets, and the shift's read-ahead.
-constexpr uint32_t kSfxP0 = 128;
-constexpr uint32_t kSfxWin = 100;  // uint4 per window
-struct __attribute__((aligned(16))) SfxSmem {
-    uint8_t tab[256];
-    uint32_t sel[16];
-    uint4 win[kWavesPerBlock][kFusePer][kSfxWin];
-};
+// shares the GPU.  A tile is read from HBM once and every character looked
+// up once: a block draws its NEXT tile, counts it (all of the tile's loads
+// in flight at once) leaving each character's table value in LDS, and
+// publishes its count; then it takes the current tile's prefix and decodes
+// the current tile from the table values in LDS with decode_range.  So a
+// tile is counted one tile before it is decoded, and the prefix waits only
+// for tiles drawn before it -- which, counted right after they were drawn,
+// are.  (Counting a tile only after decoding the one before it made every
+// prefix wait on tiles still being decoded: the grid ran nearly serially,
+// 6 ms for 1 GiB.)  The prefix
+// is not a chained look-back: it is the counts of the tiles before it in
+// its group of 64 tiles (one status word per lane) plus the sums of the
+// earlier groups (every tile adds its count into its group's word), all
+// loaded at once: one memory round trip at any depth.  A range's last
+// group is completed from the first characters of the range after it, in
+// LDS unless that range is in the next tile.  (Round 3's form counted a
+// tile from HBM and read it again from HBM to decode it, a whole tile
+// later: 2.0x the input fetched, profiles/r03_g_pmc_junk005.txt.)  Every
+// block counts itself out in `wdone` when it leaves; the block that decodes
+// the last tile writes the record, waits until every block has left (so no
+// prefix read is in flight), then clears the status and group words, the
+// ticket, `wdone` and the failure words.
 
 // The idle test of k_decode_suffix<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
@@ -2376,57 +2387,18 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
     return true;
 }
 
-// 32 stream bits from window bit x (big-endian dwords, or_field<true>).
-DEV uint32_t win_bits32(const uint32_t *wd, uint32_t x)
-{
-    const uint32_t d = x >> 5, q = x & 31u;
-    return q ? __builtin_amdgcn_alignbit(wd[d], wd[d + 1], 32u - q) : wd[d];
-}
+// The count leaves each character's table value in LDS in its place, so
+// the decode looks every character up once.
+#ifndef B64X_SFX_VALS  // A/B builds only
+#define B64X_SFX_VALS 1
+#endif
+constexpr bool kSfxVals = B64X_SFX_VALS;
 
-// Store stream bytes [0, nbytes) of a window whose byte 0 starts at window
-// bit x_start, to ob: aligned 16-byte blocks of output (lane k the k-th:
-// five dwords read, four funnel shifts by the same amount, one non-temporal
-// dwordx4), the partial head and tail blocks by byte stores (up to 15
-// each, one store of up to 30 lanes).
-DEV void store_shifted(const uint4 *win, uint32_t x_start, uint32_t nbytes, uint8_t *ob)
-{
-    if (!nbytes) return;
-    const uint32_t lane = lane_id();
-    const uint32_t *wd = (const uint32_t *) win;
-    const uint32_t a = (uint32_t) ((uintptr_t) ob & 15);
-    uint8_t *base = ob - a;              // byte k of the output sits at base + a + k
-    const uint32_t x0 = x_start - 8 * a; // window bit of base's byte (x_start >= 8 * 15)
-    const uint32_t end = a + nbytes;
-    const uint32_t klo = (a + 15) >> 4, khi = end >> 4;  // whole blocks [klo, khi)
-    const uint32_t q = x0 & 31u, dq = x0 >> 5;
-    for (uint32_t k = klo + lane; k < khi; k += 64) {
-        const uint32_t d = dq + 4 * k;
-        const uint32_t w0 = wd[d], w1 = wd[d + 1], w2 = wd[d + 2], w3 = wd[d + 3], w4 = wd[d + 4];
-        uint32_t o0 = w0, o1 = w1, o2 = w2, o3 = w3;
-        if (q) {
-            o0 = __builtin_amdgcn_alignbit(w0, w1, 32u - q);
-            o1 = __builtin_amdgcn_alignbit(w1, w2, 32u - q);
-            o2 = __builtin_amdgcn_alignbit(w2, w3, 32u - q);
-            o3 = __builtin_amdgcn_alignbit(w3, w4, 32u - q);
-        }
-        __builtin_nontemporal_store(u32x4a16{bswap32(o0), bswap32(o1), bswap32(o2), bswap32(o3)},
-                                    (u32x4a16 *) (base + 16 * (uint64_t) k));
-    }
-    const uint32_t hend = 16 * klo < end ? 16 * klo : end;  // head bytes [a, hend)
-    uint32_t i = 0;
-    bool act = false;
-    if (lane < 16) {
-        i = a + lane;
-        act = i < hend;
-    } else if (lane < 32) {
-        i = 16 * khi + (lane - 16);  // tail bytes [max(16 khi, hend), end)
-        act = i < end && i >= hend;
-    }
-    if (act) base[i] = (uint8_t) (win_bits32(wd, x0 + 8 * i) >> 24);
-}
-
+// At least 6 waves per SIMD (80 VGPRs); LDS (two tiles' table values,
+// kFusePer ranges per wave, 2 KiB each, and the windows) sets the blocks
+// per CU.
 template <bool WHOLE>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_suffix(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
@@ -2440,15 +2412,83 @@ void k_decode_suffix(
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
     if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
-    __shared__ SfxSmem sm;
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_cnt[kFuseTile];
+    __shared__ P2dSmem sm;
+    // two tiles' characters: s_chr[b][wave][j][64 h + lane] = the 16
+    // characters at beg + 1,024 h + 16 lane of the wave's range j (beg: the
+    // range's start, S for the first)
+    __shared__ uint4 s_chr[2][kWavesPerBlock][kFusePer][128];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_cnt[2][kFuseTile];
     __shared__ uint32_t s_excl;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *bq = sm.bits[wv];
 
+    auto span = [&](uint32_t r, uint64_t &beg, uint64_t &re) {
+        const uint64_t rb = (uint64_t) r * R;
+        beg = rb > S ? rb : S;
+        re = rb + R < n ? rb + R : n;
+    };
+    auto lane_nin = [&](uint32_t r, uint64_t beg, uint64_t re, int h) -> uint32_t {
+        const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
+        return r >= nranges || p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+    };
+    // Count tile t into s_cnt[b] (this wave's ranges: every load issued
+    // before any is counted; the table values' bit 7s, two ranges per packed
+    // DPP reduction) and leave each character's table value in s_chr[b],
+    // where the decode reads it: the tile is read from HBM once and every
+    // character looked up once.
+    auto count = [&](uint32_t t, uint32_t b) {
+        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;
+        uint4 c[kFusePer][2];
+        uint32_t nin[kFusePer][2];
+#pragma unroll
+        for (uint32_t j = 0; j < kFusePer; j++) {
+            uint64_t beg, re;
+            span(rw + j, beg, re);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                nin[j][h] = lane_nin(rw + j, beg, re, h);
+                c[j][h] = nin[j][h] ? load_chars(in + beg + (uint64_t) h * kChunk + 16 * lane, nin[j][h])
+                                    : make_uint4(0, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kFusePer; j += 2) {
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < 2; e++) {
+                if (j + e >= kFusePer) break;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    uint32_t P[4];
+                    lane_values(sm.tab, c[j + e][h], nin[j + e][h], P);
+                    cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
+                            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
+                           << (16 * e);
+                    s_chr[b][wv][j + e][64 * h + lane] =
+                        kSfxVals ? make_uint4(P[0], P[1], P[2], P[3]) : c[j + e][h];
+                }
+            }
+            const uint32_t tot =
+                (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
+            if (lane == 0) {
+                s_cnt[b][wv * kFusePer + j] = tot & 0xFFFFu;
+                if (j + 1 < kFusePer) s_cnt[b][wv * kFusePer + j + 1] = tot >> 16;
+            }
+        }
+    };
+    // Publish tile t's count (s_cnt[b] complete): its status word and its
+    // group's sum.  Thread 0.
+    auto publish = [&](uint32_t t, uint32_t b) {
+        uint32_t agg = 0;
+        for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[b][i];
+        st_store(&w.fstatus[t], kStAgg | agg);
+        __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
     // The alphabet characters of the suffix before tile t.  Wave 0.
     auto prefix = [&](uint32_t t) -> uint32_t {
         const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
@@ -2468,164 +2508,59 @@ void k_decode_suffix(
         }
     };
 
+    __syncthreads();  // the tables
+    if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
+    __syncthreads();
+    uint32_t tA = s_tile[0], bA = 0;
+    if (tA < ntiles) count(tA, 0);
+    __syncthreads();
+    if (threadIdx.x == 0 && tA < ntiles) publish(tA, 0);
     bool owner = false;  // this block decoded the last tile
     uint32_t Vs = 0;     // then: the suffix's alphabet characters
-    __syncthreads();     // the tables
-    for (;;) {
-        if (threadIdx.x == 0) s_tile = atomicAdd(w.fticket, 1u);
-        __syncthreads();  // also: the last tile's s_cnt and s_excl are consumed
-        const uint32_t t = s_tile;
-        if (t >= ntiles) break;
-        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
-        // Range j's characters (this lane's 16 of each 1,024-character chunk).
-        auto load = [&](uint32_t j, uint4 c[2], uint32_t nin[2]) {
-            const uint32_t r = rw + j;
-            const uint64_t rb = (uint64_t) r * R;
-            const uint64_t beg = rb > S ? rb : S;
-            const uint64_t re = rb + R < n ? rb + R : n;
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
-                nin[h] = r >= nranges || p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                c[h] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
-            }
-        };
-        // Count first -- the table values' bit 7s, two ranges per packed DPP
-        // reduction -- and publish the tile's count at once, so the tiles
-        // after it find it published when they take their prefix (counted by
-        // the decode itself, every tile waited for its predecessors' whole
-        // decode: 1.9x slower).  Every range's characters are in flight at
-        // once; the decode below reads them again, from L2, a few
-        // microseconds later (round 3's count-ahead read them again a whole
-        // tile later, from HBM).  The 64 bytes after each range (its last
-        // group's look-ahead) come in with them.
-        uint32_t la[kFusePer];
-        {
-            uint4 c[kFusePer][2];
-            uint32_t nin[kFusePer][2];
-#pragma unroll
-            for (uint32_t j = 0; j < kFusePer; j++) {
-                load(j, c[j], nin[j]);
-                const uint64_t q = (uint64_t) (rw + j + 1) * R + lane;
-                la[j] = rw + j + 1 < nranges && q < n ? in[q] : 0u;
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < kFusePer; j += 2) {
-                uint32_t cnt = 0;
-#pragma unroll
-                for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        uint32_t P[4];
-                        lane_values(sm.tab, c[j + e][h], nin[j + e][h], P);
-                        cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
-                                __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
-                               << (16 * e);
-                    }
-                }
-                const uint32_t tot =
-                    (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
-                if (lane == 0) {
-                    s_cnt[wv * kFusePer + j] = tot & 0xFFFFu;
-                    s_cnt[wv * kFusePer + j + 1] = tot >> 16;
-                }
-            }
-        }
+    while (tA < ntiles) {
+        const uint32_t bB = bA ^ 1u;
+        if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
+        __syncthreads();  // also: s_chr[bB] and s_cnt[bB] of two tiles back are consumed
+        const uint32_t tB = s_tile[bB];
+        if (tB < ntiles) count(tB, bB);
         __syncthreads();
-        if (threadIdx.x == 0) {  // publish the tile's count: its status word, its group's sum
-            uint32_t agg = 0;
-            for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[i];
-            st_store(&w.fstatus[t], kStAgg | agg);
-            __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // then the decode of each range into its window (sextet 0 at kSfxP0)
-#pragma unroll
-        for (uint32_t j = 0; j < kFusePer; j++) {
-            uint4 *win = sm.win[wv][j];
-            win[lane] = make_uint4(0, 0, 0, 0);
-            if (lane + 64 < kSfxWin) win[lane + 64] = make_uint4(0, 0, 0, 0);
-        }
-        wave_lds_order();
-        uint32_t T[kFusePer];
-        {
-            uint4 c[2], cn[2];
-            uint32_t nin[2], nn[2];
-            load(0, c, nin);
-#pragma unroll
-            for (uint32_t j = 0; j < kFusePer; j++) {
-                if (j + 1 < kFusePer) load(j + 1, cn, nn);  // in flight during this decode
-                T[j] = rw + j < nranges
-                           ? bits_step<true>(sm, (uint32_t *) sm.win[wv][j], c, nin, (int) kSfxP0)
-                           : 0u;
-                c[0] = cn[0];
-                c[1] = cn[1];
-                nin[0] = nn[0];
-                nin[1] = nn[1];
-            }
-        }
+        if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
         if (wv == 0) {
-            const uint32_t ex = t ? prefix(t) : 0u;
+            const uint32_t ex = tA ? prefix(tA) : 0u;
             if (lane == 0) s_excl = ex;
         }
         __syncthreads();
         uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
-        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[i];
-        wave_lds_order();  // the windows, written by this wave's own ORs
+        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
+        const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
-            const uint64_t re = (uint64_t) r * R + R < n ? (uint64_t) r * R + R : n;
+            uint64_t beg, re;
+            span(r, beg, re);
             const bool last = r + 1 == nranges;
-            uint32_t *bits = (uint32_t *) sm.win[wv][j];
-            // the range owns the groups that start in it: its first `skip`
-            // sextets end the group the range before it started (which took
-            // them by look-ahead), and it takes the sextets that end its own
-            // last group from the characters after it
-            const int skip = (int) ((4u - (B & 3u)) & 3u);
-            int Tp = (int) T[j] - skip;
-            bool at_end = last;
-            if (!last && Tp > 0 && (Tp & 3)) {
-                for (uint64_t q = re;;) {
-                    const bool ok = q + lane < n;
-                    // the first 64 bytes came in with the count's loads
-                    const uint32_t tv = !ok ? 0xFFu : sm.tab[q == re ? la[j] : in[q + lane]];
-                    const bool v = tv < 64u;
-                    const uint64_t m = __ballot(v);
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                        (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                    const int need = 4 - (Tp & 3);
-                    if (v && (int) rank < need)  // after the sextets taken so far
-                        or_field<true>(bits, kSfxP0 + 6u * ((uint32_t) (Tp + skip) + rank),
-                                       tv << 18);
-                    const int got = __popcll(m);
-                    if (got >= need) {
-                        Tp += need;
-                        break;
-                    }
-                    Tp += got;
-                    q += 64;
-                    if (q >= n) {
-                        at_end = true;  // the stream's final, incomplete group
-                        break;
-                    }
-                }
-                wave_lds_order();
+            uint4 c[2];
+            uint32_t nin[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                c[h] = s_chr[bA][wv][j][64 * h + lane];
+                nin[h] = lane_nin(r, beg, re, h);
             }
-            if (Tp > 0) {
-                const uint32_t ng = (uint32_t) Tp >> 2, rem = (uint32_t) Tp & 3u;
-                // the final partial group: 2 sextets -> 1 byte, 3 -> 2
-                // (floor(6r/8), src/base64decoder.c:59-62,71-76)
-                const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
-                store_shifted(sm.win[wv][j], kSfxP0 + 6u * (uint32_t) skip, 3 * ng + tail,
-                              base_out + (B + 3) / 4 * 3);
-            }
-            B += T[j];
+            // the range after it, when it is in this tile, is in LDS
+            const uint32_t jn = wv * kFusePer + j + 1;
+            const uint8_t *la_lds =
+                jn < kFuseTile ? (const uint8_t *) s_chr[bA][jn / kFusePer][jn % kFusePer] : nullptr;
+            decode_range<kSfxVals>(sm, bq, in, n, beg, re, r == r0 ? 0 : range_skip(B),
+                                   base_out + (B + 3) / 4 * 3, c, nin, 0u, false, last, hold,
+                                   la_lds, true);
+            B += s_cnt[bA][wv * kFusePer + j];
         }
-        if (t == ntiles - 1) {
+        if (tA == ntiles - 1) {
             owner = true;
             Vs = s_excl;
-            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[i];
+            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[bA][i];
         }
+        tA = tB;
+        bA = bB;
     }
     // every prefix read of this block is over (relaxed: the loads have
     // returned -- their values decided the loop -- and a release at agent
@@ -2934,7 +2869,6 @@ struct RowModel {
     uint32_t rg;            // 1: the mapping applies
 };
 static_assert(sizeof(RowModel) == 96, "RowModel layout");
-static_assert(kFusePer % 2 == 0, "suffix counts are reduced two ranges at a time");
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the model, in the region pass 1
@@ -4730,7 +4664,8 @@ static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need)
     return 0;
 }
 
-// Offsets (and, for decode, the per-job counts) and the input on the device.
+// Offsets (and, for decode, the per-job counts) and the input on the device
+// (h_in NULL: the offsets only).
 static int lane_stage_in(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                          const uint64_t *h_in_off, const uint64_t *h_out_off, uint64_t words_extra)
 {
@@ -4745,23 +4680,92 @@ static int lane_stage_in(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
         (err = hip_err(hipMemcpyAsync(l->d_offs + words, h_out_off, words * 8,
                                       hipMemcpyHostToDevice, l->stream))))
         return err;
-    if (in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
-                                                  hipMemcpyHostToDevice, l->stream))))
+    if (h_in && in_bytes && (err = hip_err(hipMemcpyAsync(l->d_in, h_in, in_bytes,
+                                                          hipMemcpyHostToDevice, l->stream))))
         return err;
     return 0;
 }
 
+// Copy host bytes [sa, se) to device bytes from d on (any alignments):
+// aligned 16-byte loads of the host range (host memory is not cached: each
+// byte crosses the link once), byte stores (device memory; a few store
+// instructions per 16 bytes -- the link, not the stores, bounds this).
+// Block-wide.
+DEV void copy_from_host(const uint8_t *sa, const uint8_t *se, uint8_t *d)
+{
+    const uintptr_t u0 = (uintptr_t) sa & ~(uintptr_t) 15;
+    uint8_t *dd = d - (uintptr_t) sa;  // dd[(uintptr_t) p]: the device byte of host p
+    for (uintptr_t u = u0 + 16 * threadIdx.x; u < (uintptr_t) se; u += 16 * kThreads) {
+        const uint4 v = *(const uint4 *) u;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uintptr_t p = u + k;
+            if (p >= (uintptr_t) sa && p < (uintptr_t) se) dd[p] = (uint8_t) (w[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
+// A batch with lent segments into the device: block b covers device bytes
+// [b T, (b+1) T) of the batch, finds the first segment ending past its
+// start by a binary search, and copies its bytes from the segments' sources
+// or, between segments, from the arena h_in -- all read straight from
+// pinned host memory.
+constexpr uint32_t kGatherTile = 64u << 10;
+__global__ __launch_bounds__(kThreads) void k_gather_host(
+    uint8_t *__restrict__ d_in, const uint8_t *__restrict__ h_in, uint64_t total,
+    const b64x_seg *__restrict__ seg, uint32_t nseg)
+{
+    __shared__ uint32_t s_i0;
+    const uint64_t lo = (uint64_t) blockIdx.x * kGatherTile;
+    const uint64_t hi = lo + kGatherTile < total ? lo + kGatherTile : total;
+    if (threadIdx.x == 0) {  // the first segment ending past lo (nseg if none)
+        uint32_t a = 0, b = nseg;
+        while (a < b) {
+            const uint32_t m = (a + b) / 2;
+            if (seg[m].off + seg[m].len > lo) b = m;
+            else a = m + 1;
+        }
+        s_i0 = a;
+    }
+    __syncthreads();
+    uint64_t p = lo;
+    for (uint32_t i = s_i0; p < hi; i++) {
+        const uint64_t so = i < nseg ? seg[i].off : hi, se = i < nseg ? seg[i].off + seg[i].len : hi;
+        const uint64_t gap_end = so < hi ? so : hi;  // arena bytes before the segment
+        if (p < gap_end) {
+            copy_from_host(h_in + p, h_in + gap_end, d_in + p);
+            p = gap_end;
+        }
+        if (p >= hi) break;
+        const uint64_t e = se < hi ? se : hi;
+        copy_from_host(seg[i].src + (p - so), seg[i].src + (e - so), d_in + p);
+        p = e;
+    }
+}
+
 int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
-                           const uint64_t *h_out_off, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg)
+                           const uint64_t *h_out_off, const b64x_seg *h_seg, uint32_t nseg,
+                           const b64x_alphabet *abc, b64x_done_fn done, void *arg)
 {
-    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off))) return -EINVAL;
+    if (!l || (njobs && (!h_in || !h_in_off || !h_out || !h_out_off)) || (nseg && !h_seg))
+        return -EINVAL;
     int err;
     if ((err = hip_err(hipSetDevice(l->device)))) return err;
     if (njobs) {
         const uint64_t words = (uint64_t) njobs + 1;
-        if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, 0))) return err;
+        const uint64_t in_bytes = h_in_off[njobs];
+        for (uint32_t i = 0; i < nseg; i++)  // sorted, inside the batch
+            if (h_seg[i].off + h_seg[i].len > in_bytes || (i && h_seg[i].off < h_seg[i - 1].off + h_seg[i - 1].len))
+                return -EINVAL;
+        if ((err = lane_stage_in(l, nseg ? nullptr : h_in, njobs, h_in_off, h_out_off, 0)))
+            return err;
+        if (nseg && in_bytes) {
+            hipLaunchKernelGGL(k_gather_host, dim3((uint32_t) ((in_bytes + kGatherTile - 1) / kGatherTile)),
+                               dim3(kThreads), 0, l->stream, l->d_in, h_in, in_bytes, h_seg, nseg);
+            if ((err = launch_status())) return err;
+        }
         if ((err = b64x_encode_batch(l->d_in, l->d_offs, njobs, h_out, l->d_offs + words, abc,
                                      l->stream)))
             return err;
@@ -5031,7 +5035,7 @@ const char *b64x_build_info(void)
 #define B64X_STR(x) B64X_STR2(x)
     return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
            "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
-           "(count first, decode into LDS windows, shifted stores); rows:line model in row "
+           "(tiles read once into LDS, counted a tile ahead); rows:line model in row "
            "bands; lanes:chained decoder blocks";
 }
 

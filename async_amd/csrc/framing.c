@@ -15,10 +15,12 @@
 #include <errno.h>
 #include <limits.h>
 #include <stdbool.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "b64_lend.h"
+#include "b64_pin.h"
 #include "blobstream.h"
 #include "chunkencoder.h"
 #include "fsalloc.h"
@@ -30,6 +32,8 @@ static void *xmalloc(size_t size)
 }
 
 /* ================================================================ queue */
+
+static const struct bytestream_1_vt queue_vt;
 
 typedef struct qnode {
     bytestream_1 stream;
@@ -118,15 +122,18 @@ void queuestream_push(queuestream_t *q, bytestream_1 s)
     queue_adopt(q, s, true);
 }
 
+/* The copy (ref src/queuestream.c:117-131) goes into pinned memory
+ * (streams.c b64_pinned_blobstream), so that a GPU encoder stage reading
+ * this queue can take the bytes from there (b64_src_peek). */
 void queuestream_enqueue_bytes(queuestream_t *q, const void *blob, size_t count)
 {
-    queue_adopt(q, blobstream_as_bytestream_1(copy_blobstream(q->async, blob, count)),
+    queue_adopt(q, blobstream_as_bytestream_1(b64_pinned_blobstream(q->async, blob, count)),
                 false);
 }
 
 void queuestream_push_bytes(queuestream_t *q, const void *blob, size_t count)
 {
-    queue_adopt(q, blobstream_as_bytestream_1(copy_blobstream(q->async, blob, count)),
+    queue_adopt(q, blobstream_as_bytestream_1(b64_pinned_blobstream(q->async, blob, count)),
                 true);
 }
 
@@ -187,6 +194,48 @@ ssize_t queuestream_read(queuestream_t *q, void *buf, size_t count)
     q->callback_owed = true;
     errno = EAGAIN;
     return -1;
+}
+
+bool b64_src_peek(bytestream_1 s, const uint8_t **p, size_t *n, b64_pin_slab **slab)
+{
+    if (s.vt != &queue_vt)
+        return false;
+    queuestream_t *q = s.obj;
+    if (q->deferred_errno)
+        return false;
+    while (q->first) {
+        if (!b64_blob_lend_peek(q->first->stream, p, n, slab) || !*slab)
+            return false;
+        if (*n)
+            break;
+        queue_drop_first(q); /* as queuestream_read() would */
+    }
+    return q->first != NULL;
+}
+
+void b64_src_take(bytestream_1 s, size_t n)
+{
+    queuestream_t *q = s.obj;
+    b64_blob_lend_take(q->first->stream, n);
+}
+
+size_t b64_src_plain(bytestream_1 s, size_t lend_min, size_t limit)
+{
+    if (s.vt != &queue_vt)
+        return limit;
+    queuestream_t *q = s.obj;
+    size_t plain = 0;
+    for (qnode *e = q->first; e && plain < limit; e = e->next) {
+        const uint8_t *p;
+        size_t n;
+        b64_pin_slab *slab;
+        if (!b64_blob_lend_peek(e->stream, &p, &n, &slab))
+            return limit; /* another kind of stream: no telling */
+        if (slab && n >= lend_min)
+            return plain;
+        plain += n;
+    }
+    return plain < limit ? limit : plain;
 }
 
 void queuestream_close(queuestream_t *q)

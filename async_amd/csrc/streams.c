@@ -13,9 +13,12 @@
  * valid memory and a counting allocator sees every object go.
  */
 #include <errno.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include "b64_lend.h"
+#include "b64_pin.h"
 #include "blobstream.h"
 #include "bytestream_1.h"
 #include "fsalloc.h"
@@ -60,6 +63,7 @@ struct blobstream {
     const uint8_t *data;
     size_t size, pos;
     void *owned;
+    b64_pin_slab *slab; /* data is a pinned piece of this slab (b64_pin.h) */
     action_1 on_close;
 };
 
@@ -110,11 +114,30 @@ ssize_t blobstream_read(blobstream_t *b, void *buf, size_t count)
     return (ssize_t) n;
 }
 
+/* copy_blobstream() into pinned memory the GPU can read (b64_pin.h), so
+ * that an encoder stage can take the bytes without copying them; an
+ * ordinary copy when the pool is off or has no room. */
+blobstream_t *b64_pinned_blobstream(async_t *async, const void *blob, size_t count)
+{
+    b64_pin_slab *slab = NULL;
+    uint8_t *copy = count ? b64_pin_alloc(count, &slab) : NULL;
+    if (!copy)
+        return copy_blobstream(async, blob, count);
+    memcpy(copy, blob, count);
+    blobstream_t *b = new_blob(async, copy, count, NULL, NULL_ACTION_1);
+    b->slab = slab;
+    return b;
+}
+
 void blobstream_close(blobstream_t *b)
 {
     action_1_perf(b->on_close);
     fsfree(b->owned);
     b->owned = NULL;
+    if (b->slab) {
+        b64_pin_unref(b->slab);
+        b->slab = NULL;
+    }
     async_wound(b->async, b);
     b->async = NULL;
 }
@@ -155,6 +178,25 @@ bytestream_1 blobstream_as_bytestream_1(blobstream_t *b)
 {
     return (bytestream_1) { b, &blob_vt };
 }
+
+/* b64_lend.h, upstream side: a pinned blob's unread bytes. */
+bool b64_blob_lend_peek(bytestream_1 s, const uint8_t **p, size_t *n, b64_pin_slab **slab)
+{
+    if (s.vt != &blob_vt)
+        return false;
+    blobstream_t *b = s.obj;
+    *p = b->data + b->pos;
+    *n = b->size - b->pos;
+    *slab = b->slab;
+    return true;
+}
+
+void b64_blob_lend_take(bytestream_1 s, size_t n)
+{
+    blobstream_t *b = s.obj;
+    b->pos += n;
+}
+
 
 /* ---- nicestream ------------------------------------------------------- */
 

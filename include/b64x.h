@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define B64X_ABI_VERSION 3
+#define B64X_ABI_VERSION 4
 
 /* Alphabet descriptor.  (char) -1 selects the reference's defaults,
  * exactly like base64_encode()/base64_decode() (ref
@@ -262,11 +262,22 @@ void b64x_lane_release(b64x_lane *l);
  * starting at 0).  All four host buffers must be pinned (b64x_host_alloc)
  * and stay untouched until `done(arg)` has run.  Asynchronous; the lane's
  * device buffers are grown (synchronously) when a batch needs more.  One
- * batch in flight per lane. */
+ * batch in flight per lane.
+ *
+ * h_seg[0 .. nseg) (pinned; nseg may be 0): parts of the batch's input
+ * that are not in h_in but elsewhere in pinned host memory -- the input's
+ * bytes [off, off+len) are at src (h_in's bytes there are not read) --
+ * sorted by off, not overlapping.  A batch with segments is gathered into
+ * the device by one kernel that reads h_in and the segments straight from
+ * host memory (no DMA of h_in). */
+typedef struct {
+    uint64_t off, len;
+    const uint8_t *src;
+} b64x_seg;
 int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
-                           const uint64_t *h_out_off, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg);
+                           const uint64_t *h_out_off, const b64x_seg *h_seg, uint32_t nseg,
+                           const b64x_alphabet *abc, b64x_done_fn done, void *arg);
 /* The encode batch whose `done` has run really finished: its completion
  * stamp (written by a kernel queued behind the encode) is there; if not,
  * counted (b64x_diag_counters), waited for and checked again.  0 or -EIO. */

@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 from async_amd import _lib  # noqa: E402
 
 if len(sys.argv) > 1:
-    _lib.LIB_PATH = os.path.abspath(sys.argv[1])
+    lib = sys.argv[1]
+    _lib.LIB_PATH = lib if os.path.isabs(lib) else os.path.join(ROOT, lib)
 from async_amd import b64  # noqa: E402
 
 sys.path.insert(0, os.path.join(ROOT, "scripts"))

@@ -11,12 +11,11 @@ OUT="$ROOT/gpurun_out/pmc_$TAG"
 mkdir -p "$OUT"
 SCRIPT="$ROOT/$1"; shift
 cd /tmp && export TMPDIR=/tmp
+# PMC_SETS="FETCH_SIZE;SQ_INSTS_VALU SQ_WAVES" runs only those sets
+SETS=${PMC_SETS:-"SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_SALU;SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SMEM;SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC;FETCH_SIZE;WRITE_SIZE"}
 i=0
-for set in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_SALU" \
-           "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SMEM" \
-           "SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC" \
-           "FETCH_SIZE" "WRITE_SIZE"; do
+IFS=';' read -ra SETLIST <<< "$SETS"
+for set in "${SETLIST[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$OUT/p$i" -o run \
       -- python3 "$SCRIPT" "$@" > "$OUT/p$i.log" 2>&1

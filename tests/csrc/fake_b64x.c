@@ -72,7 +72,31 @@ struct fjob {
     uint64_t stamp;
     b64x_done_fn done;
     void *arg;
+    /* lane encode batches run when a worker takes them (reading their
+     * inputs then, as the device would): */
+    const uint8_t *enc_in;
+    uint64_t *enc_in_off, *enc_out_off; /* copies */
+    b64x_seg *enc_seg;                  /* copy, or NULL */
+    uint32_t enc_jobs, enc_nseg;
+    b64x_alphabet enc_abc;
 };
+
+/* The device copy of the batch: the arena with the lent segments laid
+ * over it (read now, as the gather kernel would when the batch runs). */
+static void run_encode(fjob *j)
+{
+    const uint64_t total = j->enc_in_off[j->enc_jobs];
+    uint8_t *dev = malloc(total + 1);
+    memcpy(dev, j->enc_in, total);
+    for (uint32_t i = 0; i < j->enc_nseg; i++)
+        memcpy(dev + j->enc_seg[i].off, j->enc_seg[i].src, j->enc_seg[i].len);
+    for (uint32_t k = 0; k < j->enc_jobs; k++) {
+        size_t n = j->enc_in_off[k + 1] - j->enc_in_off[k];
+        (void) orc_encode(dev + j->enc_in_off[k], n, j->enc_abc.pos62, j->enc_abc.pos63,
+                          j->enc_abc.pad, j->enc_abc.padchar, j->out_src + j->enc_out_off[k]);
+    }
+    free(dev);
+}
 
 static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t cv = PTHREAD_COND_INITIALIZER;
@@ -148,6 +172,9 @@ static void publish(fjob *j)
 
 static void job_free(fjob *j)
 {
+    free(j->enc_in_off);
+    free(j->enc_out_off);
+    free(j->enc_seg);
     free(j->out_src);
     free(j->recs);
     free(j->spells);
@@ -203,6 +230,8 @@ static void *worker(void *unused)
         pthread_mutex_unlock(&mu);
         for (volatile unsigned i = 0; i < spin * 100; i++)
             ;
+        if (j->enc_jobs)
+            run_encode(j);
         if (early) {
             atomic_fetch_add(&n_early, 1);
             j->called = true;
@@ -555,17 +584,30 @@ int b64x_lane_wait(b64x_lane *l)
 
 int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
                            const uint64_t *h_in_off, uint8_t *h_out,
-                           const uint64_t *h_out_off, const b64x_alphabet *abc,
-                           b64x_done_fn done, void *arg)
+                           const uint64_t *h_out_off, const b64x_seg *h_seg, uint32_t nseg,
+                           const b64x_alphabet *abc, b64x_done_fn done, void *arg)
 {
     fjob *j = calloc(1, sizeof *j);
     j->owner = l;
     size_t total = njobs ? h_out_off[njobs] : 0;
     j->out_src = malloc(total + 16);
-    for (uint32_t k = 0; k < njobs; k++) {
-        size_t n = h_in_off[k + 1] - h_in_off[k];
-        (void) orc_encode(h_in + h_in_off[k], n, abc->pos62, abc->pos63, abc->pad,
-                          abc->padchar, j->out_src + h_out_off[k]);
+    if (njobs) {
+        j->enc_in = h_in;
+        j->enc_jobs = njobs;
+        j->enc_abc = *abc;
+        j->enc_in_off = malloc((njobs + 1) * sizeof *j->enc_in_off);
+        j->enc_out_off = malloc((njobs + 1) * sizeof *j->enc_out_off);
+        memcpy(j->enc_in_off, h_in_off, (njobs + 1) * sizeof *h_in_off);
+        memcpy(j->enc_out_off, h_out_off, (njobs + 1) * sizeof *h_out_off);
+        for (uint32_t i = 0; i < nseg; i++)
+            if (h_seg[i].off + h_seg[i].len > h_in_off[njobs] ||
+                (i && h_seg[i].off < h_seg[i - 1].off + h_seg[i - 1].len))
+                abort(); /* the hub's segments are sorted, inside the batch */
+        if (nseg) {
+            j->enc_seg = malloc(nseg * sizeof *j->enc_seg);
+            memcpy(j->enc_seg, h_seg, nseg * sizeof *h_seg);
+            j->enc_nseg = nseg;
+        }
     }
     j->out_dst = h_out;
     j->out_n = total;

@@ -177,6 +177,33 @@ typedef struct {
     size_t *live;    /* optional: consumers still running; quit at 0 */
 } consumer;
 
+/* ASYNC_B64_HUB_TRACE=1: the consumers' read time on this thread (the
+ * reads include what they trigger: upstream gathers, launches, framing,
+ * the copy out), for the config-5 phase breakdown (scripts/cfg5_profile.py). */
+static double now_s(void);
+static __thread double tl_read_s;
+static __thread unsigned long tl_reads;
+
+static int read_tracing(void)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("ASYNC_B64_HUB_TRACE");
+        on = e && *e && *e != '0';
+    }
+    return on;
+}
+
+double h_take_read_seconds(unsigned long *reads)
+{
+    double s = tl_read_s;
+    if (reads)
+        *reads = tl_reads;
+    tl_read_s = 0;
+    tl_reads = 0;
+    return s;
+}
+
 static void consumer_finish(consumer *c)
 {
     c->done = 1;
@@ -200,7 +227,12 @@ static void consume(consumer *c)
             abort();
         buf = scratch;
     }
+    double t0 = read_tracing() ? now_s() : 0;
     ssize_t n = bytestream_1_read(c->material, buf, c->read_size);
+    if (t0) {
+        tl_read_s += now_s() - t0;
+        tl_reads++;
+    }
     c->reads++;
     if (n < 0) {
         free(scratch);
@@ -498,6 +530,49 @@ int h_egress_stacks(const uint8_t *in, const uint64_t *in_off, size_t nmsg,
     if (err_out)
         *err_out = err;
     return err ? -1 : 0;
+}
+
+/* One egress stack over a queue of `npieces` messages copied in by
+ * queuestream_enqueue_bytes() (or _push_bytes() in reverse order when
+ * `push`: the same queue) -> base64_encode (GPU stage) -> chunk_encode.  With
+ * `late`, the queue is terminated only after the first read has answered
+ * EAGAIN (a timer, 2 ms), else at once.  Large messages are lent to the
+ * encoder from their pinned copies (b64_pin.h); the framed stream equals
+ * the oracle's for the concatenation whatever the mix. */
+ssize_t h_egress_pieces(const uint8_t *in, const size_t *lens, size_t npieces, int push,
+                        int late, size_t max_chunk, size_t read_size, uint8_t *out, size_t cap,
+                        int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    queuestream_t *q = make_queuestream(async);
+    size_t off = 0;
+    const uint8_t **starts = malloc((npieces ? npieces : 1) * sizeof *starts);
+    for (size_t i = 0; i < npieces; i++) {
+        starts[i] = in + off;
+        off += lens[i];
+    }
+    for (size_t k = 0; k < npieces; k++) {
+        size_t i = push ? npieces - 1 - k : k;
+        if (push)
+            queuestream_push_bytes(q, starts[i], lens[i]);
+        else
+            queuestream_enqueue_bytes(q, starts[i], lens[i]);
+    }
+    free(starts);
+    late_terminate *t = calloc(1, sizeof *t);
+    t->q = q;
+    if (late)
+        async_timer_start(async, async_now(async) + 2000000, /* 2 ms */
+                          (action_1) { t, (act_1) do_terminate });
+    else
+        queuestream_terminate(q);
+    base64encoder_t *e = base64_encode(async, queuestream_as_bytestream_1(q), -1, -1, true, -1);
+    chunkencoder_t *ch = chunk_encode(async, base64encoder_as_bytestream_1(e), max_chunk);
+    ssize_t r = run(async, chunkencoder_as_bytestream_1(ch), read_size, out, cap, err_out, NULL);
+    free(t);
+    return r;
 }
 
 /* The ingress mirror of config 5: `nmsg` decoder stacks

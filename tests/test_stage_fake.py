@@ -298,3 +298,68 @@ def test_egress_and_ingress_stacks_leak_check():
     (got, err), left = util.counted(util.ingress_stacks, msgs, 4096, lib=L)
     assert err == 0 and left == 0
     assert bad_streams(msgs, got) == []
+
+
+# ---- messages lent from their pinned queue copies (b64_pin.h) ------------
+
+LENT_SIZES = [1, 2, 3, 5000, 4095, 4096, 4097, 100001, 7, 65537, 300000, 12, 9000]
+
+
+@pytest.mark.parametrize("cap", ["1024", "65536", None])
+@pytest.mark.parametrize("lend_min", ["1", "4096", "1000000000"])
+@pytest.mark.parametrize("push,late", [(False, False), (True, False), (False, True)])
+def test_egress_lent_pieces(monkeypatch, cap, lend_min, push, late):
+    """queuestream_enqueue_bytes / _push_bytes of a mix of short and long
+    messages -> encoder -> chunkencoder: long messages are encoded from
+    their pinned copies (no copy into the arena; carries across blocks of
+    one message come from the bytes right before the next block), short
+    ones gathered.  The framed stream equals the oracle stack's (late
+    termination: the payload, since EAGAIN then shapes the read counts),
+    lent jobs happen exactly when a message reaches ASYNC_B64_LEND_MIN, and
+    every pinned piece is released once the stack is closed."""
+    L = fake()
+    L.fake_configure(13, 0, 0)
+    if cap:
+        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", cap)
+    monkeypatch.setenv("ASYNC_B64_LEND_MIN", lend_min)
+    rng = np.random.default_rng(0x1E47)
+    pieces = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in LENT_SIZES]
+    order = pieces  # push_bytes in reverse order queues them in order
+    lent0 = L.b64_hub_lent_total()
+    for max_chunk, read_size in ((4096, 1000), (1 << 20, 10240)):
+        got, err = util.egress_pieces(pieces, max_chunk, read_size, push=push, late=late, lib=L)
+        assert err == 0 and got is not None
+        data = b"".join(order)
+        if late:
+            assert util.dechunk(got) == orc.encode(data)
+        else:
+            want = orc.chunked_encode(np.frombuffer(data, np.uint8),
+                                      piece_lens=[len(p) for p in order],
+                                      max_chunk=max_chunk, read_size=read_size)
+            assert got == want
+    lent = L.b64_hub_lent_total() - lent0
+    if int(lend_min) > max(LENT_SIZES):
+        assert lent == 0
+    else:
+        assert lent > 0
+    assert L.b64_pin_live_refs() == 0
+
+
+def test_egress_stacks_lent_and_released():
+    """Config 5's shape on the fake device: every message at least
+    ASYNC_B64_LEND_MIN long is lent, and no pinned piece outlives its stack."""
+    L = fake()
+    L.fake_configure(21, 0, 0)
+    lens = [int(x) for x in util.zipf_lengths(200, seed=0x77, rmax=256)]
+    payload = util.splitmix64(0x5EED, sum(lens))
+    lent0 = L.b64_hub_lent_total()
+    got, err = util.egress_stacks(payload, lens, 1 << 20, 10240, lib=L)
+    assert err == 0
+    off = 0
+    for i, n in enumerate(lens):
+        want = orc.chunked_encode(payload[off:off + n].tobytes(), max_chunk=1 << 20,
+                                  read_size=10240)
+        off += n
+        assert got[i] == want, i
+    assert L.b64_hub_lent_total() - lent0 >= sum(1 for n in lens if n >= 4096)
+    assert L.b64_pin_live_refs() == 0

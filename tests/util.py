@@ -131,6 +131,14 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_prof_stop.argtypes = [ctypes.c_char_p]
     L.h_device_count.argtypes = []
     L.h_device_count.restype = ctypes.c_int
+    L.h_egress_pieces.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_int, sz, sz, vp, sz, ip]
+    L.h_egress_pieces.restype = ssz
+    L.b64_pin_live_refs.argtypes = []
+    L.b64_pin_live_refs.restype = ctypes.c_long
+    L.b64_hub_lent_total.argtypes = []
+    L.b64_hub_lent_total.restype = ctypes.c_ulong
+    L.h_take_read_seconds.argtypes = [ctypes.POINTER(ctypes.c_ulong)]
+    L.h_take_read_seconds.restype = ctypes.c_double
     dp = ctypes.POINTER(ctypes.c_double)
     L.h_fd_decode.argtypes = [vp, sz, sz, sz, ch, ch, vp, sz, ctypes.c_int, ip, dp]
     L.h_fd_decode.restype = ssz
@@ -362,6 +370,22 @@ def fd_encode(data, pieces=None, max_chunk=1 << 20, pos62=-1, pos63=-1, pad=True
                                          out.ctypes.data, out.size, int(bool(sock)),
                                          ctypes.byref(err), t)
     return (None if n < 0 else out[:n]), err.value, t[0]
+
+
+def egress_pieces(pieces, max_chunk: int, read_size: int, push=False, late=False, lib=None):
+    """queuestream_enqueue_bytes (or _push_bytes) of every piece ->
+    base64_encode -> chunk_encode(max_chunk), drained read_size at a time:
+    (framed bytes, errno)."""
+    data = b"".join(pieces)
+    src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    lens = np.array([len(p) for p in pieces] or [0], dtype=np.uint64)
+    cap = framed_cap(len(data), max_chunk) + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    err = ctypes.c_int(0)
+    n = _lib_or_default(lib).h_egress_pieces(src.ctypes.data, lens.ctypes.data, len(pieces),
+                                             int(push), int(late), max_chunk, read_size,
+                                             out.ctypes.data, cap, ctypes.byref(err))
+    return (out[:n].tobytes() if n >= 0 else None), err.value
 
 
 def dechunk(framed: bytes) -> bytes:
