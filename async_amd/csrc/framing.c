@@ -232,10 +232,10 @@ size_t b64_src_plain(bytestream_1 s, size_t lend_min, size_t limit)
         if (!b64_blob_lend_peek(e->stream, &p, &n, &slab))
             return limit; /* another kind of stream: no telling */
         if (slab && n >= lend_min)
-            return plain;
+            return plain < limit ? plain : limit;
         plain += n;
     }
-    return plain < limit ? limit : plain;
+    return limit;
 }
 
 void queuestream_close(queuestream_t *q)

@@ -43,6 +43,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -364,14 +365,32 @@ int b64x_device_check(void)
     return 0;
 }
 
+/* Pinned buffers stand-in: the allocation ends (64-byte aligned) right
+ * before an inaccessible page, so that a write past a buffer's end faults
+ * here as it does against the real pinned mappings (calloc'd buffers let
+ * an arena overrun go unnoticed). */
 void *b64x_host_alloc(uint64_t bytes)
 {
-    return calloc(1, bytes ? bytes : 1);
+    const size_t pg = 4096, need = ((bytes ? bytes : 1) + 63) / 64 * 64;
+    const size_t data = (need + 16 + pg - 1) / pg * pg, total = data + pg;
+    uint8_t *base = mmap(NULL, total, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (base == MAP_FAILED)
+        return NULL;
+    if (mprotect(base + data, pg, PROT_NONE) != 0) {
+        munmap(base, total);
+        return NULL;
+    }
+    uint8_t *p = base + data - need;
+    ((size_t *) p)[-2] = (size_t) base;
+    ((size_t *) p)[-1] = total;
+    return p;
 }
 
 void b64x_host_free(void *p)
 {
-    free(p);
+    if (!p)
+        return;
+    munmap((void *) ((size_t *) p)[-2], ((size_t *) p)[-1]);
 }
 
 void b64x_diag_counters(uint64_t out[2])

@@ -969,6 +969,54 @@ ssize_t h_fd_encode(const uint8_t *in, const size_t *lens, size_t npieces, size_
     return err ? -1 : (ssize_t) rd.got;
 }
 
+/* ---- a crash report: the faulting thread's native stack ------------------
+ * (Python's faulthandler shows Python frames only.)  Printed to stderr,
+ * then the previous handler runs. */
+#include <execinfo.h>
+#include <signal.h>
+
+static struct sigaction prev_segv;
+
+static void segv_report(int sig, siginfo_t *si, void *uc)
+{
+    void *frames[64];
+    int n = backtrace(frames, 64);
+    static const char msg[] = "\nstage_harness: native stack of the faulting thread:\n";
+    ssize_t w = write(2, msg, sizeof msg - 1);
+    char line[96];
+    int len = snprintf(line, sizeof line, "fault address %p, frames %d\n", si->si_addr, n);
+    w = write(2, line, (size_t) len);
+    (void) w;
+    backtrace_symbols_fd(frames, n, 2);
+    sigaction(SIGSEGV, &prev_segv, NULL);
+    if (prev_segv.sa_flags & SA_SIGINFO) {
+        if (prev_segv.sa_sigaction)
+            prev_segv.sa_sigaction(sig, si, uc);
+    } else if (prev_segv.sa_handler != SIG_DFL && prev_segv.sa_handler != SIG_IGN) {
+        prev_segv.sa_handler(sig);
+    }
+    raise(sig);
+}
+
+void h_segv_install(void);
+__attribute__((constructor)) void h_segv_install(void)
+{
+    /* an alternate stack (this thread's): a stack overflow still reports */
+    static char altstack[1 << 16];
+    stack_t ss = { .ss_sp = altstack, .ss_size = sizeof altstack, .ss_flags = 0 };
+    sigaltstack(&ss, NULL);
+    struct sigaction cur;
+    sigaction(SIGSEGV, NULL, &cur);
+    if ((cur.sa_flags & SA_SIGINFO) && cur.sa_sigaction == segv_report)
+        return; /* ours already */
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_report;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &prev_segv);
+}
+
 /* ---- a small sampling profiler (SIGPROF, process CPU time) ---------------
  * h_prof_start(hz) / h_prof_stop(path): a histogram of interrupted program
  * counters, resolved with dladdr to "object symbol+offset", written as

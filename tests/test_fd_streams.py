@@ -78,6 +78,22 @@ def test_fd_encode_fake(fake, max_chunk, sock):
     assert util.dechunk(got.tobytes()) == orc.encode(data)
 
 
+@pytest.mark.parametrize("max_chunk", [4096, 1 << 20])
+def test_fd_encode_fake_elements_past_the_arena_room(fake, max_chunk):
+    """Queue elements far longer than a block's arena room (the GPU test's
+    shapes): a block gathered by reading never takes more than its room
+    (the fake's host buffers end at an inaccessible page, as pinned
+    mappings do, so an overrun faults here)."""
+    fake.fake_configure(7, 0, 0)
+    rng = np.random.default_rng(23)
+    data = rng.integers(0, 256, (16 << 20) + 1, dtype=np.uint8).tobytes()
+    pieces = [1 << 20, 5, (15 << 20) - 4]
+    got, err, _ = util.fd_encode(data, pieces, max_chunk=max_chunk, lib=fake)
+    assert err == 0 and got is not None
+    assert got.tobytes() == orc.chunked_encode(data, pieces, max_chunk=max_chunk,
+                                               read_size=10240)
+
+
 def test_fd_encode_empty(fake):
     got, err, _ = util.fd_encode(b"", lib=fake)
     assert err == 0 and got.tobytes() == orc.chunked_encode(b"", max_chunk=1 << 20,
