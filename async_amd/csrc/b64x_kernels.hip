@@ -891,12 +891,11 @@ struct DecodeWs {
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
-// Ranges per wave of a single-pass decode tile (k_decode_suffix): a block
-// holds two tiles' characters in LDS, 2 KiB per range.
-#ifndef B64X_FUSE_PER  // A/B builds only
-#define B64X_FUSE_PER 2
-#endif
-constexpr uint32_t kFusePer = B64X_FUSE_PER;
+// Ranges per wave of a single-pass decode tile (k_decode_suffix): 8 (16
+// was 841 us, 8 766 us on 1 GiB at junk density 0.05, profiles/r03_ab_sfx_*;
+// 4 and 2: r04_g/r04_h, slower).
+constexpr uint32_t kFusePer = 8;
+constexpr uint32_t kFuseLoad = 4;  // of them loaded at once for counting
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsStatus = 64;                                        // scan tile status
@@ -1351,6 +1350,30 @@ DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
 }
 
 
+DEV uint32_t lane_valid_count(const uint32_t P[4])
+{
+    return 16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
+           __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
+}
+
+// One wave copies 64 x 16 bytes from gsrc (per lane) to LDS at lds_dst +
+// 16 x lane, straight into LDS (global_load_lds_dwordx4: no VGPR holds the
+// data).  Issued as inline asm so that the compiler does not track the copy:
+// it cannot tell the copy's destination from the decode's other LDS traffic
+// (the window's atomic ORs go through a pointer) and waited for every copy
+// in flight (vmcnt(0)) at the first of them, right after the copy was
+// issued.  The reader waits itself (vm_wait_all) before it reads the copy.
+DEV void lds_dma16(const void *gsrc, void *lds_dst)
+{
+    const uint32_t l = (uint32_t) (uintptr_t) (__attribute__((address_space(3))) void *) lds_dst;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
+}
+
+DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ---- pass 2, bit-stream form ----------------------------------------------
 //
 // The range's output is built in LDS directly as the decoded BIT stream (a
@@ -1499,9 +1522,7 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
 // sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
 // up to 18 bits past the window's byte 4: skipped sextets land in its
 // head).  Returns the step's alphabet characters.
-// VALS: c[] already holds the table values (lane_values, beyond-end bytes
-// marked), as k_decode_suffix's count leaves them in LDS.
-template <bool BE = false, class SM = P2dSmem, bool VALS = false>
+template <bool BE = false, class SM = P2dSmem>
 DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
@@ -1512,14 +1533,7 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
     uint32_t P[2][4], sel[2][4], six[2][4], cnt = 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        if (VALS) {
-            P[h][0] = c[h].x;
-            P[h][1] = c[h].y;
-            P[h][2] = c[h].z;
-            P[h][3] = c[h].w;
-        } else {
-            lane_values(sm.tab, c[h], nin[h], P[h]);
-        }
+        lane_values(sm.tab, c[h], nin[h], P[h]);
         uint32_t nb6 = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -2116,8 +2130,6 @@ void k_decode_lines(
 // flushed between steps and its partial dword carried to the front (as
 // decode_buf_bits does); the bytes flushed early are final and never reach
 // the next range's output.
-// VALS: c[] and la_lds hold table values (k_decode_suffix), not characters.
-template <bool VALS = false>
 DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ in, uint64_t n,
                       uint64_t start, uint64_t re, int T0, uint8_t *ob, const uint4 c[2],
                       const uint32_t nin[2], uint32_t la, bool la_ok, bool last, uint32_t hold,
@@ -2139,7 +2151,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     // the first step from the chunks given (its own code: joined with the
     // loads of the later steps, the compiler waited for every load in
     // flight before the step, ranges read ahead included)
-    T += (int) bits_step<true, P2dSmem, VALS>(sm, bits, c, nin, pb0 + 6 * T);
+    T += (int) bits_step<true>(sm, bits, c, nin, pb0 + 6 * T);
     for (uint64_t pos = start + 2 * kChunk; pos < re; pos += 2 * kChunk) {
         // more of this range: flush the window's whole blocks and carry the
         // partial one to the front
@@ -2172,17 +2184,20 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     bool at_end = last;
     if (!last && T > 0 && (T & 3)) {
         // complete the range's last group from the characters after it:
-        // given (la, la_ok), in LDS at la_lds (the next range's first
-        // characters, k_decode_suffix), or read from `in` only now (la_late)
+        // given (la, la_ok), in LDS at la_lds (the next range, whole, copied
+        // there by k_decode_suffix while this range decoded: waited for
+        // now), or read from `in` only now (la_late)
         bool ok = la_ok;
-        bool val = false;  // la is a table value
-        if (la_lds || la_late) {
+        if (la_lds) {
+            vm_wait_all();
+            ok = true;
+            la = la_lds[lane];
+        } else if (la_late) {
             ok = re + lane < n;
-            la = !ok ? 0u : la_lds ? la_lds[lane] : in[re + lane];
-            val = VALS && la_lds;
+            la = ok ? in[re + lane] : 0u;
         }
         for (uint64_t q = re;;) {
-            const uint32_t t = !ok ? 0xFFu : val ? la : sm.tab[la];
+            const uint32_t t = ok ? sm.tab[la] : 0xFFu;
             const bool v = t < 64u;
             const uint64_t m = __ballot(v);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -2203,7 +2218,6 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
             }
             ok = q + lane < n;
             la = ok ? in[q + lane] : 0u;
-            val = false;
         }
     }
     wave_lds_order();
@@ -2323,28 +2337,23 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
 // tiles of kFuseTile ranges (kFusePer per wave) from a ticket in the order
 // they start, so a tile's predecessors are running or done whatever else
-// shares the GPU.  A tile is read from HBM once and every character looked
-// up once: a block draws its NEXT tile, counts it (all of the tile's loads
-// in flight at once) leaving each character's table value in LDS, and
-// publishes its count; then it takes the current tile's prefix and decodes
-// the current tile from the table values in LDS with decode_range.  So a
-// tile is counted one tile before it is decoded, and the prefix waits only
-// for tiles drawn before it -- which, counted right after they were drawn,
-// are.  (Counting a tile only after decoding the one before it made every
-// prefix wait on tiles still being decoded: the grid ran nearly serially,
-// 6 ms for 1 GiB.)  The prefix
-// is not a chained look-back: it is the counts of the tiles before it in
-// its group of 64 tiles (one status word per lane) plus the sums of the
-// earlier groups (every tile adds its count into its group's word), all
-// loaded at once: one memory round trip at any depth.  A range's last
-// group is completed from the first characters of the range after it, in
-// LDS unless that range is in the next tile.  (Round 3's form counted a
-// tile from HBM and read it again from HBM to decode it, a whole tile
-// later: 2.0x the input fetched, profiles/r03_g_pmc_junk005.txt.)  Every
-// block counts itself out in `wdone` when it leaves; the block that decodes
-// the last tile writes the record, waits until every block has left (so no
-// prefix read is in flight), then clears the status and group words, the
-// ticket, `wdone` and the failure words.
+// shares the GPU.  A block counts its tile and publishes the count, then
+// draws and counts its NEXT tile before it takes the first one's prefix, and
+// decodes the first one with decode_range (re-reading it).  The prefix is not
+// a chained look-back: it is the counts of the tiles before it in its group
+// of 64 tiles (one status word per lane) plus the sums of the earlier groups
+// (every tile adds its count into its group's word), all loaded at once, so
+// it takes one memory round trip at any depth and waits only for tiles drawn
+// before this one to be counted -- which, counted one tile ahead, they are.
+// (Round 2's chained look-back -- back over predecessors' aggregates 64 at a
+// time to the first inclusive prefix, right after the count, three waves
+// idle at a barrier -- cost 157 of 945 us on 1 GiB at junk density 0.05,
+// profiles/r03_ab_sfx_breakdown.jsonl.)  Every block counts itself out in
+// `wdone` when it leaves; the block that decodes the last tile writes the
+// record, waits until every block has left (so no prefix read is in
+// flight), then clears the status and group words, the ticket, `wdone` and
+// the failure words.
+// At least 6 waves per SIMD (80 VGPRs).
 
 // The idle test of k_decode_suffix<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
@@ -2387,16 +2396,6 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
     return true;
 }
 
-// The count leaves each character's table value in LDS in its place, so
-// the decode looks every character up once.
-#ifndef B64X_SFX_VALS  // A/B builds only
-#define B64X_SFX_VALS 1
-#endif
-constexpr bool kSfxVals = B64X_SFX_VALS;
-
-// At least 6 waves per SIMD (80 VGPRs); LDS (two tiles' table values,
-// kFusePer ranges per wave, 2 KiB each, and the windows) sets the blocks
-// per CU.
 template <bool WHOLE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_suffix(
@@ -2412,11 +2411,11 @@ void k_decode_suffix(
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
     if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
+    const bool dma = (((uintptr_t) in) & 15) == 0;
     __shared__ P2dSmem sm;
-    // two tiles' characters: s_chr[b][wave][j][64 h + lane] = the 16
-    // characters at beg + 1,024 h + 16 lane of the wave's range j (beg: the
-    // range's start, S for the first)
-    __shared__ uint4 s_chr[2][kWavesPerBlock][kFusePer][128];
+    // per wave: two ranges read ahead (an LDS object of its own, so that the
+    // compiler sees table and window reads cannot alias the copies in flight)
+    __shared__ uint4 s_rng[kWavesPerBlock][2][128];
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_cnt[2][kFuseTile];
     __shared__ uint32_t s_excl;
@@ -2426,57 +2425,47 @@ void k_decode_suffix(
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
 
-    auto span = [&](uint32_t r, uint64_t &beg, uint64_t &re) {
-        const uint64_t rb = (uint64_t) r * R;
-        beg = rb > S ? rb : S;
-        re = rb + R < n ? rb + R : n;
-    };
-    auto lane_nin = [&](uint32_t r, uint64_t beg, uint64_t re, int h) -> uint32_t {
-        const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
-        return r >= nranges || p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-    };
-    // Count tile t into s_cnt[b] (this wave's ranges: every load issued
-    // before any is counted; the table values' bit 7s, two ranges per packed
-    // DPP reduction) and leave each character's table value in s_chr[b],
-    // where the decode reads it: the tile is read from HBM once and every
-    // character looked up once.
-    auto count = [&](uint32_t t, uint32_t b) {
-        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;
-        uint4 c[kFusePer][2];
-        uint32_t nin[kFusePer][2];
+    // Count tile t into s_cnt[b] (each wave its kFusePer ranges; every
+    // wave's loads issued before any is counted).  Block-uniform call.
+    auto count_tile = [&](uint32_t t, uint32_t b) {
+        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
+        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
+            uint4 c[kFuseLoad][2];
+            uint32_t nin[kFuseLoad][2];
 #pragma unroll
-        for (uint32_t j = 0; j < kFusePer; j++) {
-            uint64_t beg, re;
-            span(rw + j, beg, re);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                nin[j][h] = lane_nin(rw + j, beg, re, h);
-                c[j][h] = nin[j][h] ? load_chars(in + beg + (uint64_t) h * kChunk + 16 * lane, nin[j][h])
-                                    : make_uint4(0, 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kFusePer; j += 2) {
-            uint32_t cnt = 0;
-#pragma unroll
-            for (uint32_t e = 0; e < 2; e++) {
-                if (j + e >= kFusePer) break;
+            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
+                const uint32_t r = rw + j0 + jj;
+                const uint64_t rb = (uint64_t) r * R;
+                const uint64_t beg = rb > S ? rb : S;
+                const uint64_t re = rb + R < n ? rb + R : n;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    uint32_t P[4];
-                    lane_values(sm.tab, c[j + e][h], nin[j + e][h], P);
-                    cnt += (16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
-                            __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u))
-                           << (16 * e);
-                    s_chr[b][wv][j + e][64 * h + lane] =
-                        kSfxVals ? make_uint4(P[0], P[1], P[2], P[3]) : c[j + e][h];
+                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
+                    nin[jj][h] = r >= nranges || p >= re
+                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                    c[jj][h] = nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
                 }
             }
-            const uint32_t tot =
-                (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan_dpp(cnt), 63);
-            if (lane == 0) {
-                s_cnt[b][wv * kFusePer + j] = tot & 0xFFFFu;
-                if (j + 1 < kFusePer) s_cnt[b][wv * kFusePer + j + 1] = tot >> 16;
+            // two ranges' counts (each <= 2,048) share one packed DPP scan
+            // (a shuffle reduction per range cost 25 VALU and 6 LDS ops)
+#pragma unroll
+            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
+                uint32_t cnt = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < 2; e++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        uint32_t P[4];
+                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
+                        cnt += lane_valid_count(P) << (16 * e);
+                    }
+                }
+                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
+                    (int) wave_incl_scan_dpp(cnt), 63);
+                if (lane == 0) {
+                    s_cnt[b][wv * kFusePer + j0 + jj] = tot & 0xFFFFu;
+                    s_cnt[b][wv * kFusePer + j0 + jj + 1] = tot >> 16;
+                }
             }
         }
     };
@@ -2512,17 +2501,19 @@ void k_decode_suffix(
     if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
     __syncthreads();
     uint32_t tA = s_tile[0], bA = 0;
-    if (tA < ntiles) count(tA, 0);
-    __syncthreads();
-    if (threadIdx.x == 0 && tA < ntiles) publish(tA, 0);
+    if (tA < ntiles) {
+        count_tile(tA, 0);
+        __syncthreads();
+        if (threadIdx.x == 0) publish(tA, 0);
+    }
     bool owner = false;  // this block decoded the last tile
     uint32_t Vs = 0;     // then: the suffix's alphabet characters
     while (tA < ntiles) {
         const uint32_t bB = bA ^ 1u;
         if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
-        __syncthreads();  // also: s_chr[bB] and s_cnt[bB] of two tiles back are consumed
+        __syncthreads();  // also: s_cnt[bB] of two tiles back is consumed
         const uint32_t tB = s_tile[bB];
-        if (tB < ntiles) count(tB, bB);
+        if (tB < ntiles) count_tile(tB, bB);
         __syncthreads();
         if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
         if (wv == 0) {
@@ -2533,25 +2524,53 @@ void k_decode_suffix(
         uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
         for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
         const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
+        // A whole range (2,048 characters from its aligned start) of a
+        // 16-byte aligned input is read ahead into LDS by two direct
+        // global->LDS copies (no VGPRs held) while the range before it
+        // decodes; the others (the first, from S; the stream's last) load
+        // as they decode.
+        auto whole = [&](uint32_t r) {
+            return dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
+        };
+        auto fetch = [&](uint32_t r, uint32_t buf) {
+            const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
+            lds_dma16(src, &s_rng[wv][buf][0]);
+            lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
+        };
+        if (whole(rw)) fetch(rw, 0);
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
-            uint64_t beg, re;
-            span(r, beg, re);
-            const bool last = r + 1 == nranges;
-            uint4 c[2];
-            uint32_t nin[2];
+            const uint64_t rb = (uint64_t) r * R;
+            const uint64_t re = rb + R < n ? rb + R : n;
+            const bool first = r == r0, last = r + 1 == nranges;
+            const uint64_t start = first ? S : rb;
+            const bool next_dma = j + 1 < kFusePer && whole(r + 1);
+            uint4 *buf = s_rng[wv][j & 1];
+            uint32_t nin[2] = {16u, 16u};
+            // Every range goes through the LDS buffer, so that one code path
+            // decodes them all: a joined path made the compiler wait for the
+            // register path's loads (vmcnt(0), draining the copy in flight)
+            // on the copied path too.  A whole range waits for its copy; any
+            // other is loaded here (and waited for) and written there.
+            if (whole(r)) {
+                vm_wait_all();
+            } else {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                c[h] = s_chr[bA][wv][j][64 * h + lane];
-                nin[h] = lane_nin(r, beg, re, h);
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                    buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+                }
             }
-            // the range after it, when it is in this tile, is in LDS
-            const uint32_t jn = wv * kFusePer + j + 1;
-            const uint8_t *la_lds =
-                jn < kFuseTile ? (const uint8_t *) s_chr[bA][jn / kFusePer][jn % kFusePer] : nullptr;
-            decode_range<kSfxVals>(sm, bq, in, n, beg, re, r == r0 ? 0 : range_skip(B),
-                                   base_out + (B + 3) / 4 * 3, c, nin, 0u, false, last, hold,
-                                   la_lds, true);
+            uint4 c[2];
+            c[0] = buf[lane];
+            c[1] = buf[64 + lane];
+            // then the next range's copy: in flight while this one decodes
+            // (no global load of the compiler's is outstanding from here on)
+            if (next_dma) fetch(r + 1, (j + 1) & 1);
+            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
+                         base_out + (B + 3) / 4 * 3, c, nin, 0u, !last, last, hold,
+                         next_dma ? (const uint8_t *) s_rng[wv][(j + 1) & 1] : nullptr, true);
             B += s_cnt[bA][wv * kFusePer + j];
         }
         if (tA == ntiles - 1) {
@@ -2565,6 +2584,7 @@ void k_decode_suffix(
     // every prefix read of this block is over (relaxed: the loads have
     // returned -- their values decided the loop -- and a release at agent
     // scope would write back the L2)
+    __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!owner || wv != 0) return;
     const uint64_t V = Vb + Vs;
@@ -5035,7 +5055,7 @@ const char *b64x_build_info(void)
 #define B64X_STR(x) B64X_STR2(x)
     return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
            "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
-           "(tiles read once into LDS, counted a tile ahead); rows:line model in row "
+           "(count ahead, group sums, LDS read-ahead); rows:line model in row "
            "bands; lanes:chained decoder blocks";
 }
 
