@@ -705,11 +705,15 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
                 return stage_fail(st, rc);
             return (ssize_t) n;
         }
-        if (blocked || staged) {
-            /* blocked: the completion brings the consumer back; staged but
-             * short of `count` while upstream answered EAGAIN: so does
-             * upstream's callback (a full-or-EAGAIN upstream makes the
-             * reference return EAGAIN here too, never a short count) */
+        if (blocked) {
+            errno = EAGAIN; /* the completion brings the consumer back */
+            return -1;
+        }
+        if (st->nbusy && st->slots[st->head].out_pos < st->slots[st->head].out_len) {
+            /* staged output short of `count` while upstream answered
+             * EAGAIN: upstream's callback brings the consumer back (a
+             * full-or-EAGAIN upstream makes the reference return EAGAIN
+             * here too, never a short count) */
             errno = EAGAIN;
             return -1;
         }

@@ -456,7 +456,7 @@ def bench_host_fd(args, b64):
                thread drains.
     One stream each way, one loop thread; payload GiB/s (N bytes), wall time
     from the first byte to the last, bit-checked (ingress: == the input;
-    egress: de-chunked == G3's digest, every chunk but the last full)."""
+    egress: de-chunked == G3's digest, every chunk but the last two full)."""
     import hashlib
 
     import numpy as np
@@ -530,7 +530,10 @@ def bench_host_fd(args, b64):
         h.update(memoryview(body)[pos:pos + size])
         sizes.append(size)
         pos += size + 2
-    ok = (g3 is None or h.hexdigest() == g3) and all(k == chunk for k in sizes[:-1])
+    # every chunk full but the last two: the body's last read comes up short
+    # at EOF and the finalize characters are a read of their own (ref
+    # src/base64encoder.c:124-131 -> finalize(), :61-99)
+    ok = (g3 is None or h.hexdigest() == g3) and all(k == chunk for k in sizes[:-2])
     if not ok:
         raise SystemExit("host_fd egress: framed output mismatch")
     res["egress_pipe"] = {"GiB_s": N / best / 2**30, "seconds": best,
