@@ -72,7 +72,7 @@ $(HOOKS): $(OBJDIR)/b64x_kernels_hooks.o
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
 
-$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_hub.o $(OBJDIR)/b64_stages.o
+$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_hub.o $(OBJDIR)/b64_stages.o $(OBJDIR)/b64_pin.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64_core.so
 
 $(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h

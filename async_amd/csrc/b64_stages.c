@@ -263,6 +263,29 @@ static void stage_stop(stage *st)
     st->started = false;
 }
 
+/* Lending from the queue (b64_lend.h, upstream side) needs this library's
+ * own queuestream (framing.c, the standalone library).  The stages-only
+ * library (INTEGRATION.md Option A) runs over the reference's queuestream,
+ * which it cannot see into: there these weak stand-ins take over and every
+ * block is gathered by reading, as before. */
+__attribute__((weak)) bool b64_src_peek(bytestream_1 s, const uint8_t **p, size_t *n,
+                                        struct b64_pin_slab **slab)
+{
+    (void) s, (void) p, (void) n, (void) slab;
+    return false;
+}
+
+__attribute__((weak)) void b64_src_take(bytestream_1 s, size_t n)
+{
+    (void) s, (void) n;
+}
+
+__attribute__((weak)) size_t b64_src_plain(bytestream_1 s, size_t lend_min, size_t limit)
+{
+    (void) s, (void) lend_min;
+    return limit;
+}
+
 /* Pull from upstream into the reservation `in` from offset `at` on, until
  * at least min_pull bytes have come in, or EOF, EAGAIN or an error; after
  * a short read it asks once more, so the EOF of a finite upstream lands in

@@ -65,6 +65,18 @@ def test_product_has_no_variant_knobs():
     assert "b64x__test_range_chunks" in hooks
 
 
+def test_every_environment_knob_is_documented():
+    """Every ASYNC_B64_* variable the product libraries can read is in
+    INTEGRATION.md's runtime-configuration table."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    core = os.path.join(ROOT, "async_amd", "libasync_b64_core.so")
+    for path in (_lib.LIB_PATH, core):
+        names = set(re.findall(rb"ASYNC_B64_[A-Z0-9_]+", open(path, "rb").read()))
+        assert names, path
+        for n in names:
+            assert f"`{n.decode()}`" in doc, (path, n)
+
+
 def test_binding_loads_and_sizes():
     lib = _lib.load()
     assert lib.b64x_encoded_len(0, True) == 0
@@ -187,8 +199,10 @@ def test_core_library_dependencies():
     core = os.path.join(ROOT, "async_amd", "libasync_b64_core.so")
     out = subprocess.run(["nm", "-D", "--undefined-only", core],
                          capture_output=True, text=True, check=True).stdout
-    names = {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
-    ours = {n for n in names if n.startswith(("async_", "NULL_ACTION", "bytestream_", "fs"))}
+    # every unversioned symbol that is not the HIP runtime's or a compiler
+    # hook must be one of the documented host-library names
+    names = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    ours = {n for n in names if "@" not in n and not n.startswith(("_", "hip"))}
     assert ours == {"async_wound", "async_execute", "async_register", "async_unregister",
                     "NULL_ACTION_1", "fsalloc", "fscalloc", "fsfree"}
     # the allocator is the reference's (fsdyn's) in a reference build: the
