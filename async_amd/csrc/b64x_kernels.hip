@@ -3077,6 +3077,9 @@ void k_decode_rows_lines(
     const uint64_t *rmw = (const uint64_t *) row_model(ws);
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
+    // (the row bands' spare blocks leave after the table build: tested
+    // before it, the model's loads no longer overlapped the build and MIME
+    // rows ran 481.6 -> 499.2 us, profiles/r04_ab_rows_early_exit.jsonl)
     build_dec_table(tab, a);
     __syncthreads();
     const uint32_t j0 = (uint32_t) r6, rcpS = (uint32_t) (r6 >> 32);
@@ -4594,6 +4597,8 @@ struct b64x_lane {
     uint64_t *h_stamp;    // fine-grained pinned: the last finished encode batch
     uint64_t seq;         // the last encode batch queued
     uint64_t in_cap, offs_cap, flags_cap;  // bytes allocated
+    b64x_seg *d_seg;      // an encode batch's lent segments (k_gather_host)
+    uint64_t seg_cap;
     b64x_dec_result *d_res;  // big decode jobs: the pipeline's record ...
     void *d_ws;              // ... and workspace (allocated at the first)
 };
@@ -4630,6 +4635,7 @@ void b64x_lane_close(b64x_lane *l)
     if (l->d_in) (void) hipFree(l->d_in);
     if (l->d_offs) (void) hipFree(l->d_offs);
     if (l->d_flags) (void) hipFree(l->d_flags);
+    if (l->d_seg) (void) hipFree(l->d_seg);
     if (l->d_res) (void) hipFree(l->d_res);
     if (l->d_ws) (void) hipFree(l->d_ws);
     if (l->h_stamp) (void) hipHostFree(l->h_stamp);
@@ -4728,9 +4734,10 @@ DEV void copy_from_host(const uint8_t *sa, const uint8_t *se, uint8_t *d)
 
 // A batch with lent segments into the device: block b covers device bytes
 // [b T, (b+1) T) of the batch, finds the first segment ending past its
-// start by a binary search, and copies its bytes from the segments' sources
-// or, between segments, from the arena h_in -- all read straight from
-// pinned host memory.
+// start by a binary search over the segment table (copied to the device
+// first: a search over host memory would pay the link's latency per step),
+// and copies its bytes from the segments' sources or, between segments,
+// from the arena h_in -- both read straight from pinned host memory.
 constexpr uint32_t kGatherTile = 64u << 10;
 __global__ __launch_bounds__(kThreads) void k_gather_host(
     uint8_t *__restrict__ d_in, const uint8_t *__restrict__ h_in, uint64_t total,
@@ -4782,8 +4789,13 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
         if ((err = lane_stage_in(l, nseg ? nullptr : h_in, njobs, h_in_off, h_out_off, 0)))
             return err;
         if (nseg && in_bytes) {
+            if ((err = lane_grow(l, (void **) &l->d_seg, &l->seg_cap, (uint64_t) nseg * sizeof(b64x_seg))) ||
+                (err = hip_err(hipMemcpyAsync(l->d_seg, h_seg, (size_t) nseg * sizeof(b64x_seg),
+                                              hipMemcpyHostToDevice, l->stream))))
+                return err;
             hipLaunchKernelGGL(k_gather_host, dim3((uint32_t) ((in_bytes + kGatherTile - 1) / kGatherTile)),
-                               dim3(kThreads), 0, l->stream, l->d_in, h_in, in_bytes, h_seg, nseg);
+                               dim3(kThreads), 0, l->stream, l->d_in, h_in, in_bytes,
+                               (const b64x_seg *) l->d_seg, nseg);
             if ((err = launch_status())) return err;
         }
         if ((err = b64x_encode_batch(l->d_in, l->d_offs, njobs, h_out, l->d_offs + words, abc,

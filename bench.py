@@ -489,7 +489,22 @@ def bench_host_fd(args, b64):
         best = dt if best is None else min(best, dt)
     res["ingress_blob_clean"] = {"GiB_s": N / best / 2**30, "seconds": best,
                                  "bytes_in": int(ch.size)}
-    del ch
+    # the channel alone, as calibration: the same characters written by the
+    # same peer thread and read(2) by one thread straight into a buffer, no
+    # decode (payload-equivalent GiB/s, to set beside the ingress legs)
+    sink = np.empty(ch.size + 16, np.uint8)
+    sink.fill(0)
+    for name, sock in (("channel_raw_pipe", False), ("channel_raw_socket", True)):
+        best = None
+        for _ in range(2):
+            got, err, dt = util.fd_raw(ch, write_chunk=1 << 20, read_size=1 << 18, sock=sock,
+                                       out=sink)
+            if got is None or got.size != ch.size:
+                raise SystemExit(f"host_fd {name}: errno {err}")
+            best = dt if best is None else min(best, dt)
+        res[name] = {"GiB_s_payload_equiv": N / best / 2**30, "seconds": best,
+                     "bytes": int(ch.size)}
+    del sink, ch
     legs = [("ingress_pipe_clean", chars_d, False), ("ingress_socket_clean", chars_d, True),
             ("ingress_pipe_crlf76", None, False)]
     for name, text_d, sock in legs:

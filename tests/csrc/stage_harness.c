@@ -902,6 +902,53 @@ ssize_t h_fd_decode(const uint8_t *chars, size_t n, size_t write_chunk, size_t r
     return r;
 }
 
+/* The channel alone (calibration for h_fd_decode): the same peer writer,
+ * and this thread reading the bytes with blocking read(2)s of read_size
+ * straight into out -- the least any consumer of the fd does. */
+ssize_t h_fd_raw(const uint8_t *data, size_t n, size_t write_chunk, size_t read_size,
+                 uint8_t *out, size_t cap, int sock, int *err_out, double *times)
+{
+    int fds[2];
+    if (make_channel(fds, sock) < 0) {
+        if (err_out)
+            *err_out = errno;
+        return -1;
+    }
+    peer w = { fds[1], data, n, write_chunk ? write_chunk : (1 << 20), NULL, 0, 0, 0, 0 };
+    pthread_t th;
+    double t0 = now_s();
+    pthread_create(&th, NULL, peer_writer, &w);
+    size_t got = 0;
+    int err = 0;
+    for (;;) {
+        size_t k = cap - got < read_size ? cap - got : read_size;
+        if (!k) {
+            err = ENOSPC;
+            break;
+        }
+        ssize_t r = read(fds[0], out + got, k);
+        if (r < 0) {
+            if (errno == EINTR)
+                continue;
+            err = errno;
+            break;
+        }
+        if (r == 0)
+            break;
+        got += (size_t) r;
+    }
+    double t1 = now_s();
+    close(fds[0]);
+    pthread_join(th, NULL);
+    if (times)
+        times[0] = t1 - t0;
+    if (!err)
+        err = w.err;
+    if (err_out)
+        *err_out = err;
+    return err ? -1 : (ssize_t) got;
+}
+
 typedef struct {
     async_t *async;
     fdsink_t *sink;

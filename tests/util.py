@@ -145,6 +145,8 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_fd_encode.argtypes = [vp, vp, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ctypes.c_int,
                               ip, dp]
     L.h_fd_encode.restype = ssz
+    L.h_fd_raw.argtypes = [vp, sz, sz, sz, vp, sz, ctypes.c_int, ip, dp]
+    L.h_fd_raw.restype = ssz
     return L
 
 
@@ -386,6 +388,20 @@ def egress_pieces(pieces, max_chunk: int, read_size: int, push=False, late=False
                                              int(push), int(late), max_chunk, read_size,
                                              out.ctypes.data, cap, ctypes.byref(err))
     return (out[:n].tobytes() if n >= 0 else None), err.value
+
+
+def fd_raw(data, write_chunk=1 << 20, read_size=1 << 18, sock=False, out=None, lib=None):
+    """The pipe or socket alone: a peer thread writes `data`, this thread
+    read(2)s it into `out`.  Returns (bytes array, errno, seconds)."""
+    src = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data
+    if out is None:
+        out = np.empty(src.size + 1, np.uint8)
+    err = ctypes.c_int(0)
+    t = np.zeros(1)
+    n = _lib_or_default(lib).h_fd_raw(src.ctypes.data if src.size else None, src.size, write_chunk,
+                                      read_size, out.ctypes.data, out.size, int(sock),
+                                      ctypes.byref(err), t.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return (out[:n] if n >= 0 else None), err.value, float(t[0])
 
 
 def dechunk(framed: bytes) -> bytes:
