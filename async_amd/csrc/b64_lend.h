@@ -54,6 +54,14 @@ size_t b64_src_plain(bytestream_1 s, size_t lend_min, size_t limit);
 bool b64_blob_lend_peek(bytestream_1 s, const uint8_t **p, size_t *n,
                         struct b64_pin_slab **slab);
 void b64_blob_lend_take(bytestream_1 s, size_t n);
+/* Downstream of the chunkencoder (fdstreams.c's fdsink): b64_chunk_lend()
+ * serves exactly the bytes chunkencoder_read(s, buf, count) would, but lends
+ * them instead of copying: *p points at the next contiguous run of the
+ * frame (the header, or the data where the encoder stage lent it), at most
+ * `count` bytes, valid until the next call or close.  -1/errno and 0 as a
+ * read. */
+bool b64_chunk_lendable(bytestream_1 s);
+ssize_t b64_chunk_lend(bytestream_1 s, size_t count, const uint8_t **p);
 /* copy_blobstream() into the pinned pool (an ordinary copy without it). */
 blobstream_t *b64_pinned_blobstream(async_t *async, const void *blob, size_t count);
 

@@ -17,6 +17,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include "b64_lend.h"
 #include "b64_trace.h"
 #include "fdsink.h"
 #include "fsalloc.h"
@@ -124,7 +125,9 @@ struct fdsink {
     uint64_t uid;
     bytestream_1 source;  /* owned */
     int fd;               /* owned; -1 once closed */
-    size_t cursor, count; /* unsent bytes: outbuf[cursor, count) */
+    size_t cursor, count; /* unsent bytes: out[cursor, count) */
+    const uint8_t *out;   /* outbuf, or the run the chunkencoder lent */
+    bool lend;            /* the source is this library's chunkencoder */
     bool done, closed, probe_queued;
     int err;
     uint64_t bytes;
@@ -166,7 +169,13 @@ static void sink_probe(fdsink_t *s)
         return;
     for (int burst = 0; burst < SINK_BURST; burst++) {
         if (s->cursor == s->count) {
-            ssize_t n = bytestream_1_read(s->source, s->outbuf, sizeof s->outbuf);
+            /* over this library's chunkencoder the pull lends the frame's
+             * bytes where they are (the header, the encoder's staged
+             * characters): the same bytes and counts, one copy fewer */
+            const uint8_t *lent = NULL;
+            ssize_t n = s->lend ? b64_chunk_lend(s->source, sizeof s->outbuf, &lent)
+                                : bytestream_1_read(s->source, s->outbuf, sizeof s->outbuf);
+            s->out = lent ? lent : s->outbuf;
             FSTRACE(ASYNC_FDSINK_REPLENISH, s->uid, n);
             if (n < 0) {
                 if (errno != EAGAIN)
@@ -180,7 +189,7 @@ static void sink_probe(fdsink_t *s)
             s->cursor = 0;
             s->count = (size_t) n;
         }
-        ssize_t w = write(s->fd, s->outbuf + s->cursor, s->count - s->cursor);
+        ssize_t w = write(s->fd, s->out + s->cursor, s->count - s->cursor);
         FSTRACE(ASYNC_FDSINK_WRITE, s->uid, s->count - s->cursor, w);
         if (w < 0) {
             if (errno == EAGAIN)
@@ -206,6 +215,8 @@ fdsink_t *open_fdsink(async_t *async, bytestream_1 source, int fd)
     s->uid = b64_trace_unique_id();
     s->source = source;
     s->fd = fd;
+    s->out = s->outbuf;
+    s->lend = b64_chunk_lendable(source);
     s->cb = NULL_ACTION_1;
     FSTRACE(ASYNC_FDSINK_CREATE, s->uid, s, async, fd);
     action_1 probe = { s, (act_1) sink_probe };

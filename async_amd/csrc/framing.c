@@ -284,6 +284,8 @@ bytestream_1 queuestream_as_bytestream_1(queuestream_t *q)
 
 /* ========================================================= chunk framing */
 
+static const struct bytestream_1_vt chunk_vt;
+
 enum {
     CHUNK_MIN = 2,
     CHUNK_MAX = 16 * 1024 * 1024,
@@ -350,57 +352,98 @@ static size_t chunk_header(chunkencoder_t *c, size_t n)
     return p;
 }
 
+/* The current frame is served: build the next one (1), or 0 after the
+ * terminating frame, -1 with errno from upstream. */
+static int chunk_refill(chunkencoder_t *c)
+{
+    if (c->data) { /* the lent chunk has been served */
+        b64_lend_return(c->up);
+        c->data = NULL;
+    }
+    if (c->last_framed)
+        return 0;
+    /* same count as a read into the frame; from the GPU encoder the
+     * data usually stays where the stage has it (one copy fewer) */
+    ssize_t n = b64_lend_read(c->up, c->lend ? NULL : c->frame + CHUNK_HEAD, c->max_chunk,
+                              &c->data);
+    if (n < 0)
+        return -1;
+    c->pos = chunk_header(c, (size_t) n);
+    c->end = CHUNK_HEAD + (size_t) n;
+    if (n == 0) {
+        c->last_framed = true;
+        switch (c->termination) {
+            case CHUNKENCODER_SIMPLE: /* "0\r\n" + empty trailer "\r\n" */
+                c->frame[c->end++] = '\r';
+                c->frame[c->end++] = '\n';
+                break;
+            case CHUNKENCODER_STOP_AT_TRAILER: /* "0\r\n" */
+                break;
+            case CHUNKENCODER_STOP_AT_FINAL_EXTENSIONS: /* "0" */
+                c->end -= 2;
+                break;
+            default:
+                abort();
+        }
+    }
+    return 1;
+}
+
+/* The next contiguous run of the frame, at most `count` bytes: the header
+ * (and closing CRLF) from the frame, the data from the frame or from where
+ * the GPU encoder stage lent it. */
+static size_t chunk_run(chunkencoder_t *c, size_t count, const uint8_t **p)
+{
+    size_t n = c->end - c->pos;
+    if (n > count)
+        n = count;
+    if (c->data && c->pos < CHUNK_HEAD) {
+        if (n > CHUNK_HEAD - c->pos)
+            n = CHUNK_HEAD - c->pos;
+        *p = c->frame + c->pos;
+    } else {
+        *p = (c->data ? c->data - CHUNK_HEAD : c->frame) + c->pos;
+    }
+    c->pos += n;
+    return n;
+}
+
 ssize_t chunkencoder_read(chunkencoder_t *c, void *buf, size_t count)
 {
     if (!count)
         return 0;
     if (c->pos == c->end) {
-        if (c->data) { /* the lent chunk has been served */
-            b64_lend_return(c->up);
-            c->data = NULL;
-        }
-        if (c->last_framed)
-            return 0;
-        /* same count as a read into the frame; from the GPU encoder the
-         * data usually stays where the stage has it (one copy fewer) */
-        ssize_t n = b64_lend_read(c->up, c->lend ? NULL : c->frame + CHUNK_HEAD,
-                                  c->max_chunk, &c->data);
-        if (n < 0)
-            return -1;
-        c->pos = chunk_header(c, (size_t) n);
-        c->end = CHUNK_HEAD + (size_t) n;
-        if (n == 0) {
-            c->last_framed = true;
-            switch (c->termination) {
-                case CHUNKENCODER_SIMPLE: /* "0\r\n" + empty trailer "\r\n" */
-                    c->frame[c->end++] = '\r';
-                    c->frame[c->end++] = '\n';
-                    break;
-                case CHUNKENCODER_STOP_AT_TRAILER: /* "0\r\n" */
-                    break;
-                case CHUNKENCODER_STOP_AT_FINAL_EXTENSIONS: /* "0" */
-                    c->end -= 2;
-                    break;
-                default:
-                    abort();
-            }
-        }
+        int r = chunk_refill(c);
+        if (r <= 0)
+            return r;
     }
-    size_t n = c->end - c->pos;
-    if (n > count)
-        n = count;
-    size_t done = 0;
-    if (c->data && c->pos < CHUNK_HEAD) { /* header from the frame */
-        done = CHUNK_HEAD - c->pos < n ? CHUNK_HEAD - c->pos : n;
-        memcpy(buf, c->frame + c->pos, done);
-        c->pos += done;
+    /* as many bytes as the frame has, in up to two runs */
+    size_t done = 0, want = c->end - c->pos < count ? c->end - c->pos : count;
+    while (done < want) {
+        const uint8_t *p;
+        size_t n = chunk_run(c, want - done, &p);
+        memcpy((uint8_t *) buf + done, p, n);
+        done += n;
     }
-    if (done < n) {
-        const uint8_t *src = c->data ? c->data - CHUNK_HEAD : c->frame;
-        memcpy((uint8_t *) buf + done, src + c->pos, n - done);
-        c->pos += n - done;
+    return (ssize_t) done;
+}
+
+bool b64_chunk_lendable(bytestream_1 s)
+{
+    return s.vt == &chunk_vt;
+}
+
+ssize_t b64_chunk_lend(bytestream_1 s, size_t count, const uint8_t **p)
+{
+    chunkencoder_t *c = s.obj;
+    if (!count)
+        return 0;
+    if (c->pos == c->end) {
+        int r = chunk_refill(c);
+        if (r <= 0)
+            return r;
     }
-    return (ssize_t) n;
+    return (ssize_t) chunk_run(c, count, p);
 }
 
 void chunkencoder_close(chunkencoder_t *c)
