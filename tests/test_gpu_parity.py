@@ -766,6 +766,32 @@ def test_decode_lines_takes_clean_and_mime_whole(aligned):
             assert start <= brk and brk - start < 1 << 12, (brk, start)
 
 
+def test_repeat_junk_decode_takes_the_hinted_single_pass():
+    """A call whose probe cut the line model near the start leaves a hint
+    for the next call on the same workspace, input and length: that one
+    takes the single pass (no k_decode_lines launch) after its own probe.
+    Every call is exact; a clean stream in the same buffer goes back to the
+    lines pass on the call after the one that finds it clean."""
+    rng = np.random.default_rng(47)
+    chars = orc.encode(rng.integers(0, 256, 3_000_000, dtype=np.uint8))
+    junky = _junk(rng, chars, 0.05)
+    clean = orc.encode(rng.integers(0, 256, len(junky), dtype=np.uint8))[:len(junky)]
+    buf = torch.empty(len(junky), dtype=torch.uint8, device=DEV)
+    out = torch.empty(b64.decoded_cap(len(junky)) + 8, dtype=torch.uint8, device=DEV)
+    ws = torch.zeros(b64.workspace_size(len(junky)), dtype=torch.uint8, device=DEV)
+    starts = []
+    for text in (junky, junky, junky, clean, clean):
+        buf.copy_(dev(text))
+        d = b64.decode(buf, out=out, workspace=ws)
+        assert d.bytes().cpu().numpy().tobytes() == orc.decode(text)
+        starts.append(_sfx_start(ws))
+    # the first junk call: the lines pass and the suffix from the cut; the
+    # hinted ones leave the record of where a suffix started alone
+    assert starts[0] < len(junky) // 16 and starts[1] == starts[2] == starts[0]
+    # the first clean call still ran on the hint; its probe renewed it
+    assert starts[3] == starts[0] and starts[4] == 2**64 - 1
+
+
 def _probe_model(ws: torch.Tensor):
     """The line model k_decode_probe left in the workspace (header bytes
     32..63): (L, s, T, skip)."""
