@@ -133,3 +133,32 @@ def test_egress_stacks_threads(threads, devices):
         msg = payload[off:off + L].tobytes()
         off += L
         assert framed[i] == orc.chunked_encode(msg, max_chunk=1 << 20), (i, L)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["1024", "65536", None])
+@pytest.mark.parametrize("lend_min", ["1", "4096"])
+def test_egress_lent_pieces_gpu(monkeypatch, cap, lend_min):
+    """Messages lent from their pinned queue copies on the MI355X: short
+    and long messages mixed in one queue, blocks that mix arena bytes and
+    lent segments at every alignment (k_gather_host), carries across blocks
+    of one message; framed bytes equal the oracle stack's, and every pinned
+    reference is released."""
+    if cap:
+        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", cap)
+    monkeypatch.setenv("ASYNC_B64_LEND_MIN", lend_min)
+    L = util.harness()
+    rng = np.random.default_rng(0x1E48)
+    sizes = [1, 2, 3, 5000, 4095, 4096, 4097, 100001, 7, 65537, 300000, 12, 9000, 3 << 20, 5]
+    pieces = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    lent0 = L.b64_hub_lent_total()
+    for max_chunk, read_size in ((4096, 1000), (1 << 20, 10240)):
+        got, err = util.egress_pieces(pieces, max_chunk, read_size)
+        assert err == 0 and got is not None
+        data = b"".join(pieces)
+        want = orc.chunked_encode(np.frombuffer(data, np.uint8),
+                                  piece_lens=[len(p) for p in pieces],
+                                  max_chunk=max_chunk, read_size=read_size)
+        assert got == want
+    assert L.b64_hub_lent_total() > lent0
+    assert L.b64_pin_live_refs() == 0
