@@ -311,7 +311,10 @@ static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, 
     if (st->dir == DIR_ENCODE) /* the block so far: the carry */
         for (size_t i = 0; i < at; i++)
             st->tail[0] = st->tail[1], st->tail[1] = in[i];
-    bool lent_last = false; /* the last bytes came by lending */
+    /* the last step took fewer bytes than one copying read of the room
+     * would have (a lent message, or a read stopped where one begins): a
+     * split of what the queue's own read would have returned in one call */
+    bool split = false;
     while (got < room) {
         size_t ask = room - got;
         const uint8_t *lp;
@@ -329,25 +332,30 @@ static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, 
                     st->tail[1] = lp[0];
                 }
                 got += n;
-                lent_last = true;
-                if (got >= want)
-                    break;
+                split = true;
+                /* no min_pull stop here: a copying read of `ask` would have
+                 * gone on into the next elements, so the block fills its
+                 * room as that read would (block sizes decide the read
+                 * counts the encoder can serve, and so the framing) */
                 continue;
             }
         }
+        bool limited = false;
         if (st->dir == DIR_ENCODE) {
             ask = b64_src_plain(st->up, st->lend_min, ask);
             if (!ask) /* a lendable message comes next, but the hub is full */
                 ask = room - got;
+            limited = ask < room - got;
         }
         ssize_t n = bytestream_1_read(st->up, dst + got, ask);
         if (st->dir == DIR_DECODE)
             FSTRACE(ASYNC_BASE64DECODER_READ_INPUT_DUMP, st->uid, dst + got, n);
         if (n < 0) {
             *err = errno ? errno : EIO;
-            /* after lent bytes, the queue's own read would have returned
-             * them as a short count (ref src/queuestream.c read loop) */
-            if (lent_last && *err == EAGAIN)
+            /* after a split, the queue's own read would have returned the
+             * bytes before it as a short count (ref src/queuestream.c read
+             * loop) */
+            if (split && *err == EAGAIN)
                 st->short_seen = true;
             break;
         }
@@ -355,7 +363,7 @@ static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, 
             *eof = true;
             break;
         }
-        lent_last = false;
+        split = limited && (size_t) n == ask;
         if (n >= 2) {
             st->tail[0] = dst[got + (size_t) n - 2];
             st->tail[1] = dst[got + (size_t) n - 1];
@@ -366,7 +374,7 @@ static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, 
         got += (size_t) n;
         if ((size_t) n < ask)
             st->short_seen = true;
-        else if (got >= want)
+        else if (got >= want && !split)
             break;
     }
     if (tr) {

@@ -363,3 +363,34 @@ def test_egress_stacks_lent_and_released():
         assert got[i] == want, i
     assert L.b64_hub_lent_total() - lent0 >= sum(1 for n in lens if n >= 4096)
     assert L.b64_pin_live_refs() == 0
+
+
+def test_egress_lent_fuzz(monkeypatch):
+    """Seeded fuzz of lent and gathered messages (scripts/fuzz_lent.py's
+    cases, fake device): random queues of 0 B - 1.5 MiB messages, stage
+    capacities, lend thresholds, chunk and read sizes, pushes, late
+    termination.  Found the gather stopping at min_pull after a lent
+    message (smaller blocks than one copying read would fill, so a short
+    read count and other chunk sizes than the reference's)."""
+    L = fake()
+    for seed in range(24):
+        rng = np.random.default_rng(0xF0221 + seed)
+        k = int(rng.integers(1, 40))
+        sizes = [0 if rng.random() < 0.05 else int(np.exp(rng.uniform(0, np.log(1.5 * 2**20))))
+                 for _ in range(k)]
+        pieces = [rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]
+        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(int(rng.choice([64, 1000, 4096, 65536, 1 << 20]))))
+        monkeypatch.setenv("ASYNC_B64_LEND_MIN", str(int(rng.choice([1, 3, 4096, 65536]))))
+        max_chunk = int(rng.choice([30, 4096, 65536, 1 << 20]))
+        read_size = int(rng.choice([7, 1000, 10240, 1 << 18]))
+        push, late = bool(rng.random() < 0.3), bool(rng.random() < 0.3)
+        L.fake_configure(seed, 0, 0)
+        got, err = util.egress_pieces(pieces, max_chunk, read_size, push=push, late=late, lib=L)
+        assert err == 0 and got is not None, seed
+        data = b"".join(pieces)
+        if late:
+            assert util.dechunk(got) == orc.encode(data), seed
+        else:
+            assert got == orc.chunked_encode(np.frombuffer(data, np.uint8), piece_lens=sizes,
+                                             max_chunk=max_chunk, read_size=read_size), seed
+    assert L.b64_pin_live_refs() == 0
