@@ -12,6 +12,9 @@ Three timed passes under ASYNC_B64_HUB_TRACE=1, each broken into phases:
     reserve_s  arena reservations (with the launches of the batches they seal)
     launch_s   batch launches (H2D, kernel, D2H enqueue)
     wake_s     completion processing (hub wake-ups)
+    gpu_span_s first batch launched to last batch completed (the GPU side:
+               gather kernels reading the lent messages over the host link,
+               encode kernels writing the characters into pinned memory)
     other_s    loop_s minus read_s minus wake_s: the loop itself, waiting
                for the GPU, callbacks
 then one pass under the harness's SIGPROF sampler (the loop thread's CPU
@@ -91,6 +94,7 @@ def main():
                    hub.get("gather_bytes", 0) / max(hub.get("gather_s", 0), 1e-9) / 2**30,
                "reserve_s": hub.get("reserve_s"), "launch_s": hub.get("launch_s"),
                "wake_s": hub.get("wake_s"), "batches": hub.get("batches"),
+               "gpu_span_s": hub.get("span_s"), "lent_bytes": hub.get("lent_bytes"),
                "other_s": t[1] - read_s - hub.get("wake_s", 0.0)}
         rows.append(row)
         print(json.dumps(row), flush=True)
