@@ -962,7 +962,8 @@ static void sink_finished(sink_watch *sw)
 /* Egress: the `npieces` pieces of `in` (lens[i] bytes each) as blobstreams
  * on one terminated queuestream -> base64_encode (GPU stage) ->
  * chunk_encode(max_chunk) -> fdsink (10,240-byte pulls, write(2)) into a
- * pipe (or socketpair) that a peer thread reads into out.  times[0] = wall
+ * pipe (or socketpair) that a peer thread reads into out.  max_chunk 0:
+ * no framing, the sink reads the encoder itself (its copying path).  times[0] = wall
  * time from the loop's start to the peer's EOF.  Returns the framed length
  * or -1 + *err_out. */
 ssize_t h_fd_encode(const uint8_t *in, const size_t *lens, size_t npieces, size_t max_chunk,
@@ -991,13 +992,15 @@ ssize_t h_fd_encode(const uint8_t *in, const size_t *lens, size_t npieces, size_
     queuestream_terminate(q);
     base64encoder_t *e = base64_encode(async, queuestream_as_bytestream_1(q), pos62, pos63,
                                        pad != 0, padchar);
-    chunkencoder_t *ch = chunk_encode(async, base64encoder_as_bytestream_1(e), max_chunk);
+    bytestream_1 src = base64encoder_as_bytestream_1(e);
+    if (max_chunk)
+        src = chunkencoder_as_bytestream_1(chunk_encode(async, src, max_chunk));
     peer rd = { fds[0], NULL, 0, 0, out, cap, 0, 0, 0 };
     pthread_t th;
     double t0 = now_s();
     pthread_create(&th, NULL, peer_reader, &rd);
     sink_watch sw = { async, NULL };
-    sw.sink = open_fdsink(async, chunkencoder_as_bytestream_1(ch), fds[1]);
+    sw.sink = open_fdsink(async, src, fds[1]);
     fdsink_register_callback(sw.sink, (action_1) { &sw, (act_1) sink_finished });
     int rc = fdsink_done(sw.sink) ? 0 : async_loop(async);
     int err = rc < 0 ? errno : fdsink_error(sw.sink);

@@ -94,6 +94,21 @@ def test_fd_encode_fake_elements_past_the_arena_room(fake, max_chunk):
                                                read_size=10240)
 
 
+@pytest.mark.parametrize("sock", [False, True])
+def test_fd_encode_fake_unframed(fake, sock):
+    """fdsink reading the encoder itself (no chunk stage, so no lending):
+    its copying read path, 10,240-byte pulls, into a pipe or socket."""
+    fake.fake_configure(3, 30, 0)
+    rng = np.random.default_rng(31)
+    data = rng.integers(0, 256, 700003, dtype=np.uint8).tobytes()
+    pieces = [1, 350000, 4, 349998]
+    for pos62, pos63, pad in ((-1, -1, True), ("-", "_", False)):
+        got, err, _ = util.fd_encode(data, pieces, max_chunk=0, pos62=pos62, pos63=pos63,
+                                     pad=pad, sock=sock, lib=fake)
+        assert err == 0 and got is not None
+        assert got.tobytes() == orc.encode(data, pos62=pos62, pos63=pos63, pad=pad)
+
+
 def test_fd_encode_empty(fake):
     got, err, _ = util.fd_encode(b"", lib=fake)
     assert err == 0 and got.tobytes() == orc.chunked_encode(b"", max_chunk=1 << 20,
@@ -139,3 +154,12 @@ def test_fd_encode_gpu(max_chunk):
     assert err == 0 and got is not None
     assert got.tobytes() == orc.chunked_encode(data, pieces, max_chunk=max_chunk,
                                                read_size=10240)
+
+
+@pytest.mark.gpu
+def test_fd_encode_gpu_unframed():
+    rng = np.random.default_rng(29)
+    data = rng.integers(0, 256, (8 << 20) + 2, dtype=np.uint8).tobytes()
+    got, err, _ = util.fd_encode(data, [1 << 20, (7 << 20) + 2], max_chunk=0, sock=True)
+    assert err == 0 and got is not None
+    assert got.tobytes() == orc.encode(data)

@@ -356,12 +356,13 @@ def fd_encode(data, pieces=None, max_chunk=1 << 20, pos62=-1, pos63=-1, pad=True
               sock=False, out=None, lib=None):
     """Egress through a real fd: `data` (split into `pieces` lengths) on a
     queuestream -> base64_encode stage -> chunk_encode(max_chunk) -> fdsink
-    (10,240-byte pulls, write(2)) -> a pipe a peer thread drains.  Returns
+    (10,240-byte pulls, write(2)) -> a pipe a peer thread drains
+    (max_chunk 0: no framing, the sink reads the encoder).  Returns
     (framed bytes as a numpy view | None, errno, seconds)."""
     src = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else \
         np.ascontiguousarray(data, dtype=np.uint8)
     lens = np.asarray(pieces if pieces is not None else [src.size], dtype=np.uintp)
-    cap = framed_cap(src.size, max_chunk)
+    cap = framed_cap(src.size, max_chunk) if max_chunk else (src.size + 2) // 3 * 4 + 16
     if out is None:
         out = np.empty(cap, np.uint8)
     err = ctypes.c_int(0)
