@@ -907,6 +907,13 @@ constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kFuseTile / kSfxGroup + 1
 // failure words, fail_any, wdone: one 128-byte line each
 constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
+// Workspace bytes for plans of up to nr ranges: the fixed regions, then
+// counts + bases (at least 64 bytes).
+constexpr uint64_t ws_bytes_for(uint64_t nr)
+{
+    return kWsScratch + ((nr * 4 + 7) / 8 * 8 + nr * 8 > 64 ? (nr * 4 + 7) / 8 * 8 + nr * 8 : 64);
+}
+
 // Layout: 64-byte header (fd, fd_cur, ticket, fticket, sfx_start, model), the
 // zero-between-calls regions at fixed offsets, then the scratch counts and
 // bases of `nranges` ranges.
@@ -2868,8 +2875,8 @@ DEV bool row_last_slot(const uint8_t *tab, uint4 w, const uint32_t A[4], uint32_
 // Uniform-stride batch decode of rows with room (out_stride >= 12 S), with
 // k_decode_lines' line model (MIME-formatted batches:
 // every row in 76-character lines with CRLF).  The model is probed from the
-// batch's first row by k_rows_prep (which also zeroes outlen[], replacing a
-// memset) and applies to every row; a row that does not follow it fails a
+// batch's first row by k_rows_prep (which also zeroes the failure bitmap)
+// and applies to every row; a row that does not follow it fails a
 // check and is marked for the fix-up, which decodes it exactly.  Row slot q
 // owns the row's sextets [16q, 16q + 16) and their span; slots before the
 // row's last are checked strictly (16 alphabet characters, separator bytes
@@ -2907,10 +2914,11 @@ struct RowModel {
 static_assert(sizeof(RowModel) == 96, "RowModel layout");
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
-// The library workspace of the stream holds the model, in the region pass 1
-// uses for its per-range counts (scratch between calls), and after it the
-// rows' failure bitmap: bit b set when row b must be decoded exactly.
-DEV RowModel *row_model(void *ws) { return (RowModel *) ((uint8_t *) ws + kWsScratch); }
+// The library workspace of the stream holds the rows' failure bitmap in the
+// region pass 1 uses for its per-range counts (scratch between calls; bit b
+// set when row b must be decoded exactly), and the model past the end of the
+// decode workspace proper, where no other kernel writes: the model of the
+// stream's last row batch stays there for the next one of the same shape.
 DEV unsigned long long *row_fail(void *ws)
 {
     return (unsigned long long *) ((uint8_t *) ws + kWsScratch + sizeof(RowModel));
@@ -2954,7 +2962,9 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
 //   k_rows_prep   zeroes the failure bitmap and, in one wave, probes the line
 //                 model from row 0 and decodes row 0's last slot: its
 //                 alphabet count j0 is the shape every passing row's last slot
-//                 must have, so a passing row's length is known in advance;
+//                 must have, so a passing row's length is known in advance
+//                 (skipped when the workspace holds the model of a batch of
+//                 the same shape: b64x_decode_strided);
 //   k_decode_rows_lines  checks and decodes every slot, marking a row that
 //                 does not pass (one atomicOr of its bit, by the first failing
 //                 lane of the row in the wave; no per-row atomics otherwise);
@@ -2965,7 +2975,7 @@ DEV bool row_lines_slot(const uint8_t *tab, const RowModel &rm, const uint32_t w
 // rows, 1.09x the output's write traffic, profiles/r02_pmc_rows32_crlf76.json.)
 __global__ __launch_bounds__(kThreads) void k_rows_prep(
     uint32_t nbuf, const uint8_t *__restrict__ in, uint32_t len, uint64_t in_stride, uint32_t S,
-    uint64_t out_stride, DecAlpha a, void *ws)
+    uint64_t out_stride, DecAlpha a, void *ws, RowModel *rmodel)
 {
     unsigned long long *bm = row_fail(ws);
     const uint32_t nw = (nbuf + 63) / 64;
@@ -3050,7 +3060,7 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
                (uint64_t) kRowsU * r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
                out_stride < (1u << 24);
     }
-    if (threadIdx.x == 0) *row_model(ws) = r;
+    if (threadIdx.x == 0) *rmodel = r;
 }
 
 // The row kernel.  Clean rows (the model's L = 0): the block's first slot
@@ -3087,10 +3097,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1)))
 void k_decode_rows_lines(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint32_t len,
     uint8_t *__restrict__ out, uint64_t out_stride, uint32_t S, uint32_t magic, uint64_t m64,
-    uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws)
+    uint64_t nslots, uint64_t tail_slot, DecAlpha a, uint32_t nbuf, void *ws,
+    const RowModel *rmodel)
 {
     __shared__ uint8_t tab[256];
-    const uint64_t *rmw = (const uint64_t *) row_model(ws);
+    const uint64_t *rmw = (const uint64_t *) rmodel;
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
     // (the row bands' spare blocks leave after the table build: tested
@@ -3448,16 +3459,19 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
 }
 
 // Row lengths after k_decode_rows_lines: one wave per 64 rows (one bitmap
-// word, read through the scalar cache), every unmarked row's length (the
-// prep's len0) by one coalesced store per lane, then the marked rows decoded
-// exactly one after another with pass 2d's bit-stream machinery (as
-// k_decode_batch_fix2 does).
+// word, read through the scalar cache and cleared for the next batch), every
+// unmarked row's length (the model's len0) by one coalesced store per lane,
+// then the marked rows decoded exactly one after another with pass 2d's
+// bit-stream machinery (as k_decode_batch_fix2 does).  Row 0 marked: the
+// model does not fit this batch's first row, so *stale (pinned, the
+// launcher's) asks for a fresh probe next time.
 __global__ __launch_bounds__(kThreads) void k_rows_finish(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, BatchLayout L,
-    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a, void *ws)
+    uint32_t nbuf, uint64_t *__restrict__ outlen, DecAlpha a, void *ws,
+    const RowModel *rmodel, uint32_t *stale)
 {
     __shared__ P2dSmem sm;
-    const uint64_t len0 = scalar_load_u64((const uint64_t *) row_model(ws) + 7);
+    const uint64_t len0 = scalar_load_u64((const uint64_t *) rmodel + 7);
     const unsigned long long *bm = row_fail(ws);
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
@@ -3470,6 +3484,10 @@ __global__ __launch_bounds__(kThreads) void k_rows_finish(
         uint64_t m = scalar_load_u64((const uint64_t *) bm + g);
         const uint64_t b = base + lane;
         if (b < nbuf && !((m >> lane) & 1)) outlen[b] = len0;
+        if (m && lane == 0) {
+            ((unsigned long long *) bm)[g] = 0;
+            if (g == 0 && (m & 1) && stale) *stale = 1u;
+        }
         while (m) {
             const uint32_t r = (uint32_t) (base + __ffsll((unsigned long long) m) - 1);
             m &= m - 1;
@@ -3654,6 +3672,24 @@ bool g_info_done[kMaxDevices];
 //    test on the MI355X: hipFree waits for the whole device.)
 //  - Each call leaves the workspace zeroed for the next (re-armed by the
 //    kernels), so a rebound workspace needs no clearing.
+// A library workspace: the decode workspace for the largest plan, then the
+// row batches' model (row_model_of).
+constexpr uint64_t kLibRowsOff = (ws_bytes_for(kMaxRanges) + 255) & ~255ull;
+constexpr uint64_t kLibWsBytes = kLibRowsOff + 256;
+static RowModel *row_model_of(void *ws) { return (RowModel *) ((uint8_t *) ws + kLibRowsOff); }
+
+// The shape a row batch's model was made for (nbuf 0: no model held).
+struct RowsShape {
+    uint64_t len, in_stride, out_stride;
+    uint32_t nbuf;
+    int p62, p63;
+    bool operator==(const RowsShape &o) const
+    {
+        return len == o.len && in_stride == o.in_stride && out_stride == o.out_stride &&
+               nbuf == o.nbuf && p62 == o.p62 && p63 == o.p63;
+    }
+};
+
 struct WsEntry {
     int dev;
     void *stream;       // bound stream; nullptr = idle (reusable)
@@ -3663,6 +3699,7 @@ struct WsEntry {
     uint64_t used;      // last use (g_ws_tick)
     int pins;           // calls between lookup and their event record
     bool release;       // b64x_release_stream while pinned: unbind at unpin
+    RowsShape rows;     // the row batch shape whose model the workspace holds
 };
 constexpr int kWsCache = 8;
 std::mutex g_ws_mu;     // g_ws, g_ws_tick (never held across a waiting HIP call)
@@ -3788,8 +3825,7 @@ uint64_t b64x_decode_workspace_size(uint64_t nchars)
     // largest input); at least room for a RowModel in the scratch
     uint64_t nr = nchars ? (nchars + kChunk - 1) / kChunk : kMaxRanges;
     if (nr > kMaxRanges) nr = kMaxRanges;
-    const uint64_t scratch = (nr * 4 + 7) / 8 * 8 + nr * 8;
-    return kWsScratch + (scratch > 64 ? scratch : 64);
+    return ws_bytes_for(nr);
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
@@ -3884,8 +3920,9 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
 
 // The workspace of (current device, stream), pinned; *slot receives its
 // entry for ws_unpin().
-static void *library_workspace(void *stream, int *slot, int *err)
+static void *library_workspace(void *stream, int *slot, int *err, RowsShape *rows = nullptr)
 {
+    if (rows) *rows = RowsShape{};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
         *err = -ENODEV;
@@ -3903,6 +3940,7 @@ static void *library_workspace(void *stream, int *slot, int *err)
                 e.pins++;
                 *slot = i;
                 *err = 0;
+                if (rows) *rows = e.rows;
                 return e.ws;
             }
         }
@@ -3934,7 +3972,7 @@ static void *library_workspace(void *stream, int *slot, int *err)
     if (fresh) {
         void *p = nullptr;
         hipEvent_t ev = nullptr;
-        const uint64_t wsz = b64x_decode_workspace_size(0);
+        const uint64_t wsz = kLibWsBytes;
         hipError_t he = hipMalloc(&p, wsz);
         if (he == hipSuccess) he = hipMemsetAsync(p, 0, wsz, (hipStream_t) stream);
         if (he == hipSuccess) he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -3961,15 +3999,19 @@ static void *library_workspace(void *stream, int *slot, int *err)
     }
     *slot = v;
     *err = 0;
+    if (rows) *rows = g_ws[v].rows;
     return g_ws[v].ws;
 }
 
 // The call that pinned entry `slot` has enqueued its kernels on `stream`:
-// record the entry's last-use event behind them and unpin it.
-static void ws_unpin(int slot, void *stream)
+// record the entry's last-use event behind them and unpin it.  rows: the
+// shape of the row batch whose model and cleared bitmap the call leaves in
+// the workspace; none for any other call (its kernels use the scratch).
+static void ws_unpin(int slot, void *stream, RowsShape rows = RowsShape{})
 {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     WsEntry &e = g_ws[slot];
+    e.rows = rows;
     if (hipEventRecord(e.last, (hipStream_t) stream) == hipSuccess) e.recorded = true;
     if (--e.pins == 0 && e.release) {
         e.stream = nullptr;
@@ -4028,6 +4070,23 @@ static DecodeHint *decode_hints()
         }
     });
     return h;
+}
+
+// Per library workspace: set by k_rows_finish when the batch's first row
+// failed the model it was decoded with (pinned, coherent); allocated on
+// first use, nullptr if that fails (then every row batch probes).
+static uint32_t *rows_stale(int slot)
+{
+    static uint32_t *h = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, kWsCache * 64, hipHostMallocCoherent) == hipSuccess) {
+            memset(p, 0, kWsCache * 64);
+            h = (uint32_t *) p;
+        }
+    });
+    return h ? h + 16 * slot : nullptr;  // one 64-byte line each
 }
 
 static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
@@ -4225,21 +4284,33 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
         const uint64_t relmax = S + (uint64_t) U * kThreads;
         void *ws = nullptr;
         int slot = -1;
+        RowsShape held{};
         const uint64_t bitmap = ((uint64_t) nbuf + 63) / 64 * 8 + sizeof(RowModel);
         if (relmax * e < (1ull << 32) && (relmax / S + 1) * in_stride < (1ull << 40) &&
             bitmap <= b64x_decode_workspace_size(0) - kWsScratch &&
-            (ws = library_workspace(stream, &slot, &err))) {
+            (ws = library_workspace(stream, &slot, &err, &held))) {
             const uint64_t m64 = ~0ull / S + 1;
             const uint64_t per = (uint64_t) U * kThreads;
             const uint64_t tail_slot = (uint64_t) S * (nbuf - 1);
             const uint64_t nwords = ((uint64_t) nbuf + 63) / 64;
-            hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nwords + kThreads - 1) / kThreads,
-                                                          (uint64_t) d->cus)),
-                               dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in, (uint32_t) len,
-                               in_stride, (uint32_t) S, out_stride, a, ws);
-            if ((err = launch_status())) {
-                ws_unpin(slot, stream);
-                return err;
+            RowModel *rm = row_model_of(ws);
+            // The workspace's last call was a row batch of this shape and its
+            // first row fit the model: the model is still there and the bitmap
+            // cleared, so the probe is skipped.  Any model is exact (a row
+            // passes only by its own checks); a stale one only sends rows to
+            // the fix-up, and its first row marked renews it next time.
+            uint32_t *stale = rows_stale(slot);
+            const RowsShape key{len, in_stride, out_stride, nbuf, a.p62, a.p63};
+            if (!(held == key) || !stale || *(volatile uint32_t *) stale) {
+                if (stale) *(volatile uint32_t *) stale = 0;
+                hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nwords + kThreads - 1) / kThreads,
+                                                              (uint64_t) d->cus)),
+                                   dim3(kThreads), 0, s, nbuf, (const uint8_t *) d_in,
+                                   (uint32_t) len, in_stride, (uint32_t) S, out_stride, a, ws, rm);
+                if ((err = launch_status())) {
+                    ws_unpin(slot, stream);
+                    return err;
+                }
             }
             // + S blocks: the row-group mapping rounds the rows up to whole
             // bands of U Ru rows (NB <= S blocks each); spare blocks return
@@ -4251,7 +4322,8 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             hipLaunchKernelGGL((o32 ? k_decode_rows_lines<U, true> : k_decode_rows_lines<U, false>),
                                g, dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, in_stride, (uint32_t) len, (uint8_t *) d_out,
-                               out_stride, (uint32_t) S, magic, m64, slots, tail_slot, a, nbuf, ws);
+                               out_stride, (uint32_t) S, magic, m64, slots, tail_slot, a, nbuf, ws,
+                               (const RowModel *) rm);
             if ((err = launch_status())) {
                 ws_unpin(slot, stream);
                 return err;
@@ -4259,9 +4331,10 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             const uint32_t fg = cap_grid(((uint64_t) nbuf + 64 * kWavesPerBlock - 1) /
                                          (64 * kWavesPerBlock), (uint64_t) d->cus * 8);
             hipLaunchKernelGGL(k_rows_finish, dim3(fg), dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a, ws);
+                               (const uint8_t *) d_in, (uint8_t *) d_out, L, nbuf, d_outlen, a, ws,
+                               (const RowModel *) rm, stale);
             err = launch_status();
-            ws_unpin(slot, stream);
+            ws_unpin(slot, stream, err ? RowsShape{} : key);
             return err;
         } else if (err) {
             return err;

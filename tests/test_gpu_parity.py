@@ -901,6 +901,54 @@ def test_strided_mime_rows_bands_vs_oracle(n, L, sep, nbuf):
             assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (cap, i)
 
 
+def test_strided_rows_model_reuse_across_batches():
+    """Row batches of one shape on one stream reuse the workspace's model
+    (k_rows_prep runs only when the shape changes, another call used the
+    workspace, or the last batch's first row failed the model): batches
+    whose format changes under a held model, a first row that fails, a
+    contiguous decode in between and another alphabet all stay exact."""
+    rng = np.random.default_rng(77)
+    nbuf, n = 900, 1024
+    fmts = {"crlf76": (76, b"\r\n"), "lf64": (64, b"\n"), "clean": (0, b"")}
+
+    def batch(fmt, deviants=()):
+        L, sep = fmts[fmt]
+        if L:
+            return _mime_batch(nbuf, n, L, sep, rng, deviants=dict(deviants))
+        return [orc.encode(rng.integers(0, 256, n, dtype=np.uint8)) for _ in range(nbuf)]
+
+    stride = 1404 + 36  # room for every format's rows, padded with LF
+    dcap = b64.decoded_cap(stride)
+    cap = (dcap + 11) // 12 * 12
+
+    def run(rows, abc=None):
+        assert max(len(r) for r in rows) <= stride
+        flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
+        x = dev(flat)
+        size = (nbuf - 1) * cap + dcap
+        dec = torch.full((size + 64,), 0xA5, dtype=torch.uint8, device=DEV)
+        outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+        b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen, abc=abc)
+        ol = outlen.cpu().tolist()
+        dh = dec.cpu().numpy()
+        assert (dh[size:] == 0xA5).all()
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)), *(abc or ()))
+            assert ol[i] == len(want), i
+            assert dh[i * cap:i * cap + ol[i]].tobytes() == want, i
+
+    for step in ("crlf76", "crlf76", "lf64", "lf64", "crlf76", "clean", "clean", "crlf76"):
+        run(batch(step, deviants={7: "junk"}))
+    run(batch("crlf76", deviants={0: "junk", 9: "len"}))  # first row fails the model
+    run(batch("crlf76"))
+    z = dev(orc.encode(rng.integers(0, 256, 1 << 20, dtype=np.uint8)))
+    b64.decode(z)  # another call on the stream's workspace
+    run(batch("crlf76", deviants={nbuf - 1: "junk"}))
+    rows = [r.replace(b"+", b"-").replace(b"/", b"_") for r in batch("crlf76")]
+    run(rows, abc=("-", "_"))
+    run(batch("crlf76"))
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
