@@ -851,7 +851,9 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //           cleared by k_decode_suffix): the idle suffix kernel's one
 //           scalar load instead of a wave reading all 64 words per block
 //   model   the line model k_decode_probe found, for k_decode_lines and
-//           k_decode_suffix
+//           k_decode_suffix; model_n the length of the stream it was made for:
+//           a call of the same length may reuse it without a probe
+//           (decode_dev_ws), and k_decode_lines checks that it does
 //   fticket, fstatus, fsuper, wdone  k_decode_suffix's tile ticket, tile
 //           counts, group sums and count of blocks that have left
 //   sfx_start  where the last call's k_decode_suffix<false> started (its
@@ -878,6 +880,7 @@ struct DecodeWs {
     uint64_t *fail_any;  // nonzero: some failure word was published (own line)
     uint32_t *wdone;     // k_decode_suffix: blocks that have left (own line; zero between calls)
     LineModel *model;    // k_decode_lines' model, for k_decode_suffix
+    uint64_t *model_n;   // the stream length the model was probed for (0: none yet)
     uint64_t *fd;
     uint64_t *fd_cur;
     uint32_t *ticket;
@@ -898,7 +901,8 @@ constexpr uint32_t kFusePer = 8;
 constexpr uint32_t kFuseLoad = 4;  // of them loaded at once for counting
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
-constexpr uint64_t kWsStatus = 64;                                        // scan tile status
+constexpr uint64_t kWsModelN = 64;                                        // the model's stream length
+constexpr uint64_t kWsStatus = 128;                                       // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
 constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix: tiles per group sum
 constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
@@ -915,8 +919,8 @@ constexpr uint64_t ws_bytes_for(uint64_t nr)
 }
 
 // Layout: 64-byte header (fd, fd_cur, ticket, fticket, sfx_start, model), the
-// zero-between-calls regions at fixed offsets, then the scratch counts and
-// bases of `nranges` ranges.
+// model's stream length (its own 64 bytes), the zero-between-calls regions at
+// fixed offsets, then the scratch counts and bases of `nranges` ranges.
 DEV DecodeWs ws_view(void *ws, uint32_t nranges)
 {
     DecodeWs w;
@@ -927,6 +931,7 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
     w.fticket = (uint32_t *) (p + 20);
     w.sfx_start = (uint64_t *) (p + 24);
     w.model = (LineModel *) (p + 32);
+    w.model_n = (uint64_t *) (p + kWsModelN);
     w.status = (uint64_t *) (p + kWsStatus);
     w.fstatus = (uint64_t *) (p + kWsFStatus);
     w.fsuper = (uint64_t *) (p + kWsFSuper);
@@ -1913,6 +1918,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
         *ws_view(ws, nranges).fail_any = 1;
     }
     *ws_view(ws, nranges).model = mo;
+    *ws_view(ws, nranges).model_n = n;
     if (hint) {
         volatile DecodeHint *h = hint;
         h->junky = mo.skip && 256 * (uint64_t) mo.T < n ? 1u : 0u;  // 16 T < n / 16
@@ -1937,24 +1943,30 @@ void k_decode_lines(
     const uint64_t *mp = (const uint64_t *) ws_view(ws, nranges).model;
     const uint64_t mw0 = scalar_load_u64(mp), mw1 = scalar_load_u64(mp + 1),
                    mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
+    const uint64_t mn = scalar_load_u64(ws_view(ws, nranges).model_n);
     build_dec_table(tab, a);
+    // A model made for another length (a reused workspace whose last probe
+    // was not this stream's): no slot is taken, slot 0 is published as
+    // failing and k_decode_suffix decodes the whole stream exactly.
+    const bool mok = mn == n;
+    const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : 0u;
     // a block wholly past slot T (the probe cut the model's slots at junk)
     // leaves before the barrier: on junk-laden input nearly every block of
     // this launch does.  (Tested before the table build, the model's load
     // no longer overlapped the build: MIME text +2 %.)
-    if (blockIdx.x * kLinesWaves * kLinesSlots > (uint32_t) (mw1 >> 32)) return;
+    if (blockIdx.x * kLinesWaves * kLinesSlots > T) return;
     __syncthreads();
     LineModel m;
-    m.L = (uint32_t) mw0;
+    m.L = mok ? (uint32_t) mw0 : 0u;
     m.s = (uint32_t) (mw0 >> 32);
     m.P = (uint32_t) mw1;
-    m.T = (uint32_t) (mw1 >> 32);
+    m.T = T;
     m.m = (uint32_t) mw2;
     m.k = (uint32_t) (mw2 >> 32);
     m.rcp = (uint32_t) mw3;
-    m.skip = (uint32_t) (mw3 >> 32);
+    m.skip = mok ? (uint32_t) (mw3 >> 32) : 1u;
     const uint32_t lane = lane_id();
-    const uint32_t L = m.L, s = m.s, P = m.P, T = m.T;
+    const uint32_t L = m.L, s = m.s, P = m.P;
     // the wave's first slot, made visibly wave-uniform: its line coordinates
     // and output address are then scalar (a vector t0 cost a 64-bit
     // multiply-add per slot store and a 32-bit multiply per wave)
@@ -2086,10 +2098,15 @@ void k_decode_lines(
             }
         }
     }
-    if (fail_u < kLinesU && lane == 0) {
+    // Under a cut model (skip) the wave that owns slot T publishes it as
+    // failing unless one of its slots failed first: the probe has done so
+    // when it ran, and a call that reused the model has no probe.
+    const bool cut = m.skip && T < t0 + kLinesSlots;
+    if ((fail_u < kLinesU || cut) && lane == 0) {
         // publish the first failing slot; only an improvement (the
         // device-scope load sees what earlier waves published)
-        const unsigned long long key = ~(unsigned long long) (t0 + fail_u * 64 + fail_lane);
+        const unsigned long long key =
+            ~(unsigned long long) (fail_u < kLinesU ? t0 + fail_u * 64 + fail_lane : T);
         unsigned long long *lf = (unsigned long long *) ws_view(ws, nranges).lfail +
                                  (blockIdx.x % kFailWords) * kFailStride;
         const unsigned long long cur =
@@ -2381,9 +2398,11 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 
 // The idle test of k_decode_suffix<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
-// done); else S, Vb of the first failing slot.  Every block.
+// done); else S, Vb of the first failing slot, and *reprobe (pinned, the
+// launcher's: the next call of this length on the workspace probes again
+// instead of reusing the model) is set.  Every block.
 DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, uint64_t &S,
-                      uint64_t &Vb)
+                      uint64_t &Vb, uint32_t *reprobe)
 {
     __shared__ uint64_t s_key;
     uint64_t key = 0;
@@ -2416,7 +2435,8 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
         return false;
     }
     Vb = 16 * ~key;  // the first failing slot of k_decode_lines
-    S = line_pos(*w.model, Vb);
+    S = line_pos(*w.model, Vb);  // (slot 0 under a model of another length: 0)
+    if (reprobe && blockIdx.x == 0 && threadIdx.x == 0) *(volatile uint32_t *) reprobe = 1u;
     return true;
 }
 
@@ -2425,12 +2445,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_suffix(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
-    uint32_t seq)
+    uint32_t seq, uint32_t *reprobe)
 {
     constexpr uint64_t R = 2 * kChunk;
     DecodeWs w = ws_view(ws, nranges);
     uint64_t S = 0, Vb = 0;
-    if (!WHOLE && !suffix_start(w, res, hres, S, Vb)) return;
+    if (!WHOLE && !suffix_start(w, res, hres, S, Vb, reprobe)) return;
     uint8_t *base_out = out + Vb / 4 * 3;
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
@@ -4089,6 +4109,41 @@ static uint32_t *rows_stale(int slot)
     return h ? h + 16 * slot : nullptr;  // one 64-byte line each
 }
 
+// Workspaces whose line model (k_decode_probe's, kept in the workspace with
+// the length it was made for) a call of the same length may reuse without a
+// probe: one entry per hash of the workspace, and a pinned flag beside it
+// that k_decode_suffix<false> raises when a call found anything to decode
+// past k_decode_lines (junk, another format, a cut model), so that the next
+// call probes again.  A wrong entry or a late flag only costs speed: any
+// model gives exact output, and k_decode_lines checks the model's length.
+struct HeldModel {
+    const void *ws;
+    uint64_t n;
+};
+constexpr int kHeldModels = 64;
+std::mutex g_held_mu;
+HeldModel g_held[kHeldModels];
+
+static uint32_t *held_reprobe(int slot)
+{
+    static uint32_t *h = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, kHeldModels * 64, hipHostMallocCoherent) == hipSuccess) {
+            memset(p, 0, kHeldModels * 64);
+            h = (uint32_t *) p;
+        }
+    });
+    return h ? h + 16 * slot : nullptr;  // one 64-byte line each
+}
+
+static int held_slot(const void *ws)
+{
+    const uint64_t x = (uintptr_t) ws * 0x9E3779B97F4A7C15ull;
+    return (int) (x >> 58);  // 64 entries
+}
+
 static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
 {
     uint64_t x = (uintptr_t) ws * 0x9E3779B97F4A7C15ull ^ (uintptr_t) in * 0xC2B2AE3D27D4EB4Full ^
@@ -4120,7 +4175,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         if (flags & B64X_DEC_EXPECT_JUNK) {
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res, seq);
+                               hold, d_res, h_res, seq, nullptr);
             return launch_status();
         }
         // The probe of the last call on the same workspace, input and length
@@ -4133,13 +4188,29 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         DecodeHint *hint = hints ? hints + (key % kDecodeHints) : nullptr;
         const bool junky = hint && ((volatile DecodeHint *) hint)->key == key &&
                            ((volatile DecodeHint *) hint)->junky;
-        hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s, (const uint8_t *) d_in, nchars,
-                           a, ws, p.nranges, hint, key);
-        if ((err = launch_status())) return err;
+        // The workspace holds the model its last probe made for a stream of
+        // this length, and no call since found anything past
+        // k_decode_lines: the probe is skipped (HeldModel).
+        const int hs = held_slot(ws);
+        uint32_t *reprobe = held_reprobe(hs);
+        bool reuse = false;
+        if (!junky && reprobe) {
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            reuse = g_held[hs].ws == ws && g_held[hs].n == nchars &&
+                    !*(volatile uint32_t *) reprobe;
+        }
+        if (!reuse) {
+            if (reprobe) *(volatile uint32_t *) reprobe = 0;
+            hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
+                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key);
+            if ((err = launch_status())) return err;
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            g_held[hs] = HeldModel{ws, nchars};
+        }
         if (junky) {
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res, seq);
+                               hold, d_res, h_res, seq, nullptr);
             return launch_status();
         }
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
@@ -4149,7 +4220,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         if ((err = launch_status())) return err;
         hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                           hold, d_res, h_res, seq);
+                           hold, d_res, h_res, seq, reprobe);
         return launch_status();
     }
     // Larger inputs (ranges longer than 2,048 characters): pass 1, the scan,

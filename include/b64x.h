@@ -109,7 +109,9 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * b64x_decoded_cap(nchars)); *d_res (device memory) receives the result.
  * d_workspace: b64x_decode_workspace_size(nchars) bytes of device memory,
  * zero-filled before its first use (each call leaves it ready for the
- * next; one workspace per stream), or NULL to use a library-owned one
+ * next, holding the line model of its last probe: a call of the same length
+ * may reuse it and skip the probe; one workspace per stream), or NULL to use
+ * a library-owned one
  * per (device, stream).  The library keeps at most 8 such workspaces
  * (about 12.7 MiB of HBM each), allocated on first need and never freed: a
  * call on a stream without one takes an idle one (its stream made to wait

@@ -792,6 +792,76 @@ def test_repeat_junk_decode_takes_the_hinted_single_pass():
     assert starts[3] == starts[0] and starts[4] == 2**64 - 1
 
 
+def test_held_model_reused_across_calls_of_one_length():
+    """Calls of one length on one workspace reuse the model its last probe
+    made (no probe) until a call finds anything past k_decode_lines; the
+    data under a held model changes format, gains junk, loses it again, and
+    the workspace is zeroed under a held entry (k_decode_lines then finds a
+    model of another length and leaves the whole stream to the suffix):
+    every call exact, on a caller's workspace and on the library's."""
+    rng = np.random.default_rng(53)
+    n = 3_000_001
+    clean = orc.encode(rng.integers(0, 256, n, dtype=np.uint8))
+    size = len(clean)
+
+    def fit(t):
+        return (t + clean)[:size]
+
+    texts = {
+        "clean": clean,
+        "clean2": orc.encode(rng.integers(0, 256, n, dtype=np.uint8)),
+        "crlf76": fit(_wrap(orc.encode(rng.integers(0, 256, n, dtype=np.uint8)), 76, b"\r\n")),
+        "lf64": fit(_wrap(orc.encode(rng.integers(0, 256, n, dtype=np.uint8)), 64, b"\n")),
+        "junk": fit(_junk(rng, clean, 0.05)),
+        "sparse": fit(clean[:8192] + _junk(rng, clean[8192:], 1e-3)),
+        "tail": clean[:-100] + b"!" + clean[-99:],
+        "alljunk": b"\n" * size,
+    }
+    order = ["clean", "clean2", "clean", "crlf76", "crlf76", "lf64", "clean", "junk", "clean",
+             "clean2", "sparse", "clean", "tail", "clean", "alljunk", "clean", "clean2"]
+    buf = torch.empty(size, dtype=torch.uint8, device=DEV)
+    out = torch.empty(b64.decoded_cap(size) + 8, dtype=torch.uint8, device=DEV)
+    for ws in (torch.zeros(b64.workspace_size(size), dtype=torch.uint8, device=DEV), None):
+        for i, name in enumerate(order):
+            text = texts[name]
+            assert len(text) == size
+            buf.copy_(dev(text))
+            d = b64.decode(buf, out=out, workspace=ws)
+            assert d.bytes().cpu().numpy().tobytes() == orc.decode(text), (i, name)
+            if ws is not None and name == "clean2" and i > 2:
+                ws.zero_()  # a held entry over a zeroed workspace
+        # back-to-back calls with no sync between them (the flag a call's
+        # suffix raises may land after the next call was issued)
+        outs = []
+        for name in ("clean", "junk", "clean", "crlf76", "clean"):
+            o = torch.empty_like(out)
+            b = dev(texts[name])
+            outs.append((name, b, o, b64.decode(b, out=o, workspace=ws)))
+        for name, _, o, d in outs:
+            assert d.bytes().cpu().numpy().tobytes() == orc.decode(texts[name]), name
+
+
+def test_held_model_tiny_and_hold_tail():
+    """Short streams (under one slot) and HOLD_TAIL calls of one length on
+    one workspace, content changing between calls."""
+    rng = np.random.default_rng(59)
+    tab = orc.decode_table()
+    ws = torch.zeros(b64.workspace_size(1 << 16), dtype=torch.uint8, device=DEV)
+    for size in (5, 15, 16, 17, 100, 4099):
+        for k in range(6):
+            raw = orc.encode(rng.integers(0, 256, size, dtype=np.uint8))[:size]
+            text = raw if k % 3 else bytes(b if rng.random() > 0.2 else 0x0A for b in raw)
+            out = torch.empty(b64.decoded_cap(size) + 8, dtype=torch.uint8, device=DEV)
+            d = b64.decode(dev(text), out=out, workspace=ws, hold_tail=bool(k & 1))
+            want = orc.decode(text)
+            got = d.bytes().cpu().numpy().tobytes()
+            if k & 1:  # whole groups only
+                V = sum(1 for c in text if tab[c] >= 0)
+                assert got == want[:V // 4 * 3], (size, k)
+            else:
+                assert got == want, (size, k)
+
+
 def _probe_model(ws: torch.Tensor):
     """The line model k_decode_probe left in the workspace (header bytes
     32..63): (L, s, T, skip)."""
