@@ -107,3 +107,87 @@ def test_rows_fuzz_vs_oracle(seed):
         want = orc.decode(r + b"\n" * (stride - len(r)))
         assert ol[i] == len(want), (seed, i)
         assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (seed, i)
+
+
+def _fit(text: bytes, size: int, rng) -> bytes:
+    """text cut or extended (with clean characters) to exactly size bytes."""
+    if len(text) >= size:
+        return text[:size]
+    pad = orc.encode(rng.integers(0, 256, size, dtype=np.uint8).tobytes())
+    return (text + pad)[:size]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_reuse_fuzz_interleaved(seed):
+    """Calls that reuse models: single-buffer decodes drawn from three
+    lengths (so the held model is taken whenever the last call of that
+    length found nothing past k_decode_lines) with the content kind, the
+    alphabet and HOLD_TAIL changing between calls, on the stream's library
+    workspace or a caller's, interleaved with row batches of two shapes on
+    the same stream (which keep their own model in the library workspace),
+    some calls issued back to back without a sync.  Every result exact."""
+    rng = np.random.default_rng(5000 + seed)
+    sizes = [int(rng.integers(20, 64)), int(rng.integers(3000, 5000)),
+             int(rng.integers(150_000, 400_000))]
+    ws = torch.zeros(b64.workspace_size(max(sizes)), dtype=torch.uint8, device=DEV)
+    pending = []
+
+    def check(p):
+        kind, args = p[0], p[1:]
+        if kind == "one":
+            text, abc, hold, d = args
+            want = orc.decode(text, abc[0], abc[1])
+            info = d.info()
+            got = d.bytes().cpu().numpy().tobytes()
+            if hold:
+                assert got == want[:info.out_len] and info.out_len == info.valid // 4 * 3
+            else:
+                assert got == want, (seed, len(text))
+        else:
+            rows, stride, cap, out, outlen = args
+            ol = outlen.cpu().tolist()
+            dh = out.cpu().numpy()
+            for i, r in enumerate(rows):
+                want = orc.decode(r)
+                assert ol[i] == len(want), (seed, i)
+                assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (seed, i)
+
+    for _ in range(90):
+        if rng.random() < 0.2:
+            # a row batch: 200 rows of one of two shapes, CRLF-76 or clean,
+            # a few deviant rows
+            L = int(rng.choice([700, 1024]))
+            raws = [orc.encode(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+                    for _ in range(200)]
+            if rng.integers(2):
+                raws = [b"\r\n".join(r[i:i + 76] for i in range(0, len(r), 76)) + b"\r\n"
+                        for r in raws]
+            for k in rng.integers(0, 200, int(rng.integers(0, 3))):
+                raws[k] = raws[k][:5] + b"\t" + raws[k][6:]
+            stride = max(len(r) for r in raws) + 4
+            rows = [r + b"\n" * (stride - len(r)) for r in raws]
+            cap = (b64.decoded_cap(stride) + 11) // 12 * 12
+            out = torch.empty(200 * cap, dtype=torch.uint8, device=DEV)
+            outlen = torch.zeros(200, dtype=torch.int64, device=DEV)
+            x = torch.from_numpy(np.frombuffer(b"".join(rows), np.uint8).copy()).to(DEV)
+            b64.decode_strided(x, stride, stride, 200, out, cap, outlen)
+            pending.append(("rows", rows, stride, cap, out, outlen))
+        else:
+            size = sizes[int(rng.integers(3))]
+            text, abc = _text(rng)
+            if rng.random() < 0.5:
+                abc = (-1, -1)
+                text = orc.encode(rng.integers(0, 256, size, dtype=np.uint8).tobytes())
+            text = _fit(text, size, rng)
+            hold = bool(rng.integers(4) == 0)
+            x = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).to(DEV)
+            out = torch.empty(b64.decoded_cap(size) + 4, dtype=torch.uint8, device=DEV)
+            d = b64.decode(x, out=out, abc=(abc[0], abc[1], True, -1), hold_tail=hold,
+                           workspace=ws if rng.integers(2) else None)
+            pending.append(("one", text, abc, hold, d))
+        if rng.random() < 0.6:  # otherwise leave it in flight behind the next call
+            for p in pending:
+                check(p)
+            pending.clear()
+    for p in pending:
+        check(p)
