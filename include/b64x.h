@@ -29,7 +29,10 @@
  * All device pointers are HIP device (or host-pinned-mapped) pointers.
  * `stream` is a hipStream_t passed as void * (NULL = the null stream).
  * Device-side launches are asynchronous and capture-safe (no allocation
- * or synchronisation inside) unless the comment says otherwise.
+ * or synchronisation inside) unless the comment says otherwise.  Where a
+ * call picks its kernels from what earlier calls saw (a held line model, a
+ * junk hint), a captured graph replays the pick made at capture; results
+ * are exact either way, only the speed differs.
  */
 #ifndef ASYNC_AMD_B64X_H
 #define ASYNC_AMD_B64X_H
