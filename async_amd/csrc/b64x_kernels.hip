@@ -2932,6 +2932,12 @@ struct RowModel {
     uint32_t rg;            // 1: the mapping applies
 };
 static_assert(sizeof(RowModel) == 96, "RowModel layout");
+// The batch shape a RowModel was made for, stored right after it: the row
+// kernel checks it against its own arguments before it trusts the model's
+// geometry (a graph replayed after another shape's prep on the workspace).
+struct RowShape {
+    uint64_t len, in_stride, out_stride, nbuf;
+};
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the rows' failure bitmap in the
@@ -3080,7 +3086,10 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
                (uint64_t) kRowsU * r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
                out_stride < (1u << 24);
     }
-    if (threadIdx.x == 0) *rmodel = r;
+    if (threadIdx.x == 0) {
+        *rmodel = r;
+        *(RowShape *) (rmodel + 1) = RowShape{len, in_stride, out_stride, nbuf};
+    }
 }
 
 // The row kernel.  Clean rows (the model's L = 0): the block's first slot
@@ -3124,6 +3133,17 @@ void k_decode_rows_lines(
     const uint64_t *rmw = (const uint64_t *) rmodel;
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
+    const uint64_t *shw = (const uint64_t *) (rmodel + 1);
+    if (scalar_load_u64(shw) != len || scalar_load_u64(shw + 1) != in_stride ||
+        scalar_load_u64(shw + 2) != out_stride || scalar_load_u64(shw + 3) != nbuf) {
+        // a model made for another shape: no slot is taken, every row is
+        // marked for k_rows_finish's exact decode
+        const uint64_t nw = ((uint64_t) nbuf + 63) / 64;
+        const uint64_t wi = (uint64_t) blockIdx.x * kThreads + threadIdx.x;
+        if (wi < nw)
+            bm[wi] = wi + 1 < nw || (nbuf & 63) == 0 ? ~0ull : (1ull << (nbuf & 63)) - 1;
+        return;
+    }
     // (the row bands' spare blocks leave after the table build: tested
     // before it, the model's loads no longer overlapped the build and MIME
     // rows ran 481.6 -> 499.2 us, profiles/r04_ab_rows_early_exit.jsonl)

@@ -1019,6 +1019,51 @@ def test_strided_rows_model_reuse_across_batches():
     run(batch("crlf76"))
 
 
+def test_strided_rows_graph_replay_after_another_shape():
+    """A row batch captured in a HIP graph while its workspace held the
+    model of its shape (no prep captured), replayed after a batch of
+    another shape re-probed that workspace: the row kernel finds the model
+    made for another shape, takes no slot, and the exact fix-up decodes
+    every row."""
+    rng = np.random.default_rng(81)
+    s = torch.cuda.Stream()
+
+    def batch(n, nbuf):
+        rows = _mime_batch(nbuf, n, 76, b"\r\n", rng)
+        stride = max(len(r) for r in rows)
+        flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
+        cap = (b64.decoded_cap(stride) + 11) // 12 * 12
+        out = torch.zeros(nbuf * cap, dtype=torch.uint8, device=DEV)
+        ol = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+        return rows, stride, dev(flat), cap, out, ol
+
+    def check(rows, stride, cap, out, ol):
+        olh = ol.cpu().tolist()
+        dh = out.cpu().numpy()
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)))
+            assert olh[i] == len(want), i
+            assert dh[i * cap:i * cap + olh[i]].tobytes() == want, i
+
+    rows, stride, x, cap, out, ol = batch(1024, 500)
+    rows2, stride2, x2, cap2, out2, ol2 = batch(700, 300)
+    with torch.cuda.stream(s):
+        for _ in range(2):  # the stream's workspace, holding this shape's model
+            b64.decode_strided(x, stride, stride, 500, out, cap, ol, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            b64.decode_strided(x, stride, stride, 500, out, cap, ol, stream=s)
+        # another shape on the same stream's workspace replaces the model
+        b64.decode_strided(x2, stride2, stride2, 300, out2, cap2, ol2, stream=s)
+        out.zero_()
+        ol.zero_()
+        g.replay()
+    s.synchronize()
+    check(rows, stride, cap, out, ol)
+    check(rows2, stride2, cap2, out2, ol2)
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
