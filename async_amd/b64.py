@@ -124,13 +124,15 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
         raise ValueError("output too small")
     if result is None:
         result = torch.zeros(RES_BYTES, dtype=torch.uint8, device=x.device)
-    if workspace is None:  # must start zeroed; the library keeps it re-armed
-        workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
+    # workspace: a caller's (zeroed before its first use; the library keeps
+    # it re-armed), else the library's own for the stream (NULL), which also
+    # keeps the line model of its last probe for the next call of a length
     flags = (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0)
     seq = ctypes.c_uint32(0)
     _lib.check("b64x_decode_dev_seq", lib.b64x_decode_dev_seq(
         _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a), flags,
-        _ptr(workspace), _stream(stream), ctypes.byref(seq)))
+        _ptr(workspace) if workspace is not None else None, _stream(stream),
+        ctypes.byref(seq)))
     return Decoded(out, result, n, flags & HOLD_TAIL, seq.value,
                    stream if stream is not None else torch.cuda.current_stream())
 

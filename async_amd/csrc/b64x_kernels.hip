@@ -1945,11 +1945,13 @@ void k_decode_lines(
                    mw2 = scalar_load_u64(mp + 2), mw3 = scalar_load_u64(mp + 3);
     const uint64_t mn = scalar_load_u64(ws_view(ws, nranges).model_n);
     build_dec_table(tab, a);
-    // A model made for another length (a reused workspace whose last probe
-    // was not this stream's): no slot is taken, slot 0 is published as
-    // failing and k_decode_suffix decodes the whole stream exactly.
+    // A model made for another length (a workspace whose last probe was not
+    // for this length, or a fresh one at a reused address): the clean model
+    // of this length instead (L = 0, every slot, no cut) -- exact like any
+    // model; clean input keeps the fast path and anything else fails a slot
+    // and goes to k_decode_suffix (which then asks for a probe).
     const bool mok = mn == n;
-    const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : 0u;
+    const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : (uint32_t) n / 16u;
     // a block wholly past slot T (the probe cut the model's slots at junk)
     // leaves before the barrier: on junk-laden input nearly every block of
     // this launch does.  (Tested before the table build, the model's load
@@ -1964,7 +1966,7 @@ void k_decode_lines(
     m.m = (uint32_t) mw2;
     m.k = (uint32_t) (mw2 >> 32);
     m.rcp = (uint32_t) mw3;
-    m.skip = mok ? (uint32_t) (mw3 >> 32) : 1u;
+    m.skip = mok ? (uint32_t) (mw3 >> 32) : 0u;
     const uint32_t lane = lane_id();
     const uint32_t L = m.L, s = m.s, P = m.P;
     // the wave's first slot, made visibly wave-uniform: its line coordinates
@@ -2401,8 +2403,8 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // done); else S, Vb of the first failing slot, and *reprobe (pinned, the
 // launcher's: the next call of this length on the workspace probes again
 // instead of reusing the model) is set.  Every block.
-DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, uint64_t &S,
-                      uint64_t &Vb, uint32_t *reprobe)
+DEV bool suffix_start(DecodeWs w, uint64_t n, b64x_dec_result *res, b64x_dec_result *hres,
+                      uint64_t &S, uint64_t &Vb, uint32_t *reprobe)
 {
     __shared__ uint64_t s_key;
     uint64_t key = 0;
@@ -2435,7 +2437,9 @@ DEV bool suffix_start(DecodeWs w, b64x_dec_result *res, b64x_dec_result *hres, u
         return false;
     }
     Vb = 16 * ~key;  // the first failing slot of k_decode_lines
-    S = line_pos(*w.model, Vb);  // (slot 0 under a model of another length: 0)
+    // under the model k_decode_lines used: the workspace's, or the clean
+    // model when the workspace's was made for another length
+    S = scalar_load_u64(w.model_n) == n ? line_pos(*w.model, Vb) : Vb;
     if (reprobe && blockIdx.x == 0 && threadIdx.x == 0) *(volatile uint32_t *) reprobe = 1u;
     return true;
 }
@@ -2450,7 +2454,7 @@ void k_decode_suffix(
     constexpr uint64_t R = 2 * kChunk;
     DecodeWs w = ws_view(ws, nranges);
     uint64_t S = 0, Vb = 0;
-    if (!WHOLE && !suffix_start(w, res, hres, S, Vb, reprobe)) return;
+    if (!WHOLE && !suffix_start(w, n, res, hres, S, Vb, reprobe)) return;
     uint8_t *base_out = out + Vb / 4 * 3;
     const uint32_t r0 = (uint32_t) (S / R);
     const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
@@ -2932,12 +2936,6 @@ struct RowModel {
     uint32_t rg;            // 1: the mapping applies
 };
 static_assert(sizeof(RowModel) == 96, "RowModel layout");
-// The batch shape a RowModel was made for, stored right after it: the row
-// kernel checks it against its own arguments before it trusts the model's
-// geometry (a graph replayed after another shape's prep on the workspace).
-struct RowShape {
-    uint64_t len, in_stride, out_stride, nbuf;
-};
 constexpr uint32_t kNoRowShape = 0xFFFFFFFFu;
 
 // The library workspace of the stream holds the rows' failure bitmap in the
@@ -3086,10 +3084,7 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
                (uint64_t) kRowsU * r.ru * out_stride < (1ull << 31) && in_stride < (1u << 24) &&
                out_stride < (1u << 24);
     }
-    if (threadIdx.x == 0) {
-        *rmodel = r;
-        *(RowShape *) (rmodel + 1) = RowShape{len, in_stride, out_stride, nbuf};
-    }
+    if (threadIdx.x == 0) *rmodel = r;
 }
 
 // The row kernel.  Clean rows (the model's L = 0): the block's first slot
@@ -3133,17 +3128,6 @@ void k_decode_rows_lines(
     const uint64_t *rmw = (const uint64_t *) rmodel;
     const uint64_t r0 = scalar_load_u64(rmw), r6 = scalar_load_u64(rmw + 6);
     unsigned long long *bm = row_fail(ws);
-    const uint64_t *shw = (const uint64_t *) (rmodel + 1);
-    if (scalar_load_u64(shw) != len || scalar_load_u64(shw + 1) != in_stride ||
-        scalar_load_u64(shw + 2) != out_stride || scalar_load_u64(shw + 3) != nbuf) {
-        // a model made for another shape: no slot is taken, every row is
-        // marked for k_rows_finish's exact decode
-        const uint64_t nw = ((uint64_t) nbuf + 63) / 64;
-        const uint64_t wi = (uint64_t) blockIdx.x * kThreads + threadIdx.x;
-        if (wi < nw)
-            bm[wi] = wi + 1 < nw || (nbuf & 63) == 0 ? ~0ull : (1ull << (nbuf & 63)) - 1;
-        return;
-    }
     // (the row bands' spare blocks leave after the table build: tested
     // before it, the model's loads no longer overlapped the build and MIME
     // rows ran 481.6 -> 499.2 us, profiles/r04_ab_rows_early_exit.jsonl)
@@ -4164,6 +4148,16 @@ static int held_slot(const void *ws)
     return (int) (x >> 58);  // 64 entries
 }
 
+// A call being captured into a graph never reuses what earlier calls left
+// (a held model): the graph replays later, after other calls may have
+// replaced it, so the capture records the probe or prep as well.
+static bool capturing(void *stream)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing((hipStream_t) stream, &st) == hipSuccess &&
+           st != hipStreamCaptureStatusNone;
+}
+
 static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
 {
     uint64_t x = (uintptr_t) ws * 0x9E3779B97F4A7C15ull ^ (uintptr_t) in * 0xC2B2AE3D27D4EB4Full ^
@@ -4214,7 +4208,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         const int hs = held_slot(ws);
         uint32_t *reprobe = held_reprobe(hs);
         bool reuse = false;
-        if (!junky && reprobe) {
+        if (!junky && reprobe && !capturing(stream)) {
             std::lock_guard<std::mutex> lk(g_held_mu);
             reuse = g_held[hs].ws == ws && g_held[hs].n == nchars &&
                     !*(volatile uint32_t *) reprobe;
@@ -4392,7 +4386,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             // the fix-up, and its first row marked renews it next time.
             uint32_t *stale = rows_stale(slot);
             const RowsShape key{len, in_stride, out_stride, nbuf, a.p62, a.p63};
-            if (!(held == key) || !stale || *(volatile uint32_t *) stale) {
+            if (!(held == key) || !stale || *(volatile uint32_t *) stale || capturing(stream)) {
                 if (stale) *(volatile uint32_t *) stale = 0;
                 hipLaunchKernelGGL(k_rows_prep, dim3(cap_grid((nwords + kThreads - 1) / kThreads,
                                                               (uint64_t) d->cus)),

@@ -29,10 +29,10 @@
  * All device pointers are HIP device (or host-pinned-mapped) pointers.
  * `stream` is a hipStream_t passed as void * (NULL = the null stream).
  * Device-side launches are asynchronous and capture-safe (no allocation
- * or synchronisation inside) unless the comment says otherwise.  Where a
- * call picks its kernels from what earlier calls saw (a held line model, a
- * junk hint), a captured graph replays the pick made at capture; results
- * are exact either way, only the speed differs.
+ * or synchronisation inside) unless the comment says otherwise.  A call
+ * being captured into a graph does not reuse a line model held from earlier
+ * calls (it captures the probe or prep too); the junk hint's pick of path is
+ * replayed as made at capture -- exact either way, only the speed differs.
  */
 #ifndef ASYNC_AMD_B64X_H
 #define ASYNC_AMD_B64X_H

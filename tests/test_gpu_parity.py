@@ -1064,6 +1064,35 @@ def test_strided_rows_graph_replay_after_another_shape():
     check(rows2, stride2, cap2, out2, ol2)
 
 
+def test_decode_graph_replay_after_other_lengths():
+    """A decode captured in a HIP graph (after calls of its length left a
+    held model, which a capture does not reuse), replayed after decodes of
+    other lengths and other content on the same workspace: exact."""
+    rng = np.random.default_rng(83)
+    s = torch.cuda.Stream()
+    text = _wrap(orc.encode(rng.integers(0, 256, 1_000_000, dtype=np.uint8)), 76, b"\r\n")
+    other = orc.encode(rng.integers(0, 256, 700_000, dtype=np.uint8))
+    ws = torch.zeros(b64.workspace_size(len(text)), dtype=torch.uint8, device=DEV)
+    x, y = dev(text), dev(other)
+    out = torch.zeros(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+    out2 = torch.zeros(b64.decoded_cap(len(other)) + 8, dtype=torch.uint8, device=DEV)
+    res = torch.zeros(256, dtype=torch.uint8, device=DEV)
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            d = b64.decode(x, out=out, workspace=ws, result=res, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            b64.decode(x, out=out, workspace=ws, result=res, stream=s)
+        d2 = b64.decode(y, out=out2, workspace=ws, stream=s)
+        assert d2.bytes().cpu().numpy().tobytes() == orc.decode(other)
+        out.zero_()
+        g.replay()
+    s.synchronize()
+    want = orc.decode(text)
+    assert out[:len(want)].cpu().numpy().tobytes() == want
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
