@@ -1,5 +1,5 @@
-"""More seeds of tests/test_decode_fuzz.py::test_reuse_fuzz_interleaved and
-test_decode_fuzz_vs_oracle than the suite runs (GPU box):
+"""More seeds of tests/test_decode_fuzz.py's reuse fuzz (single buffers and
+row batches) and its plain decode and row fuzz than the suite runs (GPU box):
     python scripts/fuzz_reuse_more.py FIRST COUNT"""
 import os
 import sys
@@ -17,6 +17,8 @@ def main():
     for seed in range(first, first + count):
         f.test_reuse_fuzz_interleaved(seed)
         f.test_decode_fuzz_vs_oracle(seed)
+        f.test_rows_reuse_fuzz(seed)
+        f.test_rows_fuzz_vs_oracle(seed)
         print(f"seed {seed} ok ({time.time() - t0:.0f} s)", flush=True)
     print("ALL OK", flush=True)
 

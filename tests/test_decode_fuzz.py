@@ -109,6 +109,42 @@ def test_rows_fuzz_vs_oracle(seed):
         assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (seed, i)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_rows_reuse_fuzz(seed):
+    """Row batches of one shape on one stream, one after another (the
+    library workspace keeps the line model of the last batch of this shape,
+    so only a batch whose first row failed it re-probes): each batch draws
+    its own format (line length, separator, clean), deviant rows anywhere
+    including row 0; every row exact."""
+    rng = np.random.default_rng(3000 + seed)
+    nbuf = int(rng.integers(2, 300))
+    n = int(rng.integers(24, 2000))
+    stride = (n + 2) // 3 * 4 * 2 + 8  # room for any separator density below
+    cap = (b64.decoded_cap(stride) + 11) // 12 * 12
+    x = torch.empty(nbuf * stride, dtype=torch.uint8, device=DEV)
+    dec = torch.empty(nbuf * cap, dtype=torch.uint8, device=DEV)
+    outlen = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    for _ in range(12):
+        L = int(rng.choice([0, 16, 19, 64, 76, 76, 100]))
+        sep = b"".join(JUNK[rng.integers(4)] for _ in range(rng.integers(1, 5)))
+        rows = []
+        for i in range(nbuf):
+            c = orc.encode(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+            t = sep.join(c[j:j + L] for j in range(0, len(c), L)) + sep if L else c
+            if rng.random() < 0.05:
+                t = t[:5] + b"\x80" + t[5:]
+            rows.append(t[:stride])
+        flat = b"".join(r + b"\n" * (stride - len(r)) for r in rows)
+        x.copy_(torch.from_numpy(np.frombuffer(flat, dtype=np.uint8).copy()).to(DEV))
+        b64.decode_strided(x, stride, stride, nbuf, dec, cap, outlen)
+        ol = outlen.cpu().tolist()
+        dh = dec.cpu().numpy()
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)))
+            assert ol[i] == len(want), (seed, i)
+            assert dh[i * cap:i * cap + ol[i]].tobytes() == want, (seed, i)
+
+
 def _fit(text: bytes, size: int, rng) -> bytes:
     """text cut or extended (with clean characters) to exactly size bytes."""
     if len(text) >= size:
