@@ -127,6 +127,10 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
     # workspace: a caller's (zeroed before its first use; the library keeps
     # it re-armed), else the library's own for the stream (NULL), which also
     # keeps the line model of its last probe for the next call of a length
+    # Under graph capture with no workspace given, a torch-allocated one (the
+    # library will not allocate or rebind one inside a capture: -EBUSY).
+    if workspace is None and torch.cuda.is_current_stream_capturing():
+        workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
     flags = (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0)
     seq = ctypes.c_uint32(0)
     _lib.check("b64x_decode_dev_seq", lib.b64x_decode_dev_seq(

@@ -596,15 +596,28 @@ b64_hub *b64_hub_acquire(async_t *async)
     return h;
 }
 
-/* Teardown: back to the pool, with the references it held on a finished
- * batch (which nothing else holds any more: every stage is gone). */
-static void teardown_put(b64_batch *b)
+/* Teardown's batches: every one the hub still holds, collected before any
+ * goes back to the process pool (a pooled batch may be taken by another
+ * loop's hub at once, so none is read after its batch_put). */
+typedef struct {
+    b64_batch **v;
+    size_t n, cap;
+} batch_set;
+
+static void set_add(batch_set *s, b64_batch *b)
 {
-    b64_batch *a = b->after;
-    unsigned n = b->after_refs;
-    batch_put(b);
-    if (a && a->state == B_DONE && (a->refs -= n) == 0)
-        batch_put(a);
+    for (size_t i = 0; i < s->n; i++)
+        if (s->v[i] == b)
+            return;
+    if (s->n == s->cap) {
+        size_t cap = s->cap ? 2 * s->cap : 16;
+        b64_batch **v = realloc(s->v, cap * sizeof *v);
+        if (!v)
+            abort(); /* a few pointers; fsalloc() aborts likewise */
+        s->v = v;
+        s->cap = cap;
+    }
+    s->v[s->n++] = b;
 }
 
 static void hub_teardown(b64_hub *h)
@@ -629,13 +642,14 @@ static void hub_teardown(b64_hub *h)
         }
     }
     pthread_mutex_unlock(&registry_lock);
+    batch_set all = { NULL, 0, 0 };
     for (int i = 0; i < HUB_LANES; i++) {
         if (h->lane_head[i]) /* teardown: wait, do not wake anyone */
             (void) b64x_lane_wait(h->lanes[i]);
         while (h->lane_head[i]) {
             b64_batch *b = h->lane_head[i];
             h->lane_head[i] = b->lane_next;
-            teardown_put(b);
+            set_add(&all, b);
         }
         h->lane_tail[i] = NULL;
         h->lane_depth[i] = 0;
@@ -643,12 +657,25 @@ static void hub_teardown(b64_hub *h)
     }
     for (unsigned l = 0; l < HUB_DEPTH; l++)
         if (h->filling[l])
-            teardown_put(h->filling[l]);
+            set_add(&all, h->filling[l]);
     while (h->ready) {
         b64_batch *b = h->ready;
         h->ready = b->next;
-        teardown_put(b);
+        set_add(&all, b);
     }
+    /* the finished batches they still read records of (held only by those
+     * references: every stage is gone), then every link dropped, then each
+     * batch back to the pool exactly once */
+    for (size_t i = 0; i < all.n; i++) {
+        b64_batch *a = all.v[i]->after;
+        all.v[i]->after = NULL;
+        all.v[i]->after_refs = 0;
+        if (a && a->state == B_DONE)
+            set_add(&all, a);
+    }
+    for (size_t i = 0; i < all.n; i++)
+        batch_put(all.v[i]);
+    free(all.v);
     (void) async_unregister(h->async, h->efd);
     close(h->efd);
     h->efd = -1;

@@ -13,9 +13,9 @@
 
 enum {
     PIN_SLAB = 32 << 20, /* default slab bytes */
-    PIN_POOL = 64,       /* default idle slabs kept */
     PIN_ALIGN = 64,      /* pieces start on a cache line */
 };
+#define PIN_IDLE_BYTES ((size_t) 2 << 30) /* default idle bytes kept */
 
 struct b64_pin_slab {
     uint8_t *base;
@@ -27,11 +27,12 @@ struct b64_pin_slab {
 static pthread_once_t pin_once = PTHREAD_ONCE_INIT;
 static pthread_key_t pin_key;
 static pthread_mutex_t pin_lock = PTHREAD_MUTEX_INITIALIZER;
-static b64_pin_slab *pin_free; /* idle slabs, refs == 0 */
-static unsigned pin_nfree;
+static b64_pin_slab *pin_free; /* idle standard slabs, refs == 0 */
+static size_t pin_idle;        /* their bytes */
 static size_t pin_slab = PIN_SLAB;
-static unsigned pin_pool = PIN_POOL;
+static size_t pin_idle_max = PIN_IDLE_BYTES;
 static bool pin_on = true;
+static atomic_bool pin_active; /* a GPU stage exists (b64_pin_activate) */
 static atomic_long pin_refs; /* references held on pieces (not the threads') */
 
 static size_t env_size(const char *name, size_t dflt)
@@ -44,14 +45,16 @@ static size_t env_size(const char *name, size_t dflt)
     return (!end || *end) ? dflt : (size_t) x;
 }
 
+/* Back to the idle list while the idle bytes stay within the cap; an
+ * oversize slab (a piece of its own) is never kept. */
 static void slab_release(b64_pin_slab *s)
 {
     s->used = 0;
     pthread_mutex_lock(&pin_lock);
-    if (pin_nfree < pin_pool) {
+    if (s->size == pin_slab && pin_idle + s->size <= pin_idle_max) {
         s->next = pin_free;
         pin_free = s;
-        pin_nfree++;
+        pin_idle += s->size;
         s = NULL;
     }
     pthread_mutex_unlock(&pin_lock);
@@ -92,7 +95,7 @@ static void pin_init(void)
     pin_slab = env_size("ASYNC_B64_PIN_SLAB", PIN_SLAB);
     if (pin_slab < (1u << 20))
         pin_slab = 1u << 20;
-    pin_pool = (unsigned) env_size("ASYNC_B64_PIN_POOL", PIN_POOL);
+    pin_idle_max = env_size("ASYNC_B64_PIN_IDLE_BYTES", PIN_IDLE_BYTES);
     (void) pthread_key_create(&pin_key, thread_done);
 }
 
@@ -102,25 +105,36 @@ bool b64_pin_enabled(void)
     return pin_on;
 }
 
+void b64_pin_activate(void)
+{
+    atomic_store_explicit(&pin_active, true, memory_order_relaxed);
+}
+
+size_t b64_pin_idle_bytes(void)
+{
+    pthread_mutex_lock(&pin_lock);
+    size_t n = pin_idle;
+    pthread_mutex_unlock(&pin_lock);
+    return n;
+}
+
 long b64_pin_live_refs(void)
 {
     return atomic_load_explicit(&pin_refs, memory_order_relaxed);
 }
 
-/* An idle slab of at least `size` bytes, or a new one; refs = 0. */
+/* An idle standard slab (size == pin_slab), or a new one; refs = 0. */
 static b64_pin_slab *slab_get(size_t size)
 {
     b64_pin_slab *s = NULL;
-    pthread_mutex_lock(&pin_lock);
-    for (b64_pin_slab **p = &pin_free; *p; p = &(*p)->next) {
-        if ((*p)->size >= size) {
-            s = *p;
-            *p = s->next;
-            pin_nfree--;
-            break;
+    if (size == pin_slab) {
+        pthread_mutex_lock(&pin_lock);
+        if ((s = pin_free)) {
+            pin_free = s->next;
+            pin_idle -= s->size;
         }
+        pthread_mutex_unlock(&pin_lock);
     }
-    pthread_mutex_unlock(&pin_lock);
     if (!s) {
         s = calloc(1, sizeof *s);
         if (!s)
@@ -140,7 +154,7 @@ static b64_pin_slab *slab_get(size_t size)
 
 void *b64_pin_alloc(size_t n, b64_pin_slab **slab)
 {
-    if (!b64_pin_enabled())
+    if (!b64_pin_enabled() || !atomic_load_explicit(&pin_active, memory_order_relaxed))
         return NULL;
     const size_t need = (n + PIN_ALIGN - 1) / PIN_ALIGN * PIN_ALIGN;
     if (need > pin_slab / 4) { /* a slab of its own */

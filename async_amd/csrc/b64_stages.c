@@ -129,6 +129,11 @@ struct stage {
     bool final_queued;  /* the last block (or nothing) has been launched */
     bool short_seen;    /* an upstream read came up short (not EAGAIN)
                            since the staged output last ran out */
+    int up_err;         /* an upstream read failed (errno other than EAGAIN)
+                           after the bytes before it were committed: the
+                           staged output is served first, then one read
+                           returns -1 with it (ref base64encoder.c:127-129,
+                           base64decoder.c:58-61 return upstream's errno) */
     uint8_t carry[3];   /* encoder: bytes of the incomplete group;
                            decoder: sextets the last block held back */
     size_t ncarry;
@@ -203,6 +208,7 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->lend_min = env_size("ASYNC_B64_LEND_MIN", 4096, 1);
     st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
     st->skip = skip_char(&abc);
+    b64_pin_activate(); /* queued messages are pinned for GPU stages from now on */
     for (int i = 0; i < NSLOTS; i++)
         st->slots[i].owner = st;
 }
@@ -682,6 +688,21 @@ static void stage_return(stage *st)
         retire_head(st);
 }
 
+/* top_up(), except that an upstream failure other than EAGAIN is kept in
+ * up_err (its bytes before it are committed and get served first) and no
+ * upstream read is made while one is pending. */
+static int stage_top_up(stage *st)
+{
+    if (st->up_err)
+        return 0;
+    int rc = top_up(st);
+    if (rc > 0 && rc != EAGAIN) {
+        st->up_err = rc;
+        return 0;
+    }
+    return rc;
+}
+
 static ssize_t stage_read(stage *st, void *buf, size_t count)
 {
     stage_return(st); /* a new read ends any loan */
@@ -694,7 +715,7 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
     int rc = stage_start(st, count);
     if (rc)
         return stage_fail(st, rc);
-    rc = top_up(st);
+    rc = stage_top_up(st);
     if (rc < 0)
         return stage_fail(st, rc);
     for (;;) {
@@ -726,12 +747,13 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
          * free to pull more (a read larger than both slots). */
         bool serve = staged >= count || (staged && st->dir == DIR_DECODE) ||
                      (staged && !blocked &&
-                      (st->final_queued || st->short_seen || !next_launch_slot(st)));
+                      (st->final_queued || st->short_seen || st->up_err ||
+                       !next_launch_slot(st)));
         if (serve) {
             size_t n = serve_body(st, buf, staged < count ? staged : count);
             if (n == staged)
                 st->short_seen = false;
-            rc = top_up(st); /* keep the GPU busy while the consumer works */
+            rc = stage_top_up(st); /* keep the GPU busy while the consumer works */
             if (rc < 0)
                 return stage_fail(st, rc);
             return (ssize_t) n;
@@ -740,7 +762,8 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
             errno = EAGAIN; /* the completion brings the consumer back */
             return -1;
         }
-        if (st->nbusy && st->slots[st->head].out_pos < st->slots[st->head].out_len) {
+        if (!st->up_err && st->nbusy &&
+            st->slots[st->head].out_pos < st->slots[st->head].out_len) {
             /* staged output short of `count` while upstream answered
              * EAGAIN: upstream's callback brings the consumer back (a
              * full-or-EAGAIN upstream makes the reference return EAGAIN
@@ -750,13 +773,18 @@ static ssize_t stage_read(stage *st, void *buf, size_t count)
         }
         if (st->nbusy) { /* finished slots with nothing left to serve */
             retire_head(st);
-            rc = top_up(st);
+            rc = stage_top_up(st);
             if (rc < 0)
                 return stage_fail(st, rc);
             continue;
         }
         if (st->final_queued)
             return 0;
+        if (st->up_err) { /* everything before the failure has been served */
+            errno = st->up_err;
+            st->up_err = 0;
+            return -1;
+        }
         errno = rc > 0 ? rc : EAGAIN;
         return -1;
     }

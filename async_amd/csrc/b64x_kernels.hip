@@ -3683,17 +3683,24 @@ bool g_info_done[kMaxDevices];
 // that needs one takes a free slot, or rebinds the least recently used
 // idle workspace of its device, and never frees memory on the way.
 //  - A call pins its entry from the lookup until its kernels are enqueued
-//    and the entry's event is recorded behind them (`pins`), so no other
-//    thread can rebind a workspace between handing it out and enqueuing on
-//    it; when all kWsCache entries are pinned the call gets -EBUSY.
-//  - Rebinding makes the new stream wait on the device for the event
-//    recorded behind the workspace's last use (hipStreamWaitEvent): no host
-//    wait, no device-wide synchronisation, no hipFree, and no lock held
-//    across a HIP call that waits, so a host callback on any stream that
-//    calls back into the library cannot deadlock on it.  (Round 3 freed the
-//    LRU workspace after a hipDeviceSynchronize under the library's lock;
-//    a first fix that freed it with hipFree outside the lock hung a 12-thread
-//    test on the MI355X: hipFree waits for the whole device.)
+//    (`pins`), so no other thread can rebind a workspace between handing it
+//    out and enqueuing on it; when all kWsCache entries are pinned the call
+//    gets -EBUSY.
+//  - Rebinding makes the new stream wait on the device for the workspace's
+//    last use (hipStreamWaitEvent): no host wait, no device-wide
+//    synchronisation, no hipFree, and no lock held across a HIP call that
+//    waits, so a host callback on any stream that calls back into the
+//    library cannot deadlock on it.  (Round 3 freed the LRU workspace after
+//    a hipDeviceSynchronize under the library's lock; a first fix that freed
+//    it with hipFree outside the lock hung a 12-thread test on the MI355X:
+//    hipFree waits for the whole device.)
+//  - The event that marks the last use is recorded when the workspace leaves
+//    its stream, not after every call: on the old stream when another stream
+//    takes it over (everything enqueued there so far includes every use),
+//    or on the stream being released (b64x_release_stream, which the caller
+//    runs before destroying it).  Round 4 recorded it behind every call; an
+//    event between two kernels leaves the GPU idle for several microseconds,
+//    which showed as +5 us per config-3 batch decode.
 //  - Each call leaves the workspace zeroed for the next (re-armed by the
 //    kernels), so a rebound workspace needs no clearing.
 // A library workspace: the decode workspace for the largest plan, then the
@@ -3718,15 +3725,16 @@ struct WsEntry {
     int dev;
     void *stream;       // bound stream; nullptr = idle (reusable)
     void *ws;           // nullptr: slot not allocated yet
-    hipEvent_t last;    // recorded after the entry's last enqueued use
-    bool recorded;      // `last` has been recorded at least once
+    hipEvent_t last;    // recorded behind the last use when it left a stream
+    bool recorded;      // `last` guards a use on a stream it has left
     uint64_t used;      // last use (g_ws_tick)
     int pins;           // calls between lookup and their event record
     bool release;       // b64x_release_stream while pinned: unbind at unpin
     RowsShape rows;     // the row batch shape whose model the workspace holds
 };
 constexpr int kWsCache = 8;
-std::mutex g_ws_mu;     // g_ws, g_ws_tick (never held across a waiting HIP call)
+std::mutex g_ws_mu;     // g_ws, g_ws_tick (held across hipEventRecord, which only
+                        // enqueues, never across a HIP call that waits)
 WsEntry g_ws[kWsCache];
 uint64_t g_ws_tick;
 
@@ -3942,8 +3950,23 @@ int b64x_encode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
     return launch_status();
 }
 
+// A stream being captured into a graph: its calls never reuse what earlier
+// calls left (a held model) -- the graph replays later, after other calls
+// may have replaced it, so the capture records the probe or prep as well --
+// and never allocate or take over a library workspace.
+static bool capturing(void *stream)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing((hipStream_t) stream, &st) == hipSuccess &&
+           st != hipStreamCaptureStatusNone;
+}
+
 // The workspace of (current device, stream), pinned; *slot receives its
-// entry for ws_unpin().
+// entry for ws_unpin().  A stream that holds none and is being captured
+// gets nullptr with *err = -EBUSY: allocating or rebinding one (a hipMalloc,
+// or a wait on an event recorded outside the capture) has no place in a
+// graph, so such a stream decodes once outside the capture first, or passes
+// a workspace of its own.
 static void *library_workspace(void *stream, int *slot, int *err, RowsShape *rows = nullptr)
 {
     if (rows) *rows = RowsShape{};
@@ -3968,11 +3991,24 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
                 return e.ws;
             }
         }
-        // the least recently used idle workspace of this device, else a
-        // slot never allocated
-        for (int i = 0; i < kWsCache; i++) {
-            const WsEntry &e = g_ws[i];
-            if (e.ws && e.dev == dev && !e.pins && (v < 0 || e.used < g_ws[v].used)) v = i;
+        if (capturing(stream)) {
+            *err = -EBUSY;
+            return nullptr;
+        }
+        // the least recently used idle workspace of this device (released,
+        // or bound to a stream that is not being captured), else a slot
+        // never allocated
+        unsigned skip = 0;
+        for (;;) {
+            v = -1;
+            for (int i = 0; i < kWsCache; i++) {
+                const WsEntry &e = g_ws[i];
+                if (e.ws && e.dev == dev && !e.pins && !((skip >> i) & 1) &&
+                    (v < 0 || e.used < g_ws[v].used))
+                    v = i;
+            }
+            if (v < 0 || !g_ws[v].stream || !capturing(g_ws[v].stream)) break;
+            skip |= 1u << v;
         }
         if (v < 0)
             for (int i = 0; i < kWsCache && v < 0; i++)
@@ -3983,6 +4019,17 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
         }
         WsEntry &e = g_ws[v];
         fresh = !e.ws;
+        if (!fresh && e.stream) {
+            // taken from a stream that still holds it: mark the end of
+            // everything enqueued there so far, its last use included (an
+            // enqueue, no wait; under the lock, so the owner cannot release
+            // and destroy the stream in between)
+            if (hipEventRecord(e.last, (hipStream_t) e.stream) != hipSuccess) {
+                *err = -EBUSY;
+                return nullptr;
+            }
+            e.recorded = true;
+        }
         wait = !fresh && e.recorded;
         after = e.last;
         if (fresh) e = WsEntry{};
@@ -3991,6 +4038,7 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
         e.used = ++g_ws_tick;
         e.pins = 1;  // reserved: nobody else takes this slot
         e.release = false;
+        e.rows = RowsShape{};  // the old stream's row model is not this stream's
     }
     int rc = 0;
     if (fresh) {
@@ -4027,20 +4075,30 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
     return g_ws[v].ws;
 }
 
+// Unbind entry e from its stream, marking the stream's position (the end of
+// the workspace's last use) with the entry's event.  Under g_ws_mu.
+static void ws_leave(WsEntry &e)
+{
+    if (e.stream && hipEventRecord(e.last, (hipStream_t) e.stream) == hipSuccess)
+        e.recorded = true;
+    else if (e.stream)
+        e.recorded = false;  // nothing to wait on; the caller owns the ordering
+    e.stream = nullptr;
+    e.release = false;
+}
+
 // The call that pinned entry `slot` has enqueued its kernels on `stream`:
-// record the entry's last-use event behind them and unpin it.  rows: the
-// shape of the row batch whose model and cleared bitmap the call leaves in
-// the workspace; none for any other call (its kernels use the scratch).
+// unpin it.  rows: the shape of the row batch whose model and cleared bitmap
+// the call leaves in the workspace; none for any other call (its kernels use
+// the scratch).  No event here: the workspace stays with its stream, whose
+// own order protects the next call (see g_ws).
 static void ws_unpin(int slot, void *stream, RowsShape rows = RowsShape{})
 {
+    (void) stream;
     std::lock_guard<std::mutex> lk(g_ws_mu);
     WsEntry &e = g_ws[slot];
     e.rows = rows;
-    if (hipEventRecord(e.last, (hipStream_t) stream) == hipSuccess) e.recorded = true;
-    if (--e.pins == 0 && e.release) {
-        e.stream = nullptr;
-        e.release = false;
-    }
+    if (--e.pins == 0 && e.release) ws_leave(e);
 }
 
 void b64x_release_stream(void *stream)
@@ -4054,7 +4112,7 @@ void b64x_release_stream(void *stream)
         if (e.pins)
             e.release = true;  // the last unpin unbinds it
         else
-            e.stream = nullptr;  // idle: the next stream waits on its event
+            ws_leave(e);  // idle: the next stream waits on its event
     }
 }
 
@@ -4146,16 +4204,6 @@ static int held_slot(const void *ws)
 {
     const uint64_t x = (uintptr_t) ws * 0x9E3779B97F4A7C15ull;
     return (int) (x >> 58);  // 64 entries
-}
-
-// A call being captured into a graph never reuses what earlier calls left
-// (a held model): the graph replays later, after other calls may have
-// replaced it, so the capture records the probe or prep as well.
-static bool capturing(void *stream)
-{
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    return hipStreamIsCapturing((hipStream_t) stream, &st) == hipSuccess &&
-           st != hipStreamCaptureStatusNone;
 }
 
 static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
@@ -4421,9 +4469,13 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
             err = launch_status();
             ws_unpin(slot, stream, err ? RowsShape{} : key);
             return err;
-        } else if (err) {
+        } else if (err && err != -EBUSY) {
             return err;
         }
+        // -EBUSY (every library workspace pinned by calls being enqueued, or
+        // a capture on a stream that holds none): the general path below
+        // needs no workspace
+        err = 0;
     }
     if (!done && (err = hip_err(hipMemsetAsync(d_outlen, 0, (size_t) nbuf * 8, s)))) return err;
     if (!done && slots) {

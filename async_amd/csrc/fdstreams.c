@@ -159,13 +159,25 @@ static void sink_requeue(fdsink_t *s)
     sink_probe(s);
 }
 
+/* The fd could not be watched (open_fdsink): done with that error, reported
+ * from the loop like any other completion, so a callback registered after
+ * open_fdsink() returned is performed too. */
+static void sink_report(fdsink_t *s)
+{
+    s->probe_queued = false;
+    if (s->closed || s->done)
+        return;
+    s->done = true;
+    action_1_perf(s->cb);
+}
+
 /* ref push_output() :669-727: send what the outbuf holds, refill it with
  * one read of the source when it is empty (replenish_outbuf() :451-484);
  * EAGAIN from either side ends the turn (an fd edge or the source's
  * callback brings the sink back). */
 static void sink_probe(fdsink_t *s)
 {
-    if (s->closed || s->done)
+    if (s->closed || s->done || s->fd < 0)
         return;
     for (int burst = 0; burst < SINK_BURST; burst++) {
         if (s->cursor == s->count) {
@@ -223,9 +235,11 @@ fdsink_t *open_fdsink(async_t *async, bytestream_1 source, int fd)
     bytestream_1_register_callback(source, probe);
     if (async_register(async, fd, probe) < 0) {
         s->err = errno ? errno : EBADF;
-        s->done = true;
-        close(fd);
+        if (fd >= 0)
+            close(fd);
         s->fd = -1;
+        s->probe_queued = true;
+        async_execute(async, (action_1) { s, (act_1) sink_report });
         return s;
     }
     s->probe_queued = true;

@@ -119,8 +119,12 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * (about 12.7 MiB of HBM each), allocated on first need and never freed: a
  * call on a stream without one takes an idle one (its stream made to wait
  * on the device for the workspace's last use), or -EBUSY if all eight are
- * in use by calls being enqueued right then.  A call that allocates one is
- * not capture-safe. */
+ * in use by calls being enqueued right then.  A stream being captured into
+ * a graph that holds no library workspace yet also gets -EBUSY (allocating
+ * or rebinding one cannot be captured): decode on it once outside the
+ * capture, or pass d_workspace.  A workspace stays with its stream until
+ * b64x_release_stream() or until another stream takes it over; no event is
+ * recorded per call. */
 int b64x_decode_dev(const void *d_in, uint64_t nchars, void *d_out,
                     b64x_dec_result *d_res, const b64x_alphabet *abc,
                     unsigned flags, void *d_workspace, void *stream);
@@ -152,7 +156,11 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
 
 /* nbuf buffers of `len` characters at d_in + i*in_stride, decoded to
  * d_out + i*out_stride (capacity b64x_decoded_cap(len) each);
- * d_outlen[i] (device) receives buffer i's byte count. */
+ * d_outlen[i] (device) receives buffer i's byte count.  Rows with room
+ * (out_stride >= 12*ceil(len/16)) use the stream's library workspace (as
+ * b64x_decode_dev with d_workspace NULL) to hold the batch's line model;
+ * when none can be had (all pinned, or a capture on a stream holding none)
+ * the batch takes the general path, same bytes. */
 int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                         uint32_t nbuf, void *d_out, uint64_t out_stride,
                         uint64_t *d_outlen, const b64x_alphabet *abc,

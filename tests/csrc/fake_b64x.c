@@ -369,6 +369,8 @@ int b64x_device_check(void)
  * before an inaccessible page, so that a write past a buffer's end faults
  * here as it does against the real pinned mappings (calloc'd buffers let
  * an arena overrun go unnoticed). */
+static atomic_ullong g_host_bytes, g_host_allocs; /* live "pinned" bytes; allocations */
+
 void *b64x_host_alloc(uint64_t bytes)
 {
     const size_t pg = 4096, need = ((bytes ? bytes : 1) + 63) / 64 * 64;
@@ -383,6 +385,8 @@ void *b64x_host_alloc(uint64_t bytes)
     uint8_t *p = base + data - need;
     ((size_t *) p)[-2] = (size_t) base;
     ((size_t *) p)[-1] = total;
+    atomic_fetch_add(&g_host_bytes, total);
+    atomic_fetch_add(&g_host_allocs, 1);
     return p;
 }
 
@@ -390,7 +394,15 @@ void b64x_host_free(void *p)
 {
     if (!p)
         return;
+    atomic_fetch_sub(&g_host_bytes, ((size_t *) p)[-1]);
     munmap((void *) ((size_t *) p)[-2], ((size_t *) p)[-1]);
+}
+
+/* Tests: pinned-stand-in bytes live now, and allocations ever made. */
+void fake_host_stats(uint64_t out[2])
+{
+    out[0] = atomic_load(&g_host_bytes);
+    out[1] = atomic_load(&g_host_allocs);
 }
 
 void b64x_diag_counters(uint64_t out[2])

@@ -111,6 +111,46 @@ static void cs_unreg(void *obj)
 static const struct bytestream_1_vt cs_vt = { cs_read, cs_close, cs_reg,
                                               cs_unreg };
 
+/* ---- failing source: data, then a hard error -------------------------- */
+
+/* Serves in[0..n) at most `chunk` bytes per read (chunk 0: every read
+ * full, a read that the rest cannot fill fails), then fails every read with
+ * errno `fail` (a socket reset, a disk error): the upstream ADVICE r04
+ * describes, whose error the stage must not turn into EAGAIN. */
+typedef struct {
+    async_t *async;
+    const uint8_t *in;
+    size_t n, cursor, chunk;
+    int fail;
+} failing_source;
+
+static ssize_t fs_src_read(void *obj, void *buf, size_t count)
+{
+    failing_source *s = obj;
+    if (s->cursor == s->n || (!s->chunk && s->n - s->cursor < count)) {
+        s->cursor = s->n;
+        errno = s->fail;
+        return -1;
+    }
+    if (s->chunk && count > s->chunk)
+        count = s->chunk;
+    if (count > s->n - s->cursor)
+        count = s->n - s->cursor;
+    memcpy(buf, s->in + s->cursor, count);
+    s->cursor += count;
+    return (ssize_t) count;
+}
+
+static void fs_src_close(void *obj)
+{
+    failing_source *s = obj;
+    async_wound(s->async, s);
+    s->async = NULL;
+}
+
+static const struct bytestream_1_vt fs_src_vt = { fs_src_read, fs_src_close, cs_reg,
+                                                  cs_unreg };
+
 /* ---- tap: copies what flows between two stages ------------------------ */
 
 typedef struct {
@@ -175,7 +215,14 @@ typedef struct {
     ssize_t *counts; /* optional log of positive read returns */
     size_t max_counts, ncounts;
     size_t *live;    /* optional: consumers still running; quit at 0 */
+    int timed_out;   /* the watchdog ended the run */
 } consumer;
+
+static void watchdog(consumer *c)
+{
+    c->timed_out = 1;
+    async_quit_loop(c->async);
+}
 
 /* ASYNC_B64_HUB_TRACE=1: the consumers' read time on this thread (the
  * reads include what they trigger: upstream gathers, launches, framing,
@@ -354,6 +401,49 @@ ssize_t h_decode_stream(const uint8_t *in, size_t n, size_t burst,
         base64_decode(async, blob_chain(async, in, n, burst), pos62, pos63);
     return run(async, base64decoder_as_bytestream_1(dec), read_size, out, cap,
                err_out, NULL);
+}
+
+/* failing source (n bytes in reads of `chunk`, then errno `fail`) ->
+ * encoder (decode == 0) or decoder -> consumer reading `read_size`.  The
+ * output before the failure goes to out; returns its length (also when the
+ * run ends in the error), *err_out the errno the consumer saw (0 at EOF). */
+ssize_t h_stage_upstream_error(int decode, const uint8_t *in, size_t n, size_t chunk, int fail,
+                               size_t read_size, uint8_t *out, size_t cap, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    failing_source *src = fscalloc(1, sizeof *src);
+    src->async = async;
+    src->in = in;
+    src->n = n;
+    src->chunk = chunk;
+    src->fail = fail;
+    bytestream_1 up = { src, &fs_src_vt };
+    bytestream_1 st = decode ? base64decoder_as_bytestream_1(base64_decode(async, up, -1, -1))
+                             : base64encoder_as_bytestream_1(base64_encode(async, up, -1, -1,
+                                                                           true, -1));
+    consumer c;
+    memset(&c, 0, sizeof c);
+    c.async = async;
+    c.material = st;
+    c.read_size = read_size;
+    c.out = out;
+    c.cap = cap;
+    action_1 cb = { &c, (act_1) consume };
+    bytestream_1_register_callback(st, cb);
+    async_execute(async, cb);
+    /* the reference runner's watchdog (test/asynctest.c:60-69): a consumer
+     * left waiting for a callback that never comes ends as ETIMEDOUT */
+    async_timer_t *dog = async_timer_start(async, async_now(async) + 5 * (uint64_t) ASYNC_S,
+                                           (action_1) { &c, (act_1) watchdog });
+    int rc = async_loop(async);
+    if (!c.timed_out)
+        async_timer_cancel(async, dog);
+    destroy_async(async);
+    if (err_out)
+        *err_out = rc < 0 ? errno : c.timed_out ? ETIMEDOUT : c.err;
+    return rc < 0 ? -1 : (ssize_t) c.len;
 }
 
 /* Loop + streams only (no GPU): blob -> nice(burst) -> consumer. */
@@ -1017,6 +1107,49 @@ ssize_t h_fd_encode(const uint8_t *in, const size_t *lens, size_t npieces, size_
     if (err_out)
         *err_out = err;
     return err ? -1 : (ssize_t) rd.got;
+}
+
+/* fdsink over a descriptor the loop cannot watch (-1, a regular file):
+ * the sink ends with the error and a callback registered after
+ * open_fdsink() returned is still performed.  Returns 1 if the
+ * callback ran (0 if the watchdog ended the loop); *err_out the sink's
+ * errno. */
+typedef struct {
+    async_t *async;
+    int fired;
+} sink_flag;
+
+static void sink_flag_fire(sink_flag *f)
+{
+    f->fired = 1;
+    async_quit_loop(f->async);
+}
+
+static void sink_flag_dog(sink_flag *f)
+{
+    async_quit_loop(f->async);
+}
+
+int h_fdsink_unwatchable(int fd, int *err_out)
+{
+    async_t *async = make_async();
+    if (!async)
+        return -1;
+    static const uint8_t msg[] = "aGVsbG8=";
+    bytestream_1 src = blobstream_as_bytestream_1(open_blobstream(async, msg, sizeof msg - 1));
+    sink_flag f = { async, 0 };
+    fdsink_t *sink = open_fdsink(async, src, fd);
+    fdsink_register_callback(sink, (action_1) { &f, (act_1) sink_flag_fire });
+    async_timer_t *dog = async_timer_start(async, async_now(async) + 5 * (uint64_t) ASYNC_S,
+                                           (action_1) { &f, (act_1) sink_flag_dog });
+    (void) async_loop(async);
+    if (f.fired)
+        async_timer_cancel(async, dog);
+    if (err_out)
+        *err_out = fdsink_error(sink);
+    fdsink_close(sink);
+    destroy_async(async);
+    return f.fired;
 }
 
 /* ---- a crash report: the faulting thread's native stack ------------------

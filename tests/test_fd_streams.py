@@ -115,6 +115,28 @@ def test_fd_encode_empty(fake):
                                                             read_size=10240)
 
 
+@pytest.mark.parametrize("what", ["minus_one", "regular_file"])
+def test_fdsink_unwatchable_fd_calls_back(fake, tmp_path, what):
+    """fdsink over a descriptor the loop cannot watch (-1; a regular file,
+    which epoll refuses): the sink ends with the error, reported from the
+    loop, so a callback registered after open_fdsink() returned is still
+    performed (it used to be marked done at once and the
+    callback never ran)."""
+    import ctypes
+    import errno
+    import os
+    fd = -1
+    if what == "regular_file":
+        fd = os.open(str(tmp_path / "sink.bin"), os.O_WRONLY | os.O_CREAT)
+    err = ctypes.c_int(0)
+    fired = fake.h_fdsink_unwatchable(fd, ctypes.byref(err))
+    assert fired == 1
+    assert err.value in (errno.EBADF, errno.EPERM), err.value
+    if what == "regular_file":  # the sink owned and closed it
+        with pytest.raises(OSError):
+            os.fstat(fd)
+
+
 def test_fd_ends_leak_check(fake):
     """The reference runner's counting allocator (test/asynctest.c:111-147)
     around both fd ends: pipestream, fdsink, stages, hub -- nothing left."""

@@ -1093,6 +1093,103 @@ def test_decode_graph_replay_after_other_lengths():
     assert out[:len(want)].cpu().numpy().tobytes() == want
 
 
+def test_capture_on_a_fresh_stream():
+    """Graph capture on a stream that never decoded: the
+    library does not allocate or rebind a workspace inside a capture.
+    b64.decode() then captures with a torch-allocated workspace,
+    decode_strided takes the general batch path, and the C call with
+    d_workspace NULL answers -EBUSY without enqueuing anything; every replay
+    is exact."""
+    import ctypes
+
+    from async_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(85)
+    raw = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    text = _wrap(orc.encode(raw), 76, b"\r\n")
+    x = dev(text)
+    out = torch.zeros(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+    res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+    nbuf = 300
+    rows = _mime_batch(nbuf, 1024, 76, b"\r\n", rng)
+    stride = max(len(r) for r in rows)
+    flat = dev(b"".join(r + b"\n" * (stride - len(r)) for r in rows))
+    cap = (b64.decoded_cap(stride) + 11) // 12 * 12
+    rout = torch.zeros(nbuf * cap, dtype=torch.uint8, device=DEV)
+    ol = torch.zeros(nbuf, dtype=torch.int64, device=DEV)
+    a = b64._abc(None)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        b64.decode(x, out=out, result=res, stream=s)
+        b64.decode_strided(flat, stride, stride, nbuf, rout, cap, ol, stream=s)
+        rc = lib.b64x_decode_dev(ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                 ctypes.byref(a), 0, None, ctypes.c_void_p(s.cuda_stream))
+    assert rc == -16  # -EBUSY
+    for _ in range(2):
+        out.zero_()
+        rout.zero_()
+        ol.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out[:raw.size].cpu().numpy(), raw)
+        olh = ol.cpu().tolist()
+        dh = rout.cpu().numpy()
+        for i, r in enumerate(rows):
+            want = orc.decode(r + b"\n" * (stride - len(r)))
+            assert olh[i] == len(want), i
+            assert dh[i * cap:i * cap + olh[i]].tobytes() == want, i
+    lib.b64x_release_stream(ctypes.c_void_p(s.cuda_stream))
+
+
+def test_workspace_taken_over_while_its_stream_is_busy():
+    """No event is recorded per call: a workspace stays with its stream and
+    the event that guards it is recorded when another stream takes it over.
+    Nine streams (one more than the cache) decode in turn with the library
+    workspace while each stream's earlier work is still queued behind a long
+    decode, so every take-over must wait for the old stream on the device;
+    every result is exact."""
+    import ctypes
+
+    from async_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(87)
+    big = rng.integers(0, 256, 30 << 20, dtype=np.uint8)
+    bx = dev(orc.encode(big))
+    bout = torch.empty(b64.decoded_cap(bx.numel()), dtype=torch.uint8, device=DEV)
+    a = b64._abc(None)
+    streams = [torch.cuda.Stream() for _ in range(9)]
+    jobs = []
+    for k in range(27):
+        raw = rng.integers(0, 256, 100_000 + 4099 * k, dtype=np.uint8)
+        text = _wrap(orc.encode(raw), 76, b"\r\n") if k % 3 == 0 else \
+            _junk(rng, orc.encode(raw), 0.01) if k % 3 == 1 else orc.encode(raw)
+        jobs.append((raw, dev(text),
+                     torch.zeros(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV),
+                     torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)))
+    bres = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+    torch.cuda.synchronize()
+    for k, (raw, x, out, res) in enumerate(jobs):
+        st = streams[k % 9]
+        if k % 9 == 0:  # keep the streams busy while their workspaces move
+            for s2 in streams[::2]:
+                assert lib.b64x_decode_dev(ctypes.c_void_p(bx.data_ptr()), bx.numel(),
+                                           ctypes.c_void_p(bout.data_ptr()),
+                                           ctypes.c_void_p(bres.data_ptr()), ctypes.byref(a), 0,
+                                           None, ctypes.c_void_p(s2.cuda_stream)) == 0
+        assert lib.b64x_decode_dev(ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                   ctypes.byref(a), 0, None, ctypes.c_void_p(st.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    for raw, x, out, res in jobs:
+        assert np.array_equal(out[:raw.size].cpu().numpy(), raw)
+    assert np.array_equal(bout[:big.size].cpu().numpy(), big)
+    for st in streams:
+        lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;

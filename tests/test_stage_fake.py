@@ -394,3 +394,88 @@ def test_egress_lent_fuzz(monkeypatch):
             assert got == orc.chunked_encode(np.frombuffer(data, np.uint8), piece_lens=sizes,
                                              max_chunk=max_chunk, read_size=read_size), seed
     assert L.b64_pin_live_refs() == 0
+
+
+@pytest.mark.parametrize("decode", [0, 1])
+@pytest.mark.parametrize("n,chunk,read_size", [(10_000, 3_000, 400), (200_000, 65_536, 4_096),
+                                               (5, 5, 8), (0, 1, 8), (100_000, 0, 8),
+                                               (100_000, 0, 4096), (3_000, 0, 200)])
+def test_upstream_error_is_returned_not_eagain(small_blocks, decode, n, chunk, read_size):
+    """An upstream that gives data and then fails hard (EIO): the stage
+    serves what it had (the reference returns each read's output as it
+    goes) and then returns -1 with EIO -- not EAGAIN, not a clean EOF
+    (ref src/base64encoder.c:127-129, base64decoder.c:58-61)."""
+    import errno
+    L = fake()
+    rng = np.random.default_rng(n + chunk)
+    raw = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    data = orc.encode(raw) if decode else raw
+    src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
+    cap = 2 * len(data) + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    err = ctypes.c_int(0)
+    got = L.h_stage_upstream_error(decode, src.ctypes.data, len(data), chunk, errno.EIO,
+                                   read_size, out.ctypes.data, cap, ctypes.byref(err))
+    assert err.value == errno.EIO
+    assert got >= 0
+    want = orc.decode(data) if decode else orc.encode(raw)
+    assert out[:got].tobytes() == want[:got]
+    if chunk:  # upstream gave every byte before failing
+        if decode:
+            # whole groups; the reference may also have emitted the bytes
+            # of a trailing partial group (at most 2)
+            assert len(want) - got <= 2
+        else:
+            # every full sextet of the bytes (base64encoder.c:132-139)
+            assert got == len(raw) * 8 // 6
+
+
+_PIN_SCRIPT = r"""
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from tests import util
+L = util.fake_harness()
+L.b64_pin_idle_bytes.restype = ctypes.c_size_t
+L.fake_host_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+def host():
+    o = (ctypes.c_uint64 * 2)()
+    L.fake_host_stats(o)
+    return int(o[0]), int(o[1])
+rng = np.random.default_rng(3)
+# a queue alone, before any GPU stage exists: no pinned memory at all
+pieces = [rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes() for _ in range(3)]
+got, err, _ = util.queue_stream(pieces, read_size=4096, lib=L)
+assert err == 0 and got == b"".join(pieces)
+assert host() == (0, 0), host()
+# with the encoder stage: 20 MiB messages (a slab of their own each, never
+# kept idle) and 3 MiB ones (standard 32 MiB slabs, kept within the cap)
+slab = 32 << 20
+for rnd in range(3):
+    pieces = [rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+              for n in (20 << 20, 3 << 20, 3 << 20, 21 << 20, 3 << 20)]
+    framed, err = util.egress_pieces(pieces, 1 << 20, 10240, lib=L)
+    assert err == 0, err
+    idle = L.b64_pin_idle_bytes()
+    assert idle % slab == 0 and idle <= int(sys.argv[2]), idle
+    assert L.b64_pin_live_refs() == 0
+print("ok", host(), L.b64_pin_idle_bytes())
+"""
+
+
+@pytest.mark.parametrize("cap", [32 << 20, 2 << 30])
+def test_pinned_message_pool_is_bounded(tmp_path, cap):
+    """The pinned message pool: nothing is pinned (and no HIP
+    runtime started) before the process has a GPU stage; slabs made for one
+    oversize message are freed on release; the idle slabs stay within
+    ASYNC_B64_PIN_IDLE_BYTES.  A fresh process, since the pool is
+    process-wide."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ASYNC_B64_PIN_IDLE_BYTES=str(cap))
+    p = subprocess.run([sys.executable, "-c", _PIN_SCRIPT, root, str(cap)], capture_output=True,
+                       text=True, env=env, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.startswith("ok"), p.stdout

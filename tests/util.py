@@ -106,6 +106,10 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.h_decode_stream.restype = ssz
     L.h_copy_stream.argtypes = [vp, sz, sz, sz, vp, sz, ip, ctypes.POINTER(sz)]
     L.h_copy_stream.restype = ssz
+    L.h_stage_upstream_error.argtypes = [ctypes.c_int, vp, sz, sz, ctypes.c_int, sz, vp, sz, ip]
+    L.h_stage_upstream_error.restype = ssz
+    L.h_fdsink_unwatchable.argtypes = [ctypes.c_int, ip]
+    L.h_fdsink_unwatchable.restype = ctypes.c_int
     L.h_encode_counts.argtypes = [vp, sz, sz, sz, sz, ch, ch, ctypes.c_int, ch, vp, sz, ip]
     L.h_encode_counts.restype = ssz
     L.h_chunk_stream.argtypes = [vp, sz, sz, sz, ctypes.c_int, sz, vp, sz, ip]
