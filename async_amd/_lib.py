@@ -110,6 +110,7 @@ SIGNATURES = {
     "b64x_lane_decode_check": (_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "b64x_lane_wait": (_int, [_vp]),
     "b64x_diag_counters": (None, [ctypes.POINTER(_u64)]),
+    "b64x_diag_paths": (None, [ctypes.POINTER(_u64)]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),
     "b64x_build_info": (ctypes.c_char_p, []),

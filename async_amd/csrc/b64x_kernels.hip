@@ -4206,6 +4206,19 @@ static int held_slot(const void *ws)
     return (int) (x >> 58);  // 64 entries
 }
 
+// Which path each automatic decode and row batch took (b64x_diag_paths):
+// probes launched, probes skipped (held model), hinted single passes, row
+// preps launched, row preps skipped (row model reused).
+enum { kPathProbe, kPathHeld, kPathHinted, kPathRowsPrep, kPathRowsReuse, kPaths };
+static std::atomic<uint64_t> g_paths[kPaths];
+
+static void path_taken(int k) { g_paths[k].fetch_add(1, std::memory_order_relaxed); }
+
+void b64x_diag_paths(uint64_t out[5])
+{
+    for (int k = 0; k < kPaths; k++) out[k] = g_paths[k].load(std::memory_order_relaxed);
+}
+
 static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
 {
     uint64_t x = (uintptr_t) ws * 0x9E3779B97F4A7C15ull ^ (uintptr_t) in * 0xC2B2AE3D27D4EB4Full ^
@@ -4266,10 +4279,14 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
             hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
                                (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key);
             if ((err = launch_status())) return err;
+            path_taken(kPathProbe);
             std::lock_guard<std::mutex> lk(g_held_mu);
             g_held[hs] = HeldModel{ws, nchars};
+        } else {
+            path_taken(kPathHeld);
         }
         if (junky) {
+            path_taken(kPathHinted);
             hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
@@ -4444,6 +4461,9 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
                     ws_unpin(slot, stream);
                     return err;
                 }
+                path_taken(kPathRowsPrep);
+            } else {
+                path_taken(kPathRowsReuse);
             }
             // + S blocks: the row-group mapping rounds the rows up to whole
             // bands of U Ru rows (NB <= S blocks each); spare blocks return

@@ -34,6 +34,49 @@
  * calls (it captures the probe or prep too); the junk hint's pick of path is
  * replayed as made at capture -- exact either way, only the speed differs.
  */
+/*
+ * Process-wide state a decode call reads and writes.  None of it decides a
+ * byte of output: every path below is exact for any input, and the state only
+ * picks which path runs (b64x_diag_paths counts the picks).
+ *
+ *   library workspaces   at most 8, one per (device, stream), for calls with
+ *                        d_workspace NULL and for b64x_decode_strided's rows
+ *                        with room.  Read and written by those calls: scratch
+ *                        (left zeroed), the probe's line model with the length
+ *                        it was made for, a row batch's model and the shape it
+ *                        was made for.  Guarded by a mutex; an entry is pinned
+ *                        while a call enqueues on it.
+ *   held models          64 entries keyed by a hash of the workspace address:
+ *                        {workspace, length of its last probe}, plus a pinned
+ *                        "probe again" flag each.  Read by every automatic
+ *                        b64x_decode_dev of <= 2^31 characters (not
+ *                        EXPECT_JUNK): a call of the same length on the same
+ *                        workspace with the flag down skips the probe.
+ *                        Written by every probe launch (host) and by
+ *                        k_decode_suffix, which raises the flag whenever it
+ *                        finds anything to decode past the line pass.  Any
+ *                        model is exact (k_decode_lines checks every slot and
+ *                        the model's length); a wrong one only costs speed.
+ *   probe hints          64 pinned entries keyed by a hash of (workspace,
+ *                        input address, length): "the last probe of this key
+ *                        cut the model near the start".  Read (without a
+ *                        sync) by every automatic decode, which then takes the
+ *                        probe + single exact pass; written by every probe on
+ *                        the device.  A stale or torn hint only picks the
+ *                        slower path; new content at the same address and
+ *                        length is decoded exactly either way.
+ *   row-model staleness  one pinned flag per library workspace, raised by
+ *                        k_rows_finish when a batch's first row failed its
+ *                        model; read by the next b64x_decode_strided of the
+ *                        same shape on that workspace, which then probes.
+ *   sequence numbers     one counter, drawn by every decode call and batch
+ *                        (b64x_dec_result.seq).
+ *
+ * A call being captured into a graph reads no held model or row model (it
+ * captures the probe or prep), and never allocates or takes over a library
+ * workspace.  The hint's pick is recorded in the capture as made.
+ */
+
 #ifndef ASYNC_AMD_B64X_H
 #define ASYNC_AMD_B64X_H
 
@@ -347,6 +390,11 @@ int b64x_lane_wait(b64x_lane *l);
  * out[0] session decode records, out[1] lane batches (process-wide totals,
  * for tests and diagnostics). */
 void b64x_diag_counters(uint64_t out[2]);
+/* Paths the automatic decodes took (process-wide totals, for tests and
+ * diagnostics): out[0] probes launched, out[1] probes skipped on a held
+ * model, out[2] hinted single passes, out[3] row-batch preps launched,
+ * out[4] row-batch preps skipped (the workspace's row model reused). */
+void b64x_diag_paths(uint64_t out[5]);
 
 /* ---- utilities ----------------------------------------------------------- */
 

@@ -1093,6 +1093,81 @@ def test_decode_graph_replay_after_other_lengths():
     assert out[:len(want)].cpu().numpy().tobytes() == want
 
 
+def _paths():
+    import ctypes
+
+    from async_amd import _lib
+    out = (ctypes.c_uint64 * 5)()
+    _lib.load().b64x_diag_paths(out)
+    return [int(v) for v in out]
+
+
+def test_new_content_at_a_held_address_and_length():
+    """The held model and the probe's hint are keyed on workspace, input
+    address and length, never on content.  Different
+    content written into the same buffer, decoded right after a junk-laden
+    call and right after a clean one, on a caller's workspace and on the
+    library's: every decode is exact, and each takes the path the state
+    predicts (b64x_diag_paths: probes, held-model skips, hinted single
+    passes)."""
+    rng = np.random.default_rng(89)
+    n = (3 << 20) + 7  # a length no other test decodes (hints and held models)
+    raw = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)]
+    clean = [orc.encode(r) for r in raw]
+    m = len(clean[0])
+    # junk-laden text of exactly the clean length: the first m characters of
+    # a 5 %-junk text, and what they decode to
+    junky = [_junk(rng, c, 0.05)[:m] for c in clean]
+    want_j = [orc.decode(t) for t in junky]
+    x = torch.empty(m, dtype=torch.uint8, device=DEV)
+    out = torch.zeros(b64.decoded_cap(m) + 8, dtype=torch.uint8, device=DEV)
+    res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+    PROBE, HELD, HINT = 0, 1, 2
+
+    for ws in (torch.zeros(b64.workspace_size(m), dtype=torch.uint8, device=DEV), None):
+        s = torch.cuda.Stream()
+
+        def run(text, want, expect):
+            x.copy_(torch.from_numpy(np.frombuffer(text, dtype=np.uint8).copy()))
+            torch.cuda.synchronize()
+            before = _paths()
+            d = b64.decode(x, out=out, workspace=ws, result=res, stream=s)
+            s.synchronize()
+            after = _paths()
+            assert d.info().out_len == len(want)
+            assert out[:len(want)].cpu().numpy().tobytes() == want
+            took = [after[k] - before[k] for k in (PROBE, HELD, HINT)]
+            assert took == expect, (took, expect)
+
+        # a call of another length on the workspace: whatever an earlier
+        # test left there, nothing is held for this length now
+        x.copy_(torch.from_numpy(np.frombuffer(clean[0], dtype=np.uint8).copy()))
+        b64.decode(x[:m - 4], workspace=ws, stream=s).info()
+        # a clean call probes (nothing held for this length)...
+        run(clean[0], raw[0].tobytes(), [1, 0, 0])
+        # ...and the next clean content at the same address and length reuses
+        # the model without a probe
+        run(clean[1], raw[1].tobytes(), [0, 1, 0])
+        # junk right after a clean call: held model (the hint is clean), the
+        # lines pass fails at the first junk byte and the suffix raises the flag
+        run(junky[0], want_j[0], [0, 1, 0])
+        # the same junk again: the flag forces a probe, which cuts the model
+        # near the start and sets the hint
+        run(junky[0], want_j[0], [1, 0, 0])
+        # different junk: the hint picks the probe + single pass
+        run(junky[1], want_j[1], [1, 0, 1])
+        # clean content right after a junk-laden call: the hint still says
+        # junk (single pass, exact), and its probe renews the hint as clean
+        run(clean[2], raw[2].tobytes(), [1, 0, 1])
+        # then the lines pass on the held clean model, no probe
+        run(clean[3], raw[3].tobytes(), [0, 1, 0])
+        if ws is None:
+            import ctypes
+
+            from async_amd import _lib
+            _lib.load().b64x_release_stream(ctypes.c_void_p(s.cuda_stream))
+
+
 def test_capture_on_a_fresh_stream():
     """Graph capture on a stream that never decoded: the
     library does not allocate or rebind a workspace inside a capture.
