@@ -148,6 +148,11 @@ def _import_torch_first() -> None:
         pass
 
 
+# Diagnostics an A/B timing may load an older library without
+# (tests/test_abi.py checks that the product exports them).
+_DIAG_ONLY = {"b64x_diag_paths"}
+
+
 def load() -> ctypes.CDLL:
     """Load libasync_b64.so (raises if it was not built)."""
     global _lib
@@ -161,6 +166,8 @@ def load() -> ctypes.CDLL:
         _import_torch_first()
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in _DIAG_ONLY and not hasattr(lib, name):
+                continue  # an older build under A/B (scripts/ab_*.py): no diagnostics
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

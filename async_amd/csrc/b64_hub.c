@@ -40,13 +40,18 @@ enum {
     HUB_LANES = 4,          /* batches in flight per loop */
     HUB_MAX_LIVE = HUB_LANES + 4, /* arenas a hub holds before idle
                                      stages are made to wait */
-    POOL_MAX = 128,         /* default of ASYNC_B64_POOL_MAX: idle arenas kept
+    POOL_MAX = 256,         /* default of ASYNC_B64_POOL_MAX: idle arenas kept
                                process-wide for reuse (~41 MB pinned each at
-                               the default ASYNC_B64_BATCH_BYTES; 16 loops on
-                               one GPU hold ~50 at once, and every arena freed
-                               and allocated again costs milliseconds of
-                               pinned-memory calls that stall the other
-                               loops) */
+                               the default ASYNC_B64_BATCH_BYTES).  Every arena
+                               freed and allocated again costs milliseconds of
+                               pinned-memory calls that stall the other loops:
+                               config 5 on 16 loops holds more than 128 at its
+                               peak (a hub exceeds HUB_MAX_LIVE for stages that
+                               must progress), and with 128 kept each pass
+                               allocated 1-18 arenas again and ran 10.8-14.1
+                               GiB/s against 16.2-16.5 without
+                               (profiles/r05_cfg5_t16_pool128.jsonl).  The pool
+                               never holds more than the process's peak. */
     HUB_JOBS = 1 << 16,     /* jobs per arena */
     HUB_DEPTH = 8,          /* reservations open at once (stages reading
                                through stages, see b64_hub_reserve) */
@@ -116,7 +121,7 @@ struct b64_hub {
     size_t nkicking;
     struct {                     /* ASYNC_B64_HUB_TRACE=1: printed at teardown */
         bool on;
-        unsigned long batches, jobs, allocs, wake_calls, max_ready;
+        unsigned long batches, jobs, allocs, wake_calls, max_ready, max_live;
         unsigned long long in_bytes, out_bytes, gather_bytes;
         unsigned long reserves, lent_jobs;
         unsigned long long lent_bytes;
@@ -134,6 +139,7 @@ static double mono_s(void)
 
 static pthread_mutex_t registry_lock = PTHREAD_MUTEX_INITIALIZER;
 static b64_hub *registry;
+static atomic_uint nhubs; /* hubs in the registry (loops with GPU stages) */
 
 /* Idle arenas, shared by all hubs of the process (pinned allocation costs
  * milliseconds; a hub's life may be one message). */
@@ -160,8 +166,12 @@ static void pool_init(void)
 
 /* ---------------------------------------------------------------- batches */
 
+static atomic_uint arenas_total; /* arenas in existence, pooled or not */
+static atomic_bool stocking;      /* a thread is stocking the pool */
+
 static void batch_free(b64_batch *b)
 {
+    atomic_fetch_sub_explicit(&arenas_total, 1, memory_order_relaxed);
     b64x_host_free(b->h_in);
     b64x_host_free(b->h_out);
     b64x_host_free(b->h_in_off);
@@ -197,6 +207,7 @@ static b64_batch *batch_new(b64_hub *h, size_t in_cap)
     b->pins = calloc(HUB_SEGS, sizeof *b->pins);
     b->jobs = malloc(HUB_JOBS * sizeof *b->jobs);
     b->lane = -1;
+    atomic_fetch_add_explicit(&arenas_total, 1, memory_order_relaxed);
     if (!b->h_in || !b->h_out || !b->h_in_off || !b->h_out_off || !b->h_flags || !b->h_res ||
         !b->h_spell || !b->h_prev || !b->h_seg || !b->pins || !b->jobs) {
         batch_free(b);
@@ -259,6 +270,41 @@ static void batch_drop_after(b64_hub *h, b64_batch *b)
         batch_recycle(h, a);
 }
 
+/* The pool ran dry: stock it, by one thread at a time and within the
+ * pool's cap, up to the arenas the live hubs hold under their normal limit
+ * (HUB_MAX_LIVE each), and past that by a quarter of the arenas in
+ * existence (at least 2).  Demand grows a little at a time -- config 5 on 16
+ * loops took one more arena than ever before in a pass now and then -- and
+ * every arena allocated on demand is a pinned-memory call that stalls every
+ * loop for milliseconds: with the pool filled only on demand, passes that
+ * allocated ran 10.8-14.1 GiB/s against 16.2-16.5 for those that did not
+ * (profiles/r05_cfg5_t16_pool128.jsonl, r05_cfg5_t16_stocked.jsonl). */
+static void stock_pool(b64_hub *h)
+{
+    bool idle = false;
+    if (!atomic_compare_exchange_strong(&stocking, &idle, true))
+        return;
+    const unsigned total = atomic_load_explicit(&arenas_total, memory_order_relaxed);
+    const unsigned cover = atomic_load_explicit(&nhubs, memory_order_relaxed) * HUB_MAX_LIVE;
+    unsigned want = cover > total ? cover - total : total / 4;
+    if (want < 2)
+        want = 2;
+    pthread_once(&pool_once, pool_init);
+    for (unsigned i = 0; i < want; i++) {
+        pthread_mutex_lock(&pool_lock);
+        const bool room = npool < pool_max;
+        pthread_mutex_unlock(&pool_lock);
+        if (!room)
+            break;
+        b64_batch *x = batch_new(h, h->batch_bytes);
+        if (!x)
+            break;
+        h->tr.allocs++;
+        batch_put(x);
+    }
+    atomic_store(&stocking, false);
+}
+
 static b64_batch *batch_get(b64_hub *h, size_t need)
 {
     b64_batch *b = NULL;
@@ -277,9 +323,13 @@ static b64_batch *batch_get(b64_hub *h, size_t need)
         b = batch_new(h, need > h->batch_bytes ? need : h->batch_bytes);
         if (!b)
             return NULL;
+        if (need <= h->batch_bytes)
+            stock_pool(h);
     }
     b->hub = h;
     h->live++;
+    if (h->live > h->tr.max_live)
+        h->tr.max_live = h->live;
     return b;
 }
 
@@ -592,6 +642,7 @@ b64_hub *b64_hub_acquire(async_t *async)
     h->users = 1;
     h->next_hub = registry;
     registry = h;
+    atomic_fetch_add_explicit(&nhubs, 1, memory_order_relaxed);
     pthread_mutex_unlock(&registry_lock);
     return h;
 }
@@ -626,11 +677,11 @@ static void hub_teardown(b64_hub *h)
     if (h->tr.on)
         fprintf(stderr,
                 "b64_hub: batches %lu jobs %lu in %llu out %llu allocs %lu "
-                "max_ready %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f "
+                "max_ready %lu max_live %lu wakes %lu wake_s %.4f launch_s %.4f span_s %.4f "
                 "first %.6f last %.6f gather_s %.4f gather_bytes %llu reserve_s %.4f "
                 "reserves %lu lent_segs %lu lent_bytes %llu\n",
                 h->tr.batches, h->tr.jobs, h->tr.in_bytes, h->tr.out_bytes,
-                h->tr.allocs, h->tr.max_ready, h->tr.wake_calls, h->tr.wake_s,
+                h->tr.allocs, h->tr.max_ready, h->tr.max_live, h->tr.wake_calls, h->tr.wake_s,
                 h->tr.launch_s, h->tr.t_last - h->tr.t_first, h->tr.t_first, h->tr.t_last,
                 h->tr.gather_s, h->tr.gather_bytes, h->tr.reserve_s, h->tr.reserves,
                 h->tr.lent_jobs, h->tr.lent_bytes);
@@ -638,6 +689,7 @@ static void hub_teardown(b64_hub *h)
     for (b64_hub **p = &registry; *p; p = &(*p)->next_hub) {
         if (*p == h) {
             *p = h->next_hub;
+            atomic_fetch_sub_explicit(&nhubs, 1, memory_order_relaxed);
             break;
         }
     }
@@ -845,6 +897,14 @@ void b64_hub_commit(b64_hub *h, b64_ticket *t, size_t n, size_t out_len,
 }
 
 static atomic_ulong lent_total; /* segments lent, process-wide (tests) */
+
+unsigned long b64_hub_pooled(void)
+{
+    pthread_mutex_lock(&pool_lock);
+    unsigned long n = npool;
+    pthread_mutex_unlock(&pool_lock);
+    return n;
+}
 
 unsigned long b64_hub_lent_total(void)
 {

@@ -100,6 +100,8 @@ bool b64_hub_lend(b64_hub *h, size_t pos, const uint8_t *src, size_t n,
                   struct b64_pin_slab *slab);
 /* Segments lent so far in this process (tests). */
 unsigned long b64_hub_lent_total(void);
+/* Idle arenas in the process-wide pool (tests, traces). */
+unsigned long b64_hub_pooled(void);
 void b64_hub_cancel(b64_hub *h);
 /* ASYNC_B64_HUB_TRACE=1: the stages add the time of their upstream reads
  * (the copies into the arenas) to the hub's trace line. */

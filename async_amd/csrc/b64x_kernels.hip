@@ -565,7 +565,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_tight2(
         // tail block: guarded loads (the last buffer's windows may run past
         // the input) and stores (the output may end inside a slot)
         for (int u = 0; u < U; u++) {
-            const uint64_t t = s0 + u * kThreads + threadIdx.x;
+            const uint64_t t = s0 + (u * kThreads + threadIdx.x);
             if (t >= nslots) continue;
             const uint8_t *src = ib + (pos[u] & ~3ull);
             const uint64_t gofs = (uint64_t) (src - in);
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_tight2(
         const uint32_t z = __builtin_amdgcn_alignbyte(w[u].w, w[u].z, s);
         uint4 c = enc_quad(tab, x, y, z);
         if (r != 0 && pp[u] + 16 >= E) c = enc_seam2(tab, x, y, z, c, pp[u], E, r, a);
-        store16<true>(out + 16 * (s0 + u * kThreads + threadIdx.x), c);
+        store16<true>(out + 16 * (s0 + (u * kThreads + threadIdx.x)), c);
     }
 }
 
@@ -3325,7 +3325,7 @@ void k_decode_rows_lines(
     uint32_t bl[U], qq[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t rel = q0 + u * kThreads + threadIdx.x;
+        const uint32_t rel = q0 + (u * kThreads + threadIdx.x);
         if (rcpS) {
             bl[u] = __umul24(rel, rcpS) >> 20;
             qq[u] = rel - __umul24(bl[u], S);
@@ -3337,7 +3337,7 @@ void k_decode_rows_lines(
     if (s0 + U * kThreads > tail_slot) {
         // tail block: page-safe loads, decoded bytes only
         for (int u = 0; u < U; u++) {
-            const uint64_t t = s0 + u * kThreads + threadIdx.x;
+            const uint64_t t = s0 + (u * kThreads + threadIdx.x);
             const uint32_t q = qq[u];
             const bool live = t < nslots;
             const bool last = q == S - 1;
@@ -3366,15 +3366,34 @@ void k_decode_rows_lines(
     for (int u = 0; u < U; u++)
         w[u] = ld16<true>(O32 ? ib + (__umul24(bl[u], (uint32_t) in_stride) + 16 * qq[u])
                               : ib + (uint64_t) bl[u] * in_stride + 16 * qq[u]);
+    // the last slot's rule as a mask test (the band path's): bits 7.. of
+    // the invalid mask over its nlast characters must be exactly those past
+    // row 0's j0
+    const uint32_t ckm = 128u * (nlast >= 16 ? 0xFFFFu : (1u << nlast) - 1u);
+    const uint32_t cexp = j0 == kNoRowShape ? 1u : ckm & ~(128u * ((1u << j0) - 1u));
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t q = qq[u];
         const bool last = q == S - 1;
-        uint32_t G[4], A[4];
-        map_fast_acc(tab, w[u], G, A);
-        uint32_t k = 16;
-        bool ok = ((A[0] | A[1] | A[2] | A[3]) & ~63u) == 0;
-        if (last) ok = row_last_slot(tab, w[u], A, G, nlast, k) && k == j0;
+        // packed table values: groups by v_dot4 of their low 6 bits (a
+        // non-alphabet character contributes 63 inside its own field, past
+        // a passing last slot's bytes), the invalid mask by v_dot4 of the
+        // bit 7s; the row's last slot by a mask test, no branch (the
+        // per-lane row_last_slot branch cost 6 us per config-4 batch,
+        // profiles/r05_ab_rows_last.jsonl)
+        const uint32_t dw[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+        uint32_t G[4], m128 = 0;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t P = tab_pack4(tab, dw[g]);
+            const uint32_t Pz = P & 0x3F3F3F3Fu;
+            G[g] = (__builtin_amdgcn_udot4(Pz, 0x00000140u, 0u, false) << 12) |
+                   __builtin_amdgcn_udot4(Pz, 0x01400000u, 0u, false);
+            const uint32_t wt = (g & 1) ? 0x80402010u : 0x08040201u;
+            const uint32_t part = __builtin_amdgcn_udot4(P & 0x80808080u, wt, 0u, false);
+            m128 += (g & 2) ? part << 8 : part;
+        }
+        const bool ok = (last ? (m128 & ckm) ^ cexp : m128) == 0;
         uint32_t o0, o1, o2;
         groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
         uint8_t *dst = O32 ? ob + (__umul24(bl[u], (uint32_t) out_stride) + __umul24(q, 12u))
@@ -3901,7 +3920,9 @@ int b64x_encode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (slots > 0xFFFFFFFFull - 4096) return -EINVAL;
     const DeviceInfo *d = device_info();
     if (!d) return -ENODEV;
-    constexpr int U = 2;  // output slots per lane of k_encode_tight2
+    // output slots per lane of k_encode_tight2 (1: +9 %, 4: +5 % on config
+    // 4, profiles/r05_ab_tight_shapes.jsonl)
+    constexpr int U = 2;
     const EncAlpha ea = enc_alpha(abc);
     const uint64_t E = b64x_encoded_len(len, ea.pad);
     const uint32_t r = (uint32_t) (len % 3);
@@ -4961,11 +4982,22 @@ void b64x_lane_release(b64x_lane *l)
     b64x_lane_close(l);
 }
 
-// Grow a device buffer to at least `need` (rounded up: growth is rare).
-static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need)
+// Grow a device buffer to at least `need`, and on first use at least to
+// `floor`: the size the hub's default batches need (16 MiB arenas, 2^16 jobs,
+// 2^14 lent segments), so that a lane taken from the pool by another loop
+// does not grow under load.  Growing synchronises the lane's stream and
+// frees the old buffer (hipFree waits for the whole device); under config 5
+// on 16 loops the lanes' growth and the arenas' allocation made passes
+// 10-20 % slower now and then.
+constexpr uint64_t kLaneInFloor = (16u << 20) + (1u << 20);
+constexpr uint64_t kLaneOffsFloor = 3ull * ((1u << 16) + 1) * 8;
+constexpr uint64_t kLaneFlagsFloor = (1u << 16) + 64;
+constexpr uint64_t kLaneSegFloor = (1u << 14) * sizeof(b64x_seg);
+static int lane_grow(b64x_lane *l, void **buf, uint64_t *cap, uint64_t need, uint64_t floor)
 {
     if (need <= *cap) return 0;
     uint64_t want = need + need / 4 + (1u << 20);
+    if (want < floor) want = floor;
     int err;
     if ((err = hip_err(hipStreamSynchronize(l->stream)))) return err;
     if (*buf) (void) hipFree(*buf);
@@ -4984,8 +5016,9 @@ static int lane_stage_in(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
     const uint64_t in_bytes = h_in_off[njobs];
     const uint64_t words = (uint64_t) njobs + 1;
     int err;
-    if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64))) return err;
-    if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, (2 * words + words_extra) * 8)))
+    if ((err = lane_grow(l, (void **) &l->d_in, &l->in_cap, in_bytes + 64, kLaneInFloor))) return err;
+    if ((err = lane_grow(l, (void **) &l->d_offs, &l->offs_cap, (2 * words + words_extra) * 8,
+                          kLaneOffsFloor)))
         return err;
     if ((err = hip_err(hipMemcpyAsync(l->d_offs, h_in_off, words * 8, hipMemcpyHostToDevice,
                                       l->stream))) ||
@@ -5075,7 +5108,8 @@ int b64x_lane_encode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
         if ((err = lane_stage_in(l, nseg ? nullptr : h_in, njobs, h_in_off, h_out_off, 0)))
             return err;
         if (nseg && in_bytes) {
-            if ((err = lane_grow(l, (void **) &l->d_seg, &l->seg_cap, (uint64_t) nseg * sizeof(b64x_seg))) ||
+            if ((err = lane_grow(l, (void **) &l->d_seg, &l->seg_cap, (uint64_t) nseg * sizeof(b64x_seg),
+                               kLaneSegFloor)) ||
                 (err = hip_err(hipMemcpyAsync(l->d_seg, h_seg, (size_t) nseg * sizeof(b64x_seg),
                                               hipMemcpyHostToDevice, l->stream))))
                 return err;
@@ -5127,7 +5161,7 @@ int b64x_lane_decode_async(b64x_lane *l, const uint8_t *h_in, uint32_t njobs,
         const uint64_t words = (uint64_t) njobs + 1;
         for (uint32_t j = 0; j < njobs; j++) b64x_poison_result(h_res + j);
         if ((err = lane_stage_in(l, h_in, njobs, h_in_off, h_out_off, words))) return err;
-        if ((err = lane_grow(l, (void **) &l->d_flags, &l->flags_cap, njobs))) return err;
+        if ((err = lane_grow(l, (void **) &l->d_flags, &l->flags_cap, njobs, kLaneFlagsFloor))) return err;
         if ((err = hip_err(hipMemcpyAsync(l->d_flags, h_flags, njobs, hipMemcpyHostToDevice,
                                           l->stream))))
             return err;

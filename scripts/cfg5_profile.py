@@ -20,7 +20,12 @@ Three timed passes under ASYNC_B64_HUB_TRACE=1, each broken into phases:
 then one pass under the harness's SIGPROF sampler (the loop thread's CPU
 time by function).
 
-    python scripts/cfg5_profile.py OUTDIR
+    python scripts/cfg5_profile.py OUTDIR [--passes K] [--threads T] [--no-prof]
+           [--no-trace]
+
+--threads T runs the stacks on T loops (one hub each; the hub rows are
+summed over them); --no-trace times the passes without the hub trace (the
+bench's own conditions), so only setup_s / loop_s are reported.
 """
 import ctypes
 import json
@@ -35,7 +40,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["ASYNC_B64_HUB_TRACE"] = "1"
+if "--no-trace" not in sys.argv:
+    os.environ["ASYNC_B64_HUB_TRACE"] = "1"
 
 import torch  # noqa: E402,F401  (one HIP runtime, see async_amd/_lib.py)
 
@@ -65,20 +71,32 @@ def parse(line):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/cfg5prof"
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out", nargs="?", default="gpurun_out/cfg5prof")
+    ap.add_argument("--passes", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--no-trace", action="store_true")
+    a = ap.parse_args()
+    out = a.out
     os.makedirs(out, exist_ok=True)
     lens = util.zipf_lengths()
     payload = util.splitmix64(0x5EED, int(lens.sum()))
     H = util.harness()
+    T = a.threads
     util.egress_stacks(payload[:4096], [64] * 64, 1 << 20, 10240)  # warm-up
-    util.egress_stacks(payload, lens, 1 << 20, 10240, raw=True)    # pools filled
+    util.egress_stacks(payload, lens, 1 << 20, 10240, raw=True, threads=T)  # pools filled
+    H.b64_hub_pooled.restype = ctypes.c_ulong
     rows = []
-    for _ in range(3):
+    for _ in range(a.passes):
+        pooled0 = H.b64_hub_pooled()
         t = np.zeros(2)
         H.h_take_read_seconds(None)
         t0 = time.perf_counter()
         (res, err), lines = hub_lines(
-            lambda: util.egress_stacks(payload, lens, 1 << 20, 10240, times=t, raw=True))
+            lambda: util.egress_stacks(payload, lens, 1 << 20, 10240, times=t, raw=True,
+                                       threads=T))
         wall = time.perf_counter() - t0
         assert res is not None, err
         nreads = ctypes.c_ulong()
@@ -95,12 +113,19 @@ def main():
                "reserve_s": hub.get("reserve_s"), "launch_s": hub.get("launch_s"),
                "wake_s": hub.get("wake_s"), "batches": hub.get("batches"),
                "gpu_span_s": hub.get("span_s"), "lent_bytes": hub.get("lent_bytes"),
+               "arena_allocs": hub.get("allocs"), "hubs": len(lines),
+               "arenas_live_max_sum": hub.get("max_live"),
+               "pooled_before": pooled0, "pooled_after": H.b64_hub_pooled(),
                "other_s": t[1] - read_s - hub.get("wake_s", 0.0)}
+        row["threads"] = T
         rows.append(row)
         print(json.dumps(row), flush=True)
-    with open(os.path.join(out, "cfg5_phases.jsonl"), "w") as f:
+        del res
+    with open(os.path.join(out, f"cfg5_phases_t{T}.jsonl"), "w") as f:
         for r in rows:
             f.write(json.dumps(r) + "\n")
+    if a.no_prof:
+        return
     H.h_prof_start(2000)
     t = np.zeros(2)
     util.egress_stacks(payload, lens, 1 << 20, 10240, times=t, raw=True)

@@ -8,6 +8,6 @@ TAG=${TAG:-bab}
 K=${PYTEST_K:-"workspace or capture or graph or strided"}
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "$K" > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/${TAG}_pytest.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 900 python scripts/ab_batch.py --rounds ${ROUNDS:-3} "$@" > gpurun_out/${TAG}_ab.jsonl 2>&1
+timeout -k 10 900 python scripts/ab_batch.py --rounds ${ROUNDS:-3} ${ABARGS} "$@" > gpurun_out/${TAG}_ab.jsonl 2>&1
 rc=$?; grep summary gpurun_out/${TAG}_ab.jsonl; [ $rc -ne 0 ] && exit $rc
 echo ALLDONE
