@@ -39,7 +39,7 @@ OBJDIR   = build
 KERNEL_SRC = async_amd/csrc/b64x_kernels.hip
 HOST_SRC   = async_amd/csrc/fsalloc.c async_amd/csrc/loop.c async_amd/csrc/streams.c \
              async_amd/csrc/framing.c async_amd/csrc/fdstreams.c async_amd/csrc/b64_hub.c \
-             async_amd/csrc/b64_stages.c async_amd/csrc/b64_pin.c async_amd/csrc/b64_copy.c
+             async_amd/csrc/b64_stages.c async_amd/csrc/b64_pin.c
 HEADERS    = $(wildcard include/*.h)
 
 HOST_OBJ   = $(patsubst async_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRC))
@@ -60,8 +60,7 @@ $(OBJDIR):
 $(OBJDIR)/b64x_kernels.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h async_amd/csrc/b64_pin.h \
-              async_amd/csrc/b64_copy.h | $(OBJDIR)
+$(OBJDIR)/%.o: async_amd/csrc/%.c $(HEADERS) async_amd/csrc/b64_hub.h async_amd/csrc/b64_lend.h async_amd/csrc/b64_pin.h | $(OBJDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(OBJDIR)/b64x_kernels_hooks.o: $(KERNEL_SRC) $(HEADERS) async_amd/csrc/b64x_result_check.h | $(OBJDIR)
@@ -73,8 +72,7 @@ $(HOOKS): $(OBJDIR)/b64x_kernels_hooks.o
 $(LIB): $(OBJDIR)/b64x_kernels.o $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64.so
 
-$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_hub.o $(OBJDIR)/b64_stages.o $(OBJDIR)/b64_pin.o \
-         $(OBJDIR)/b64_copy.o
+$(CORE): $(OBJDIR)/b64x_kernels.o $(OBJDIR)/b64_hub.o $(OBJDIR)/b64_stages.o $(OBJDIR)/b64_pin.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,libasync_b64_core.so
 
 $(ORACLE): oracle/b64_oracle.c oracle/b64_oracle.h

@@ -81,7 +81,6 @@
 #include "async.h"
 #include "b64_hub.h"
 #include "b64_lend.h"
-#include "b64_copy.h"
 #include "b64_pin.h"
 #include "b64_trace.h"
 #include "b64x.h"
@@ -652,7 +651,7 @@ static size_t serve_body(stage *st, uint8_t *dst, size_t n)
         size_t take = sl->body_end - sl->out_pos;
         if (take > n - done)
             take = n - done;
-        b64_copy(dst + done, slot_out(sl) + sl->out_pos, take);
+        memcpy(dst + done, slot_out(sl) + sl->out_pos, take);
         sl->out_pos += take;
         done += take;
         if (sl->out_pos == sl->out_len)

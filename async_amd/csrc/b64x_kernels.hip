@@ -2214,18 +2214,14 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
         T += (int) bits_step<true>(sm, bits, ch, nh, pb0 + 6 * T);
     }
     bool at_end = last;
-    // The next range's copy (la_lds) is waited for here, before this range's
-    // stores are issued: vmcnt counts stores too on gfx9, so a wait after
-    // them (the caller's, at the next range) would also wait for every one of
-    // them to be written.  The caller does not wait again.
-    if (la_lds) vm_wait_all();
     if (!last && T > 0 && (T & 3)) {
         // complete the range's last group from the characters after it:
         // given (la, la_ok), in LDS at la_lds (the next range, whole, copied
         // there by k_decode_suffix while this range decoded: waited for
-        // above), or read from `in` only now (la_late)
+        // now), or read from `in` only now (la_late)
         bool ok = la_ok;
         if (la_lds) {
+            vm_wait_all();
             ok = true;
             la = la_lds[lane];
         } else if (la_late) {
@@ -2468,44 +2464,8 @@ void k_decode_suffix(
 
     // Count tile t into s_cnt[b] (each wave its kFusePer ranges; every
     // wave's loads issued before any is counted).  Block-uniform call.
-    const bool a4 = (((uintptr_t) in) & 3) == 0;
     auto count_tile = [&](uint32_t t, uint32_t b) {
         const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
-        if (a4 && (uint64_t) rw * R >= S && (uint64_t) (rw + kFusePer) * R <= n &&
-            rw + kFusePer <= nranges) {
-            // every range of the wave whole and inside [S, n): unguarded
-            // 16-byte loads and lookups of 16 characters each (the guarded
-            // form's per-chunk bounds and byte paths cost VALU and SALU per
-            // range; the kernel is issue-bound)
-            for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
-                uint4 c[kFuseLoad][2];
-#pragma unroll
-                for (uint32_t jj = 0; jj < kFuseLoad; jj++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++)
-                        c[jj][h] = load16_a4(in + (uint64_t) (rw + j0 + jj) * R + h * kChunk + 16 * lane);
-#pragma unroll
-                for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
-                    uint32_t cnt = 0;
-#pragma unroll
-                    for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            uint32_t P[4];
-                            lane_values(sm.tab, c[jj + e][h], 16u, P);
-                            cnt += lane_valid_count(P) << (16 * e);
-                        }
-                    }
-                    const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
-                        (int) wave_incl_scan_dpp(cnt), 63);
-                    if (lane == 0) {
-                        s_cnt[b][wv * kFusePer + j0 + jj] = tot & 0xFFFFu;
-                        s_cnt[b][wv * kFusePer + j0 + jj + 1] = tot >> 16;
-                    }
-                }
-            }
-            return;
-        }
         for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
             uint4 c[kFuseLoad][2];
             uint32_t nin[kFuseLoad][2];
@@ -2615,7 +2575,6 @@ void k_decode_suffix(
             lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
         };
         if (whole(rw)) fetch(rw, 0);
-        bool landed = false;  // this range's copy was waited for by decode_range
         for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
             const uint32_t r = rw + j;
             const uint64_t rb = (uint64_t) r * R;
@@ -2631,7 +2590,7 @@ void k_decode_suffix(
             // on the copied path too.  A whole range waits for its copy; any
             // other is loaded here (and waited for) and written there.
             if (whole(r)) {
-                if (!landed) vm_wait_all();
+                vm_wait_all();
             } else {
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -2649,7 +2608,6 @@ void k_decode_suffix(
             decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
                          base_out + (B + 3) / 4 * 3, c, nin, 0u, !last, last, hold,
                          next_dma ? (const uint8_t *) s_rng[wv][(j + 1) & 1] : nullptr, true);
-            landed = next_dma;
             B += s_cnt[bA][wv * kFusePer + j];
         }
         if (tA == ntiles - 1) {

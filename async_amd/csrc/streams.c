@@ -18,7 +18,6 @@
 #include <string.h>
 
 #include "b64_lend.h"
-#include "b64_copy.h"
 #include "b64_pin.h"
 #include "blobstream.h"
 #include "bytestream_1.h"
@@ -110,7 +109,7 @@ ssize_t blobstream_read(blobstream_t *b, void *buf, size_t count)
     if (n > count)
         n = count;
     if (n)
-        b64_copy(buf, b->data + b->pos, n);
+        memcpy(buf, b->data + b->pos, n);
     b->pos += n;
     return (ssize_t) n;
 }

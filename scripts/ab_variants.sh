@@ -13,7 +13,7 @@ mkdir -p "$d"
     -Iasync_amd/csrc -Iinclude -Wno-pass-failed -mllvm -amdgpu-kernarg-preload-count=16 $* -c async_amd/csrc/b64x_kernels.hip -o "$d/k.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$d/libasync_b64.so" "$d/k.o" \
     build/fsalloc.o build/loop.o build/streams.o build/framing.o build/fdstreams.o build/b64_hub.o \
-    build/b64_stages.o build/b64_pin.o build/b64_copy.o \
+    build/b64_stages.o build/b64_pin.o \
     -Wl,-soname,libasync_b64.so
 rm -f "$d/k.o"
 echo "$d/libasync_b64.so"

@@ -480,26 +480,3 @@ def test_pinned_message_pool_is_bounded(tmp_path, cap):
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.startswith("ok"), p.stdout
 
-
-def test_split_copy_is_a_copy():
-    """b64_copy (async_amd/csrc/b64_copy.c): copies of at least the split
-    size are shared with helper threads and must still be exact copies --
-    any length, any misalignment of either end, back to back, and with the
-    helpers asleep between calls."""
-    import time
-    L = fake()
-    L.b64_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
-    L.b64_copy.restype = None
-    rng = np.random.default_rng(17)
-    src = rng.integers(0, 256, (8 << 20) + 257, dtype=np.uint8)
-    sizes = [1, 100, (128 << 10) - 1, 128 << 10, (128 << 10) + 1, 300_001, 1 << 20,
-             (3 << 20) + 7, 8 << 20, 1663490, 661825]  # (the last two lost bytes once)
-    sizes += [int(x) for x in rng.integers(128 << 10, 2 << 20, 400)]
-    for i, n in enumerate(sizes):
-        so, do = int(rng.integers(0, 64)), int(rng.integers(0, 64))
-        dst = np.zeros(n + 128, dtype=np.uint8)
-        L.b64_copy(dst.ctypes.data + do, src.ctypes.data + so, n)
-        assert np.array_equal(dst[do:do + n], src[so:so + n]), n
-        assert not dst[:do].any() and not dst[do + n:].any(), n
-        if i == 5:
-            time.sleep(0.3)  # helpers go to sleep; the next split wakes them
