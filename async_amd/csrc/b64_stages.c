@@ -118,6 +118,7 @@ struct stage {
     direction dir;
     b64x_alphabet abc;
     size_t cap, min_pull, max_cap;
+    size_t grow_max;    /* a stream whose blocks fill grows its blocks to this */
     size_t lend_min;    /* encoder: pinned messages this long are lent */
     b64_hub *hub;       /* the loop's batching hub */
     unsigned hub_waits; /* entries on the hub's waiter list (room for a block) */
@@ -207,6 +208,11 @@ static void stage_init(stage *st, async_t *async, bytestream_1 up,
     st->min_pull = env_size("ASYNC_B64_MIN_PULL", (size_t) 64 << 10, 1);
     st->lend_min = env_size("ASYNC_B64_LEND_MIN", 4096, 1);
     st->max_cap = env_size("ASYNC_B64_STAGE_MAX_CAPACITY", (size_t) 64 << 20, 64);
+    /* an explicit block size stays fixed unless growth is asked for too */
+    st->grow_max = env_size("ASYNC_B64_STAGE_GROW_MAX",
+                            getenv("ASYNC_B64_STAGE_CAPACITY") ? st->cap : (size_t) 8 << 20, 64);
+    if (st->grow_max < st->cap)
+        st->grow_max = st->cap;
     st->skip = skip_char(&abc);
     b64_pin_activate(); /* queued messages are pinned for GPU stages from now on */
     for (int i = 0; i < NSLOTS; i++)
@@ -392,6 +398,24 @@ static size_t gather(stage *st, uint8_t *in, size_t at, size_t room, bool *eof, 
     return got;
 }
 
+/* A block that took all the room it asked for (upstream kept up) doubles
+ * the next one, up to grow_max: one long stream then moves in a few large
+ * blocks instead of many 1 MiB ones.  A stream's blocks are chained on one
+ * lane (its carry), so each block is a serial round trip -- H2D, the
+ * decode's kernels, the completion -- of 140 us or so at 1 MiB, and one
+ * stream through the stages was bound by that, not by the copies: 1 GiB of
+ * characters from memory 5.1 GiB/s with 1 MiB blocks, 8.5 with 4 MiB, 9.1
+ * with 8 MiB; through an AF_UNIX socket 5.0 / 7.4 / 8.4
+ * (profiles/r05_host_fd_stage_cap_*).  Messages that do not fill a block
+ * (config 5's, a short read) never grow it. */
+static void grow_block(stage *st, size_t granted, size_t asked, bool filled)
+{
+    if (filled && granted == asked && st->cap < st->grow_max) {
+        size_t c = 2 * st->cap;
+        st->cap = c < st->grow_max ? c : st->grow_max;
+    }
+}
+
 static slot *next_launch_slot(stage *st)
 {
     if (st->nbusy >= NSLOTS || st->final_queued)
@@ -463,8 +487,10 @@ static int top_up_encoder(stage *st)
         memcpy(in, st->carry, st->ncarry);
         bool eof;
         int uerr;
+        const size_t asked = st->cap;
         size_t got = gather(st, in, st->ncarry, room - st->ncarry, &eof, &uerr);
         size_t total = st->ncarry + got;
+        grow_block(st, room, asked, !eof && !uerr && total == room);
         /* The block encodes all `total` bytes.  Its full sextets,
          * floor(8*total/6) characters, are served now -- the reference
          * emits them in the read that brought the bytes in
@@ -538,6 +564,7 @@ static int top_up_decoder(stage *st)
         bool eof;
         int uerr;
         size_t got = gather(st, in, DEC_HEAD, room - DEC_HEAD, &eof, &uerr);
+        grow_block(st, room, want, !eof && !uerr && got == room - DEC_HEAD);
         if (eof) {
             st->final_queued = true;
             if (got == 0 && !pending && st->ncarry == 0) { /* nothing held back: done */

@@ -28,10 +28,14 @@ def test_stage_read_counts_match_reference(case, burst):
     assert got == want
 
 
+@pytest.mark.parametrize("grow", [1, 16])
 @pytest.mark.parametrize("cap", [64, 4096])
 @pytest.mark.parametrize("seed", range(4))
-def test_stage_read_counts_small_slots(monkeypatch, cap, seed):
+def test_stage_read_counts_small_slots(monkeypatch, cap, seed, grow):
+    """Read counts with small blocks, fixed or growing while upstream keeps
+    up (ASYNC_B64_STAGE_GROW_MAX): the reference's counts either way."""
     monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+    monkeypatch.setenv("ASYNC_B64_STAGE_GROW_MAX", str(cap * grow))
     monkeypatch.setenv("ASYNC_B64_MIN_PULL", "1")
     rng = np.random.default_rng(seed)
     n = int(rng.integers(0, 50000))

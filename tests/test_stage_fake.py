@@ -96,6 +96,23 @@ def test_long_decoder_streams_adversarial_orders(small_blocks, seed, pct):
         assert early == batches and counters(L)[1] - e0[1] == batches
 
 
+@pytest.mark.parametrize("seed,pct", [(4, 30), (5, 100)])
+def test_long_decoder_streams_growing_blocks(monkeypatch, seed, pct):
+    """The same streams with blocks that start at 256 characters and double
+    while upstream keeps up (ASYNC_B64_STAGE_GROW_MAX): carries and chains
+    across blocks of changing sizes, adversarial completion orders; every
+    stream is the oracle's."""
+    monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", "256")
+    monkeypatch.setenv("ASYNC_B64_STAGE_GROW_MAX", str(1 << 16))
+    L = fake()
+    L.fake_configure(seed, pct, 0)
+    msgs = long_msgs(seed, n=120) + [orc.encode(np.random.default_rng(seed).integers(
+        0, 256, 300_000, dtype=np.uint8).tobytes())]
+    got, err = util.ingress_stacks(msgs, 4096, lib=L)
+    assert err == 0
+    assert bad_streams(msgs, got) == []
+
+
 @pytest.mark.parametrize("mode,seed", [(2, 31), (3, 32)])
 def test_zero_and_torn_records_are_rejected(small_blocks, mode, seed):
     """Early callbacks that find a well-formed all-zero record (mode 2: what
@@ -373,13 +390,16 @@ def test_egress_lent_fuzz(monkeypatch):
     message (smaller blocks than one copying read would fill, so a short
     read count and other chunk sizes than the reference's)."""
     L = fake()
-    for seed in range(24):
+    for seed in range(48):
         rng = np.random.default_rng(0xF0221 + seed)
         k = int(rng.integers(1, 40))
         sizes = [0 if rng.random() < 0.05 else int(np.exp(rng.uniform(0, np.log(1.5 * 2**20))))
                  for _ in range(k)]
         pieces = [rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]
-        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(int(rng.choice([64, 1000, 4096, 65536, 1 << 20]))))
+        cap = int(rng.choice([64, 1000, 4096, 65536, 1 << 20]))
+        monkeypatch.setenv("ASYNC_B64_STAGE_CAPACITY", str(cap))
+        # blocks that fill grow (up to 8x or 64x), or stay fixed
+        monkeypatch.setenv("ASYNC_B64_STAGE_GROW_MAX", str(cap * int(rng.choice([1, 8, 64]))))
         monkeypatch.setenv("ASYNC_B64_LEND_MIN", str(int(rng.choice([1, 3, 4096, 65536]))))
         max_chunk = int(rng.choice([30, 4096, 65536, 1 << 20]))
         read_size = int(rng.choice([7, 1000, 10240, 1 << 18]))
