@@ -5696,8 +5696,11 @@ __global__ __launch_bounds__(TH) void k_test_mix(const uint8_t *__restrict__ in,
     uint32_t v[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint8_t *p = in + (u0 + (uint64_t) u * TH) * IN;
-        if (IN == 16) {
+        const uint8_t *p = in + (u0 + (uint64_t) u * TH) * (IN == 1612 ? 12 : IN);
+        if (IN == 1612) {  // 16 bytes at a 12-byte stride (k_encode_tight2's loads)
+            const u32x4a4 w = __builtin_nontemporal_load((const u32x4a4 *) p);
+            v[u][0] = w.x, v[u][1] = w.y ^ w.w, v[u][2] = w.z, v[u][3] = w.x ^ w.z;
+        } else if (IN == 16) {
             const uint4 w = ld16<true>(p);
             v[u][0] = w.x, v[u][1] = w.y, v[u][2] = w.z, v[u][3] = w.w;
         } else {
@@ -5727,8 +5730,9 @@ static int test_mix(const void *src, void *dst, uint64_t units, void *stream)
 }
 }  // extern "C++"
 
-// mix 0: encode's 12 -> 16, mix 1: decode's 16 -> 12; shape 0..2: U = 1, 2, 4
-// (TH = 256).  `units` must be a multiple of 256 * U.
+// mix 0: encode's 12 -> 16, mix 1: decode's 16 -> 12, mix 2: 16-byte loads
+// at a 12-byte stride -> 16 (k_encode_tight2's shape); shape 0..2: U = 1, 2,
+// 4 (TH = 256).  `units` must be a multiple of 256 * U.
 int b64x__test_copy_mix(const void *src, void *dst, uint64_t units, void *stream, int mix,
                         int shape)
 {
@@ -5739,6 +5743,9 @@ int b64x__test_copy_mix(const void *src, void *dst, uint64_t units, void *stream
     case 3: return test_mix<1, 256, 16, 12>(src, dst, units, stream);
     case 4: return test_mix<2, 256, 16, 12>(src, dst, units, stream);
     case 5: return test_mix<4, 256, 16, 12>(src, dst, units, stream);
+    case 6: return test_mix<1, 256, 1612, 16>(src, dst, units, stream);
+    case 7: return test_mix<2, 256, 1612, 16>(src, dst, units, stream);
+    case 8: return test_mix<4, 256, 1612, 16>(src, dst, units, stream);
     default: return -EINVAL;
     }
 }
@@ -5759,7 +5766,11 @@ const char *b64x_build_info(void)
 #define B64X_STR(x) B64X_STR2(x)
     return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
            "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
+#if B64X_SFX_HELD
+           "(decoded once, held until its prefix, group sums, LDS read-ahead); rows:line model in row "
+#else
            "(count ahead, group sums, LDS read-ahead); rows:line model in row "
+#endif
            "bands; lanes:chained decoder blocks";
 }
 
