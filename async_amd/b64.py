@@ -205,6 +205,15 @@ def decode_batch(x: torch.Tensor, in_off: torch.Tensor, out: torch.Tensor,
         _ptr(out_off), _ptr(outlen), ctypes.byref(a), _stream(stream)))
 
 
+def release_stream(stream=None) -> None:
+    """Hand back the library decode workspace bound to `stream`
+    (b64x_release_stream): call it before destroying a stream that decoded
+    without a workspace of its own, so the workspace is free at once instead
+    of when the least recently used one is taken over.  The next decode on
+    the stream binds one again; work already queued is not affected."""
+    _lib.load().b64x_release_stream(_stream(stream))
+
+
 def fill_splitmix64(x: torch.Tensor, seed: int, stream=None) -> torch.Tensor:
     """Fill a device buffer with the synthetic splitmix64 byte stream."""
     lib = _lib.load()

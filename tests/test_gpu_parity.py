@@ -1305,6 +1305,29 @@ def test_library_workspace_is_bounded():
     lib.b64x_release_stream(ctypes.c_void_p(keep[5].cuda_stream))
 
 
+def test_release_stream_from_python():
+    """b64.release_stream(): a stream that decoded with the
+    library workspace hands it back while its decode may still be queued;
+    the next decode on the stream binds one again; every result is exact."""
+    rng = np.random.default_rng(91)
+    s = torch.cuda.Stream()
+    raws = [rng.integers(0, 256, 200_000 + 777 * k, dtype=np.uint8) for k in range(4)]
+    texts = [dev(orc.encode(r)) if k % 2 else dev(_junk(rng, orc.encode(r), 0.02))
+             for k, r in enumerate(raws)]
+    outs = [torch.zeros(b64.decoded_cap(t.numel()) + 8, dtype=torch.uint8, device=DEV)
+            for t in texts]
+    ress = [torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV) for _ in texts]
+    torch.cuda.synchronize()
+    for t, o, r in zip(texts, outs, ress):
+        b64.decode(t, out=o, result=r, stream=s)
+        b64.release_stream(s)
+    torch.cuda.synchronize()
+    for raw, o, r in zip(raws, outs, ress):
+        assert b64.Decoded(o, r).info().out_len == raw.size
+        assert np.array_equal(o[:raw.size].cpu().numpy(), raw)
+    b64.release_stream(s)  # nothing bound: a no-op
+
+
 def test_library_workspace_threads_past_the_cache():
     """12 threads, each decoding on its own stream with d_workspace == NULL
     (more streams than the 8 cached workspaces, so entries are evicted while
