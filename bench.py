@@ -68,7 +68,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s base64 encode+decode, device-resident, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ROUND = "r04"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
+ROUND = "r05"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
 
 
 def parse():
@@ -1127,7 +1127,7 @@ def main():
         dom_ms = max(r["enc_ms"], r["dec_ms"])
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         knames = ["k_encode_flat"] if dom == "encode" else \
-            ["k_decode_probe", "k_decode_lines", "k_decode_suffix"]
+            ["k_decode_probe", "k_decode_lines", "k_decode_suffix_held"]
         out = {
             "metric": METRIC,
             "value": world * N * K / r["wall"] / 2**30,
