@@ -625,18 +625,25 @@ def bench_mime(args, b64, steps=20):
 
     spread = {}
 
-    def timed(fn, name):
+    def timed(fn, name, sync_each=False):
+        # calls back to back, each between two events of its own, one host
+        # sync at the end (a sync after every call left the GPU idle between
+        # calls, and the call after a longer host pause ran slow); the junk
+        # legs sync after every call, so that each call finds the hint its
+        # predecessor's probe left (the path the host picks reads it)
         fn()
         preheat()
         torch.cuda.synchronize()
-        ts = []
-        for _ in range(steps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        for e0, e1 in evs:
             e0.record(stream)
             fn()
             e1.record(stream)
-            e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
+            if sync_each:
+                e1.synchronize()
+        torch.cuda.synchronize()
+        ts = [e0.elapsed_time(e1) for e0, e1 in evs]
         spread[name] = {"ms_min": min(ts), "ms_median": statistics.median(ts), "ms_max": max(ts)}
         return statistics.median(ts)
 
@@ -666,7 +673,7 @@ def bench_mime(args, b64, steps=20):
         out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device="cuda")
         ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device="cuda")
         ms_j = timed(lambda: b64.decode(text, out=out, workspace=ws, result=res, stream=stream),
-                     f"cfg2_junk{d:g}")
+                     f"cfg2_junk{d:g}", sync_each=True)
         info = b64.Decoded(out, res).info()
         if info.out_len != N or not torch.equal(out[:N], x):
             raise SystemExit(f"junk {d} decode mismatch")
