@@ -27,9 +27,10 @@
 //     = output bytes [12t, 12t+12)), loads each slot's span, drops the
 //     separator with funnel shifts, checks it and stores 12 bytes, and
 //     publishes the first slot that does not fit the model;
-//     k_decode_suffix decodes exactly whatever follows that slot (nothing,
-//     on clean and MIME-formatted text): persistent tiles of 64 ranges of
-//     2,048 characters, counts, a decoupled look-back, and the range body
+//     k_decode_suffix_held decodes exactly whatever follows that slot
+//     (nothing, on clean and MIME-formatted text): persistent tiles of 16
+//     ranges of 2,048 characters, each decoded once and held in VGPRs until
+//     the tile's prefix (group sums) is known, and the range body
 //     that ORs each lane's compacted sextet fields into a wave's LDS window
 //     (v_perm compaction, v_dot4 fields, ds_or) -- the window's bytes are
 //     the output bytes.  Larger inputs: pass 1 (input-indexed fast paths),
@@ -632,6 +633,19 @@ DEV void wave_lds_order()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// __syncthreads() with every LDS access of this wave done first.  hipcc's
+// barrier for a workgroup-scope release did not always wait for them: in
+// k_decode_suffix_held's loop the barrier at the top of an iteration had no
+// lgkmcnt(0) behind thread 0's write of the next tile's ticket at the end of
+// the last one, and now and then another wave read the old ticket after the
+// barrier (profiles/r05_sfx_held_stress*.jsonl: one 1 GiB decode in 5 wrong
+// at 3 ranges per wave, the waves' tickets seen differing; none with this).
+DEV void block_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 // Four groups -> 12 output bytes as three little-endian dwords.
 DEV void groups_to_bytes(uint32_t G0, uint32_t G1, uint32_t G2, uint32_t G3,
                          uint32_t &o0, uint32_t &o1, uint32_t &o2)
@@ -900,14 +914,28 @@ constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 constexpr uint32_t kFusePer = 8;
 constexpr uint32_t kFuseLoad = 4;  // of them loaded at once for counting
 constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
+// k_decode_suffix_held: ranges per wave of a tile (held in VGPRs, decoded;
+// 4 with 5 waves per SIMD, see there)
+#ifndef B64X_SFX_HP
+#define B64X_SFX_HP 4
+#endif
+#ifndef B64X_SFX_WPE
+#define B64X_SFX_WPE 5
+#endif
+#ifndef B64X_SFX_HELD
+#define B64X_SFX_HELD 1  // k_decode_suffix_held (0: the counting form)
+#endif
+constexpr uint32_t kHeldPer = B64X_SFX_HP;
+constexpr uint32_t kHeldTile = kHeldPer * kWavesPerBlock;
+constexpr uint32_t kSfxTileMin = kHeldTile < kFuseTile ? kHeldTile : kFuseTile;
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsModelN = 64;                                        // the model's stream length
 constexpr uint64_t kWsStatus = 128;                                       // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
 constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix: tiles per group sum
 constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
-constexpr uint64_t kWsFSuper = kWsFStatus + kMaxRanges / kFuseTile * 8;   // suffix group sums
-constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kFuseTile / kSfxGroup + 16) * 8;  // lines failures
+constexpr uint64_t kWsFSuper = kWsFStatus + (kMaxRanges / kSfxTileMin + 1) * 8;   // suffix group sums
+constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kSfxTileMin / kSfxGroup + 16) * 8;  // lines failures
 // failure words, fail_any, wdone: one 128-byte line each
 constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
@@ -2409,7 +2437,7 @@ DEV bool suffix_start(DecodeWs w, uint64_t n, b64x_dec_result *res, b64x_dec_res
             }
         }
         if (threadIdx.x == 0) s_key = key;
-        __syncthreads();
+        block_sync();
         key = s_key;
     }
     if (key == 0) {
@@ -2534,13 +2562,13 @@ void k_decode_suffix(
         }
     };
 
-    __syncthreads();  // the tables
+    block_sync();  // the tables
     if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
-    __syncthreads();
+    block_sync();
     uint32_t tA = s_tile[0], bA = 0;
     if (tA < ntiles) {
         count_tile(tA, 0);
-        __syncthreads();
+        block_sync();
         if (threadIdx.x == 0) publish(tA, 0);
     }
     bool owner = false;  // this block decoded the last tile
@@ -2548,16 +2576,16 @@ void k_decode_suffix(
     while (tA < ntiles) {
         const uint32_t bB = bA ^ 1u;
         if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
-        __syncthreads();  // also: s_cnt[bB] of two tiles back is consumed
+        block_sync();  // also: s_cnt[bB] of two tiles back is consumed
         const uint32_t tB = s_tile[bB];
         if (tB < ntiles) count_tile(tB, bB);
-        __syncthreads();
+        block_sync();
         if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
         if (wv == 0) {
             const uint32_t ex = tA ? prefix(tA) : 0u;
             if (lane == 0) s_excl = ex;
         }
-        __syncthreads();
+        block_sync();
         uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
         for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
         const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
@@ -2621,7 +2649,7 @@ void k_decode_suffix(
     // every prefix read of this block is over (relaxed: the loads have
     // returned -- their values decided the loop -- and a release at agent
     // scope would write back the L2)
-    __syncthreads();
+    block_sync();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!owner || wv != 0) return;
     const uint64_t V = Vb + Vs;
@@ -2637,6 +2665,342 @@ void k_decode_suffix(
         __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(w.wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (WHOLE too: after a probe, the hinted single pass, decode_dev_ws)
+        for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
+        *w.fail_any = 0;
+    }
+}
+
+// ---- single-pass exact decode, each range read and looked up once ----------
+//
+// k_decode_suffix_held: the same contract, tiles, ticket, group sums and
+// result record as k_decode_suffix, but no counting pass.  A range is
+// decoded once, at relative bit 0 of the wave's window (its prefix is not
+// known yet), and the window -- the range's output bit stream, at most
+// 1,536 bytes -- is held in VGPRs (6 dwords per lane) while the tile is
+// published and the next tile is decoded; the range's count comes out of
+// the decode.  A tile is stored one iteration later, when its prefix is
+// known (its predecessors have had a whole tile's time to publish): the
+// held dwords go back into the window, the range's last partial group is
+// completed from the characters after it (their raw bytes loaded when the
+// range was decoded), and the window is copied to the output shifted by
+// the range's skip (0-3 sextets the range before it completed) and the
+// output's alignment.  Each input byte is read from HBM once (the counting
+// form reads every range twice) and looked up once.  Shipped (B64X_SFX_HELD
+// = 1).  On 1 GiB at junk density 0.05 (profiles/r05_pmc_sfx_held.txt,
+// r05_ab_sfx_held*.jsonl): FETCH 1.02x the input against 2.01x, VALU -10 %,
+// SALU -27 %, LDS instructions -20 %, and the same time (747.5 / 778.4 us
+// against 746.2 / 771.7 in two A/B runs): the kernel is bound by latency at
+// 5 waves per SIMD (96 VGPRs, two tiles held while the next decodes), not
+// by its bytes.  The prefix is 12 % of it (a pricing build without it: 658
+// us).  Tried and slower: a tile's ticket drawn one iteration ahead (940
+// us), storing range j of A right after decoding range j of B (A's prefix
+// then needed one range after B is drawn: 2.2-2.8 ms, tiles waiting on
+// their predecessors), 3 or 2 ranges per wave (810 / 1,156 us), 4 waves per
+// SIMD without spills (835 us).  Its first form's barriers were hipcc's
+// __syncthreads(), and the one at the top of an iteration did not wait for
+// thread 0's write of the next ticket: now and then a wave decoded another
+// tile than its block (one repeated 1 GiB decode in five came out shifted;
+// block_sync()'s explicit lgkmcnt(0) fixed it: 96 + 96 stress decodes exact,
+// scripts/held_stress.py, profiles/r05_sfx_held_*.jsonl).
+
+// The window dword a range's held dwords go back to, so that
+// store_window_bits reads aligned 16-byte groups: the range's bits start at
+// bit s (its skip) and its output at dst.
+DEV uint32_t window_delta(uint32_t s, const uint8_t *dst)
+{
+    const uint32_t a = (uint32_t) ((uintptr_t) dst & 15);
+    const uint32_t i0 = (s + (a ? 128u : 0u) - 8 * a) >> 5;
+    return (4u - (i0 & 3u)) & 3u;
+}
+
+// Output bytes [0, nb) at dst are window bits [s, s + 8 nb) (big-endian
+// dwords, or_field<true>; s placed by window_delta): aligned 16-byte
+// blocks of dst, each four window dwords read as one aligned 16-byte LDS
+// read (consecutive lanes, consecutive 16-byte groups: no bank conflicts)
+// plus the next group's first dword from the next lane, funnel-shifted by
+// the same amount for every block; the partial blocks at both ends one byte
+// per lane.
+DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t *dst)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t a = (uint32_t) ((uintptr_t) dst & 15);
+    // block m of the aligned grid covers bytes [16 m - a, 16 m - a + 16)
+    const uint32_t m0 = a ? 1u : 0u, mend = (nb + a) >> 4;
+    const uint32_t sh = (s + 128 * m0 - 8 * a) & 31;  // the same for every block
+    const uint4 *win4 = (const uint4 *) win;
+    for (uint32_t m0l = m0; m0l < mend; m0l += 64) {
+        const uint32_t m = m0l + lane;
+        const uint32_t i = (s + 128 * m - 8 * a) >> 5;  // a multiple of 4
+        uint4 g = make_uint4(0, 0, 0, 0);
+        if (m < mend) g = win4[i >> 2];
+        uint32_t w4 = (uint32_t) __shfl_down((int) g.x, 1, 64);
+        if (m < mend && (lane == 63 || m + 1 >= mend)) w4 = win[i + 4];
+        auto f = [sh](uint32_t hi, uint32_t lo) {
+            return (uint32_t) ((((uint64_t) hi << 32) | lo) >> (32 - sh));
+        };
+        if (m < mend)
+            __builtin_nontemporal_store(u32x4a16{bswap32(f(g.x, g.y)), bswap32(f(g.y, g.z)),
+                                                 bswap32(f(g.z, g.w)), bswap32(f(g.w, w4))},
+                                        (u32x4a16 *) (dst - a + 16 * (uint64_t) m));
+    }
+    const uint32_t hend = a ? (16 - a < nb ? 16 - a : nb) : 0u;  // head bytes [0, hend)
+    const uint32_t tb = mend > m0 ? 16 * mend - a : hend;          // tail bytes [tb, nb)
+    uint32_t bi = 0;
+    bool act = false;
+    if (lane < 16) {
+        bi = lane;
+        act = bi < hend;
+    } else if (lane < 32) {
+        bi = (tb > hend ? tb : hend) + (lane - 16);
+        act = bi < nb;
+    }
+    if (act) {
+        const uint32_t X = s + 8 * bi;
+        const uint64_t W = ((uint64_t) win[X >> 5] << 32) | win[(X >> 5) + 1];
+        dst[bi] = (uint8_t) (W >> (56 - (X & 31)));
+    }
+}
+
+template <bool WHOLE>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
+void k_decode_suffix_held(
+    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
+    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
+    uint32_t seq, uint32_t *reprobe)
+{
+    constexpr uint64_t R = 2 * kChunk;
+    constexpr uint32_t HP = kHeldPer, TILE = kHeldTile;
+    DecodeWs w = ws_view(ws, nranges);
+    uint64_t S = 0, Vb = 0;
+    if (!WHOLE && !suffix_start(w, n, res, hres, S, Vb, reprobe)) return;
+    uint8_t *base_out = out + Vb / 4 * 3;
+    const uint32_t r0 = (uint32_t) (S / R);
+    const uint32_t ntiles = (nranges - r0 + TILE - 1) / TILE;
+    if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
+    const bool dma = (((uintptr_t) in) & 15) == 0;
+    __shared__ P2dSmem sm;
+    __shared__ uint4 s_rng[kWavesPerBlock][2][128];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_cnt[2][TILE];
+    __shared__ uint32_t s_excl;
+    build_dec_table(sm.tab, a);
+    build_compact_sel(sm.sel);
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *bq = sm.bits[wv];
+    uint32_t *bits = (uint32_t *) bq;
+
+    auto publish = [&](uint32_t t, uint32_t b) {
+        uint32_t agg = 0;
+        for (uint32_t i = 0; i < TILE; i++) agg += s_cnt[b][i];
+        st_store(&w.fstatus[t], kStAgg | agg);
+        __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto prefix = [&](uint32_t t) -> uint32_t {
+        const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
+        const uint32_t ng = (k + 63) / 64;
+        for (;;) {
+            const uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
+            bool ok = (v & kStAgg) != 0;
+            uint32_t sum = (uint32_t) v;
+            for (uint32_t i = 0; i < ng; i++) {
+                const uint32_t j = lane + 64 * i;
+                const uint64_t g = j < k ? st_load(&w.fsuper[j]) : kGroupFull;
+                ok = ok && (g >> 56) == kSfxGroup;
+                sum += (uint32_t) g;
+            }
+            if (__all(ok)) return wave_sum(sum);
+            __builtin_amdgcn_s_sleep(2);
+        }
+    };
+    auto whole = [&](uint32_t r) {
+        return dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
+    };
+    auto fetch = [&](uint32_t r, uint32_t buf) {
+        const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
+        lds_dma16(src, &s_rng[wv][buf][0]);
+        lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
+    };
+
+    // Decode range j of tile t (this wave's) into the window; hold its
+    // dwords [6 lane, 6 lane + 6) in Hn and the byte after its end at lane
+    // offset in lan (the completion's first look); count into s_cnt[b].
+    auto decode_one = [&](uint32_t rw, uint32_t j, uint32_t b, uint32_t Hn[6], uint32_t &lan) {
+        const uint32_t r = rw + j;
+        uint32_t T = 0;
+        lan = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) Hn[i] = 0;
+        if (r < nranges) {
+            const uint64_t rb = (uint64_t) r * R;
+            const uint64_t re = rb + R < n ? rb + R : n;
+            const uint64_t start = r == r0 ? S : rb;
+            const bool next_dma = j + 1 < HP && whole(r + 1);
+            uint4 *buf = s_rng[wv][j & 1];
+            uint32_t nin[2] = {16u, 16u};
+            lan = re + lane < n ? (uint32_t) in[re + lane] : 0u;
+            if (whole(r)) {
+                vm_wait_all();
+            } else {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
+                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
+                    buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
+                }
+            }
+            uint4 c[2];
+            c[0] = buf[lane];
+            c[1] = buf[64 + lane];
+            if (next_dma) fetch(r + 1, (j + 1) & 1);
+            wave_lds_order();
+            bq[lane] = make_uint4(0, 0, 0, 0);
+            if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
+            wave_lds_order();
+            T = bits_step<true>(sm, bits, c, nin, 0);
+            wave_lds_order();
+#pragma unroll
+            for (int i = 0; i < 6; i++) Hn[i] = bits[lane + 64 * i];  // consecutive lanes
+            wave_lds_order();
+        }
+        if (lane == 0) s_cnt[b][wv * HP + j] = T;
+    };
+    // Store range j of tile A (this wave's) from its held dwords: Bp = the
+    // suffix's alphabet characters before it, T its own.
+    auto store_one = [&](uint32_t r, uint32_t Bp, uint32_t T, const uint32_t Hj[6], uint32_t la) {
+        const uint64_t rb = (uint64_t) r * R;
+        const uint64_t re = rb + R < n ? rb + R : n;
+        const bool last = r + 1 == nranges;
+        const uint32_t k = (4u - (Bp & 3u)) & 3u;  // sextets the range before took
+        uint8_t *dst = base_out + (uint64_t) (Bp + k) / 4 * 3;
+        const uint32_t dl = window_delta(6 * k, dst);  // the held dwords go to dl..
+#pragma unroll
+        for (int i = 0; i < 6; i++) bits[dl + lane + 64 * i] = Hj[i];
+        if (lane < 8) bits[dl + 384 + lane] = 0;  // past 1,536 bytes: the completion's
+        wave_lds_order();
+        uint32_t Tc = T;
+        bool at_end = last;
+        if (!last && ((Bp + T) & 3u)) {
+            // complete the range's last group from the characters after it
+            bool ok = re + lane < n;
+            for (uint64_t q = re;;) {
+                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+                const bool v = t < 64u;
+                const uint64_t m = __ballot(v);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                const uint32_t need = 4u - ((Bp + Tc) & 3u);
+                if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 18);
+                const uint32_t got = (uint32_t) __popcll(m);
+                if (got >= need) {
+                    Tc += need;
+                    break;
+                }
+                Tc += got;
+                q += 64;
+                if (q >= n) {
+                    at_end = true;
+                    break;
+                }
+                ok = q + lane < n;
+                la = ok ? in[q + lane] : 0u;
+            }
+            wave_lds_order();
+        }
+        if (Tc > k) {
+            const uint32_t Tk = Tc - k;
+            const uint32_t rem = Tk & 3u;
+            const uint32_t tail = at_end && !hold && rem >= 2 ? rem - 1 : 0u;
+            store_window_bits(bits, 32 * dl + 6 * k, 3 * (Tk >> 2) + tail, dst);
+        }
+        wave_lds_order();
+    };
+
+    // Tile A (decoded, published, held: HA, LA, counts in s_cnt[bA]) is
+    // stored after tile B is drawn, decoded and published, so that A's
+    // predecessors have had a whole tile's time to publish.
+    // (LA: the bytes after each held range, byte j for range j)
+    uint32_t HA[HP][6], LA = 0;
+    static_assert(HP <= 4, "one byte per held range in LA");
+#pragma unroll
+    for (uint32_t j = 0; j < HP; j++) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) HA[j][i] = 0;
+    }
+    block_sync();  // the tables
+    bool haveA = false, owner = false;
+    uint32_t tA = 0, bA = 1, bB = 0, Vs = 0;
+    if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
+    for (;;) {
+        block_sync();  // the ticket; s_cnt[bB] (two tiles back) consumed
+        const uint32_t tB = s_tile[bB];
+        const bool haveB = tB < ntiles;
+        if (!haveA && !haveB) break;
+        uint32_t HB[HP][6], LB = 0;
+        if (haveB) {
+            const uint32_t rwB = r0 + tB * TILE + wv * HP;
+            if (whole(rwB)) fetch(rwB, 0);
+#pragma unroll
+            for (uint32_t j = 0; j < HP; j++) {
+                uint32_t lan;
+                decode_one(rwB, j, bB, HB[j], lan);
+                LB |= lan << (8 * j);
+            }
+        }
+        block_sync();  // s_cnt[bB] complete
+        if (haveB && threadIdx.x == 0) publish(tB, bB);
+        if (haveA) {
+            if (wv == 0) {
+                const uint32_t ex = tA ? prefix(tA) : 0u;
+                if (lane == 0) s_excl = ex;
+            }
+            block_sync();
+            uint32_t Bp = s_excl;
+            for (uint32_t i = 0; i < wv * HP; i++) Bp += s_cnt[bA][i];
+            const uint32_t rwA = r0 + tA * TILE + wv * HP;
+#pragma unroll
+            for (uint32_t j = 0; j < HP; j++) {
+                if (rwA + j < nranges) {
+                    const uint32_t T = s_cnt[bA][wv * HP + j];
+                    store_one(rwA + j, Bp, T, HA[j], (LA >> (8 * j)) & 0xFFu);
+                    Bp += T;
+                }
+            }
+            if (tA == ntiles - 1) {
+                owner = true;
+                Vs = s_excl;
+                for (uint32_t i = 0; i < TILE; i++) Vs += s_cnt[bA][i];
+            }
+        }
+        if (!haveB) break;
+        LA = LB;
+#pragma unroll
+        for (uint32_t j = 0; j < HP; j++) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) HA[j][i] = HB[j][i];
+        }
+        haveA = true;
+        tA = tB;
+        bA = bB;
+        bB ^= 1u;
+        if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
+    }
+    block_sync();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!owner || wv != 0) return;
+    const uint64_t V = Vb + Vs;
+    if (lane == 0) write_result(res, hres, V, hold, n, seq);
+    find_tail_sextets(sm.tab, in, n, V, res, hres);
+    if (lane == 0) {
+        while (__hip_atomic_load(w.wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
+    for (uint32_t i = lane; i < (ntiles + kSfxGroup - 1) / kSfxGroup; i += 64) st_store(&w.fsuper[i], 0);
+    if (lane == 0) {
+        __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w.wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
         *w.fail_any = 0;
     }
@@ -4265,6 +4629,16 @@ static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
 }
 
 // decode_dev_impl's launches on a given workspace.
+// The single-pass suffix decode: the counting form or the held form
+// (B64X_SFX_HELD; same arguments, same workspace).
+extern "C++" {
+template <bool WHOLE>
+static auto sfx_kernel()
+{
+    return B64X_SFX_HELD ? k_decode_suffix_held<WHOLE> : k_decode_suffix<WHOLE>;
+}
+}  // extern "C++"
+
 static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
                          b64x_dec_result *d_res, b64x_dec_result *h_res,
                          const b64x_alphabet *abc, unsigned flags, void *ws, void *stream,
@@ -4282,10 +4656,10 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         // of whatever suffix it could not take -- nothing, on clean and
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
-        static const int occ_sfx = occupancy_of(k_decode_suffix<false>);
+        static const int occ_sfx = occupancy_of(sfx_kernel<false>());
         const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
         if (flags & B64X_DEC_EXPECT_JUNK) {
-            hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(sfx_kernel<true>(), dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
@@ -4324,7 +4698,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         }
         if (junky) {
             path_taken(kPathHinted);
-            hipLaunchKernelGGL(k_decode_suffix<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(sfx_kernel<true>(), dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
@@ -4334,7 +4708,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
                            dim3(kLinesTH), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
-        hipLaunchKernelGGL(k_decode_suffix<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(sfx_kernel<false>(), dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                            hold, d_res, h_res, seq, reprobe);
         return launch_status();

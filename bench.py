@@ -1140,7 +1140,7 @@ def main():
         dom_ms = max(r["enc_ms"], r["dec_ms"])
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         knames = ["k_encode_flat"] if dom == "encode" else \
-            ["k_decode_probe", "k_decode_lines", "k_decode_suffix"]
+            ["k_decode_probe", "k_decode_lines", "k_decode_suffix_held"]
         out = {
             "metric": METRIC,
             "value": world * N * K / r["wall"] / 2**30,

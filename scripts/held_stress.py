@@ -69,10 +69,27 @@ def main():
     bad = 0
     for d in (0.05, 0.001):
         junk = sprinkle(enc, d)
+        # each 2,048-character range's alphabet count and its output start
+        # (ceil(B/4)*3 for B alphabet characters before it), for locating a
+        # wrong run
+        tn = junk.cpu().numpy()
+        import numpy as np
+        valid = np.zeros(256, dtype=np.uint8)
+        for c in b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/":
+            valid[c] = 1
+        nr = (tn.size + 2047) // 2048
+        v = np.zeros(nr * 2048, dtype=np.uint8)
+        v[:tn.size] = valid[tn]
+        cnt = v.reshape(nr, 2048).sum(axis=1, dtype=np.int64)
+        B = np.concatenate([[0], np.cumsum(cnt)])
+        starts = (B[:-1] + 3) // 4 * 3
+        del tn, v
         out = torch.empty(b64.decoded_cap(junk.numel()), dtype=torch.uint8, device="cuda")
         ws = torch.zeros(b64.workspace_size(junk.numel()), dtype=torch.uint8, device="cuda")
         res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device="cuda")
         for it in range(a.iters):
+            if it % 10 == 0:
+                print(json.dumps({"density": d, "iter": it, "bad_so_far": bad}), flush=True)
             for ej in (True, False):
                 out.fill_(0xAA)
                 b64.decode(junk, out=out, workspace=ws, result=res, expect_junk=ej)
@@ -89,7 +106,12 @@ def main():
                     bad += 1
                     m = out[:n] != x
                     rr = runs(m)
-                    print(json.dumps({"density": d, "iter": it, "expect_junk": ej,
+                    first = rr[0][0] if rr else -1
+                    r = int(np.searchsorted(starts, first, side="right") - 1)
+                    where = {"range": r, "tile12": r // 12, "tile16": r // 16,
+                             "offset_in_range_output": int(first - starts[r]),
+                             "range_count": int(cnt[r]), "range_B_mod4": int(B[r] % 4)}
+                    print(json.dumps({"density": d, "iter": it, "expect_junk": ej, "where": where,
                                       "out_len": info.out_len, "bytes_bad": int(m.sum()),
                                       "runs": rr, "runs_mod1536": [(o % 1536, l) for o, l in rr]}),
                           flush=True)
