@@ -202,6 +202,19 @@ DEV uint4 load_chars(const uint8_t *p, uint32_t nin)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// __syncthreads() with every LDS access of this wave done first.  hipcc's
+// barrier for a workgroup-scope release did not always wait for them: in
+// k_decode_suffix_held's loop the barrier at the top of an iteration had no
+// lgkmcnt(0) behind thread 0's write of the next tile's ticket at the end of
+// the last one, and now and then another wave read the old ticket after the
+// barrier (profiles/r05_sfx_held_stress*.jsonl: one 1 GiB decode in 5 wrong
+// at 3 ranges per wave, the waves' tickets seen differing; none with this).
+DEV void block_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 // ----------------------------------------------------------- encode core --
 
 // 3 bytes (big-endian in bits 23..0) -> 4 characters, little-endian dword.
@@ -332,7 +345,7 @@ __global__ __launch_bounds__(kThreads) void k_encode(
 {
     __shared__ uint8_t tab[64];
     build_enc_table(tab, a);
-    __syncthreads();
+    block_sync();
 
     const uint64_t step = (uint64_t) gridDim.x * kThreads * kEncUnroll;
     for (uint64_t base = (uint64_t) blockIdx.x * kThreads * kEncUnroll;
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(kEncTH) void k_encode_flat(
     __shared__ uint8_t tab[64];
     const uint32_t tid = threadIdx.x;
     build_enc_table(tab, a);
-    __syncthreads();
+    block_sync();
     for (uint64_t t = blockIdx.x; t < full; t += gridDim.x) {
         const uint64_t q = t * kEncTH + tid;
         const u32x3a4 v = ld12<true>(in + q * 12);
@@ -461,7 +474,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_strided(
 {
     __shared__ uint8_t tab[64];
     build_enc_table(tab, a);
-    __syncthreads();
+    block_sync();
     u32x3a4 v[U];
     const uint8_t *srcs[U];
     uint8_t *dsts[U];
@@ -548,7 +561,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_tight2(
 {
     __shared__ uint8_t tab[64];
     build_enc_table(tab, a);
-    __syncthreads();
+    block_sync();
     const uint64_t s0 = (uint64_t) blockIdx.x * U * kThreads;
     const uint64_t b0 = __umul64hi(16 * s0, m64);
     const uint32_t p0 = (uint32_t) (16 * s0 - b0 * E);
@@ -608,7 +621,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_ragged(
 {
     __shared__ uint8_t tab[64];
     build_enc_table(tab, a);
-    __syncthreads();
+    block_sync();
     for (uint32_t b = blockIdx.x; b < nbuf; b += gridDim.x) {
         const uint64_t beg = in_off[b], len = in_off[b + 1] - beg;
         const uint8_t *src = in + beg;
@@ -633,18 +646,6 @@ DEV void wave_lds_order()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// __syncthreads() with every LDS access of this wave done first.  hipcc's
-// barrier for a workgroup-scope release did not always wait for them: in
-// k_decode_suffix_held's loop the barrier at the top of an iteration had no
-// lgkmcnt(0) behind thread 0's write of the next tile's ticket at the end of
-// the last one, and now and then another wave read the old ticket after the
-// barrier (profiles/r05_sfx_held_stress*.jsonl: one 1 GiB decode in 5 wrong
-// at 3 ranges per wave, the waves' tickets seen differing; none with this).
-DEV void block_sync()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-}
 
 // Four groups -> 12 output bytes as three little-endian dwords.
 DEV void groups_to_bytes(uint32_t G0, uint32_t G1, uint32_t G2, uint32_t G3,
@@ -1056,7 +1057,7 @@ void k_decode_pass1(
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     // wave-uniform, and provably so (scalar loop control, no exec masking)
     const uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -1210,7 +1211,7 @@ DEV uint64_t block_excl_scan256(uint64_t x, uint64_t *wtot, uint64_t &total)
         if (lane >= (uint32_t) d) v += y;
     }
     if (lane == 63) wtot[wave] = v;
-    __syncthreads();
+    block_sync();
     uint64_t before = 0;
     total = 0;
 #pragma unroll
@@ -1266,7 +1267,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     if (packed == 0) {
         if (blockIdx.x != 0) return;
         build_dec_table(tab, a);
-        __syncthreads();
+        block_sync();
         const uint64_t V = (uint64_t) (nranges - 1) * R + w.counts[nranges - 1];
         if (threadIdx.x == 0) {
             *w.fd_cur = 0;
@@ -1278,7 +1279,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
     const uint32_t r0 = (uint32_t) (~packed >> 32);
     const uint32_t ntiles = (nranges - r0 + kScanTile - 1) / kScanTile;
     if (threadIdx.x == 0) s_tile = atomicAdd(w.ticket, 1u);
-    __syncthreads();
+    block_sync();
     const uint32_t t = s_tile;
     if (t >= ntiles) return;
     build_dec_table(tab, a);
@@ -1322,7 +1323,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_scan2(
             s_excl = excl;
         }
     }
-    __syncthreads();
+    block_sync();
     uint64_t run = s_excl + ex;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -1871,7 +1872,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
     }
     build_dec_table(tab, a);
     if (threadIdx.x == 0) s_first = 0xFFFFFFFFu;
-    __syncthreads();
+    block_sync();
     if (threadIdx.x < 64) {
         uint32_t pj = 0xFFFFFFFFu;
         LineModel m = probe_lines(tab, in, n, &pj);
@@ -1902,7 +1903,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
             s_m = m;
         }
     }
-    __syncthreads();
+    block_sync();
     const LineModel m = s_m;
     if (sample && !m.skip) {
         // the first sampled byte the model gets wrong: outside the alphabet
@@ -1917,7 +1918,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
         }
         if (first != 0xFFFFFFFFu) atomicMin(&s_first, first);
     }
-    __syncthreads();
+    block_sync();
     if (threadIdx.x != 0) return;
     LineModel mo = m;
     const uint32_t pf = s_first;
@@ -1974,7 +1975,7 @@ void k_decode_lines(
     // this launch does.  (Tested before the table build, the model's load
     // no longer overlapped the build: MIME text +2 %.)
     if (blockIdx.x * kLinesWaves * kLinesSlots > T) return;
-    __syncthreads();
+    block_sync();
     LineModel m;
     m.L = mok ? (uint32_t) mw0 : 0u;
     m.s = (uint32_t) (mw0 >> 32);
@@ -2328,7 +2329,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
@@ -3057,7 +3058,7 @@ void k_decode_batch_fast(
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -3152,7 +3153,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_slots(
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     uint4 w[U];
     uint32_t nin[U], bq[U][2];
 #pragma unroll
@@ -3381,7 +3382,7 @@ __global__ __launch_bounds__(kThreads) void k_rows_prep(
     if (blockIdx.x != 0) return;
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     if (threadIdx.x >= 64) return;
     const LineModel lm = probe_lines(tab, in, len);
     RowModel r{};
@@ -3505,7 +3506,7 @@ void k_decode_rows_lines(
     // before it, the model's loads no longer overlapped the build and MIME
     // rows ran 481.6 -> 499.2 us, profiles/r04_ab_rows_early_exit.jsonl)
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     const uint32_t j0 = (uint32_t) r6, rcpS = (uint32_t) (r6 >> 32);
     if ((uint32_t) r0 != 0) {
         RowModel rm;
@@ -3860,7 +3861,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_batch_fix2(
     __shared__ P2dSmem sm;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
@@ -3898,7 +3899,7 @@ __global__ __launch_bounds__(kThreads) void k_rows_finish(
     const unsigned long long *bm = row_fail(ws);
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t) gridDim.x * kWavesPerBlock;
@@ -3939,7 +3940,7 @@ __global__ __launch_bounds__(kThreads) void k_batch_finish(
 {
     __shared__ uint8_t tab[256];
     build_dec_table(tab, a);
-    __syncthreads();
+    block_sync();
     const uint32_t lane = lane_id();
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     for (uint32_t j = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -5464,7 +5465,7 @@ __global__ __launch_bounds__(kThreads) void k_gather_host(
         }
         s_i0 = a;
     }
-    __syncthreads();
+    block_sync();
     uint64_t p = lo;
     for (uint32_t i = s_i0; p < hi; i++) {
         const uint64_t so = i < nseg ? seg[i].off : hi, se = i < nseg ? seg[i].off + seg[i].len : hi;
