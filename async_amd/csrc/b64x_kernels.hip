@@ -5785,7 +5785,11 @@ const char *b64x_build_info(void)
 #define B64X_STR(x) B64X_STR2(x)
     return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
            "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
+#if B64X_SFX_HELD
+           "(decoded once, held until its prefix, group sums, LDS read-ahead); rows:line model in row "
+#else
            "(count ahead, group sums, LDS read-ahead); rows:line model in row "
+#endif
            "bands; lanes:chained decoder blocks";
 }
 
