@@ -2952,12 +2952,15 @@ void k_decode_suffix_held(
         block_sync();  // s_cnt[bB] complete
         if (haveB && threadIdx.x == 0) publish(tB, bB);
         if (haveA) {
+            // (every wave taking the prefix itself, no barrier: 841 against
+            // 780 us, profiles/r05_ab_sfx_held_wavepfx.jsonl)
             if (wv == 0) {
                 const uint32_t ex = tA ? prefix(tA) : 0u;
                 if (lane == 0) s_excl = ex;
             }
             block_sync();
-            uint32_t Bp = s_excl;
+            const uint32_t exw = s_excl;
+            uint32_t Bp = exw;
             for (uint32_t i = 0; i < wv * HP; i++) Bp += s_cnt[bA][i];
             const uint32_t rwA = r0 + tA * TILE + wv * HP;
 #pragma unroll
@@ -2970,7 +2973,7 @@ void k_decode_suffix_held(
             }
             if (tA == ntiles - 1) {
                 owner = true;
-                Vs = s_excl;
+                Vs = exw;
                 for (uint32_t i = 0; i < TILE; i++) Vs += s_cnt[bA][i];
             }
         }
