@@ -436,6 +436,7 @@ DEV u32x3a4 ld12(const uint8_t *p)
 // +20 / +120 us; software pipelining and cached loads slower (r01_v6_*).
 constexpr uint32_t kEncTH = 256;
 
+
 __global__ __launch_bounds__(kEncTH) void k_encode_flat(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t full, uint64_t n,
     EncAlpha a)
@@ -1950,6 +1951,26 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
 // blocks with one block-wide table (per-wave tables without the barrier:
 // neutral, profiles/r03_ab_probe_wtab.jsonl).
 constexpr uint32_t kLinesTH = 256, kLinesWaves = kLinesTH / 64;
+
+// The wave's first failing slot from each lane's failed-slot bits (bit u:
+// slot u): one ballot on the hot paths, the per-slot ones only when
+// something failed (a ballot and a scalar branch per slot: clean 1 GiB
+// 412.9 -> 408.6 us, CRLF-76 447.3 -> 445.0 with the separator check made
+// branch-free, profiles/r05_ab_lines_defer.jsonl).
+DEV void lines_first_fail(uint32_t badm, uint32_t &fail_u, uint32_t &fail_lane)
+{
+    if (__ballot(badm != 0) == 0) return;
+#pragma unroll
+    for (uint32_t u = 0; u < kLinesU; u++) {
+        const uint64_t fb = __ballot((badm >> u) & 1u);
+        if (fb) {
+            fail_u = u;
+            fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
+            return;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
@@ -2016,17 +2037,15 @@ void k_decode_lines(
         uint4 c[kLinesU];
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) c[u] = ld16<true>(in + 16 * (t0 + u * 64 + lane));
+        uint32_t badm = 0;  // bit u: this lane's slot u failed
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
             uint32_t G[4], bad;
             map_fast(tab, c[u], 16, G, bad);
-            const uint64_t fb = __ballot(bad != 0);
-            if (fb && fail_u == kLinesU) {
-                fail_u = u;
-                fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
-            }
+            badm |= bad ? 1u << u : 0u;
             emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
         }
+        lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns && L != 0 && full && oal && ial && safe) {
         // The hot path of line-structured text: 32-bit offsets from the
         // input's base, unguarded window loads, non-temporal stores.
@@ -2052,6 +2071,8 @@ void k_decode_lines(
             const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
             wx[u] = make_uint2(v.x, v.y);
         }
+        const uint32_t need = sep_need(s);
+        uint32_t badm = 0;  // bit u: this lane's slot u failed
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
             const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
@@ -2061,15 +2082,13 @@ void k_decode_lines(
             map_fast(tab, d, 16, G, bad);
             // the separator bytes of a line that ends here must all be
             // outside the alphabet (looked up by every lane, kept by those)
-            const uint32_t need = sep_need(s);
-            if (hs[u] && (sep_nonalpha(tab, sep) & need) != need) bad |= 0x100u;
-            const uint64_t fb = __ballot(bad != 0);
-            if (fb && fail_u == kLinesU) {
-                fail_u = u;
-                fail_lane = (uint32_t) __ffsll((unsigned long long) fb) - 1;
-            }
+            // (no branch: the bytes required are zero where no line ends)
+            const uint32_t nd = hs[u] ? need : 0u;
+            if ((sep_nonalpha(tab, sep) & nd) != nd) bad |= 0x100u;
+            badm |= bad ? 1u << u : 0u;
             emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
         }
+        lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns) {
         // Everything else (a partial wave, the input's end, misaligned
         // buffers): guarded window loads through 64-bit addresses.
