@@ -3326,6 +3326,7 @@ DEV unsigned long long *row_fail(void *ws)
 
 constexpr uint32_t kRowsU = 4;  // slots per lane of the row kernels
 
+
 // The groups and the invalid mask (x 128, bits 7..22) of 16 characters by
 // packed table values: groups by v_dot4 of their low 6 bits (a non-alphabet
 // character contributes 63 inside its own field), the mask by v_dot4 of the
@@ -3645,6 +3646,8 @@ void k_decode_rows_lines(
                 uint32_t o0, o1, o2;
                 groups_to_bytes(G[0], G[1], G[2], G[3], o0, o1, o2);
                 __builtin_nontemporal_store(u32x3a4{o0, o1, o2}, (u32x3a4 *) (ob + (ooff + u * uo)));
+                // (one ballot per wave instead, as k_decode_lines: neutral
+                // here, profiles/r05_ab_rows_defer.jsonl)
                 const uint64_t junk = __ballot(bad != 0);
                 if (junk) mark_failed_rows(bm, junk, q, row_st + u * Ru + rin);
             }
