@@ -666,6 +666,36 @@ def test_single_pass_decode_vs_oracle(density):
         assert bytes(hinfo.tail)[:hinfo.tail_n] == bytes(hrinfo.tail)[:hrinfo.tail_n], n
 
 
+def test_single_pass_decode_repeated_large():
+    """Repeated single-pass decodes of one large junk-laden stream in one
+    process, every output checked: the form of the stress that found the
+    suffix kernel's loop-top barrier not waiting for thread 0's LDS write of
+    the next tile's ticket (a wave then decoded another tile; one 1 GiB
+    decode in 5 to 60 came out shifted, DESIGN.md §5, scripts/held_stress.py).
+    Smaller and shorter here; round trip, so size-independent."""
+    n = 192 << 20
+    x = torch.empty(n, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0xB10C)
+    chars = b64.encode(x)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for d in (0.05, 0.001):
+        mask = torch.rand(chars.numel(), device=DEV, generator=g) < d
+        idx = torch.arange(chars.numel(), device=DEV) + torch.cumsum(mask, 0)
+        text = torch.full((chars.numel() + int(mask.sum()),), ord("!"), dtype=torch.uint8,
+                          device=DEV)
+        text[idx] = chars
+        del mask, idx
+        out = torch.empty(b64.decoded_cap(text.numel()), dtype=torch.uint8, device=DEV)
+        ws = torch.zeros(b64.workspace_size(text.numel()), dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+        for it in range(12):
+            out.fill_(0xAA)
+            b64.decode(text, out=out, workspace=ws, result=res, expect_junk=it % 2 == 0)
+            info = b64.Decoded(out, res).info()
+            assert info.out_len == n and torch.equal(out[:n], x), (d, it)
+        del text, out, ws
+
+
 def test_single_pass_decode_structured_and_alphabets():
     rng = np.random.default_rng(12)
     host = rng.integers(0, 256, 1_500_000, dtype=np.uint8)
