@@ -1631,7 +1631,9 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
 //
 // Reference: the per-character loop of decoder_read(), src/base64decoder.c:
 // 52-80 (skip non-alphabet bytes, 8 bits out per 4 characters' 24).
-constexpr uint32_t kLinesU = 4;                     // slots per lane (2: +1-3 %, 8: +7 %)
+// slots per lane (2: +1-3 %, 8: +7 %; with one ballot per wave, round 5: 2 +1 %,
+// 6 +4 % clean, profiles/r05_ab_lines_u.jsonl)
+constexpr uint32_t kLinesU = 4;
 constexpr uint32_t kLinesSlots = 64 * kLinesU;      // per wave
 constexpr uint32_t kLinesMaxL = 252, kLinesMaxS = 4;
 
