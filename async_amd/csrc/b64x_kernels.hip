@@ -2717,8 +2717,10 @@ void k_decode_suffix(
 // us).  Tried and slower: a tile's ticket drawn one iteration ahead (940
 // us), storing range j of A right after decoding range j of B (A's prefix
 // then needed one range after B is drawn: 2.2-2.8 ms, tiles waiting on
-// their predecessors), 3 or 2 ranges per wave (810 / 1,156 us), 4 waves per
-// SIMD without spills (835 us).  Its first form's barriers were hipcc's
+// their predecessors), 3 or 2 ranges per wave (810 / 1,156 us; with the
+// incremental prefix 815 / 1,153 against 725), 4 waves per SIMD without
+// spills (835 us).  The prefix loads only the groups completed since the
+// block's last tile (746.5 against 778.2 us, profiles/r05_ab_sfx_prefix_incremental.jsonl).  Its first form's barriers were hipcc's
 // __syncthreads(), and the one at the top of an iteration did not wait for
 // thread 0's write of the next ticket: now and then a wave decoded another
 // tile than its block (one repeated 1 GiB decode in five came out shifted;
@@ -2819,20 +2821,30 @@ void k_decode_suffix_held(
         __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     };
+    // The groups before kdone are complete and sum to sdone (wave 0's, from
+    // its earlier prefixes): a prefix loads its own group's statuses and the
+    // groups since -- about 20 for a block's next tile, one word per lane,
+    // one round trip.  (Loading every earlier group, 64 per lane-pass, took
+    // one round trip per pass, each waited for before the next: 6 on average
+    // on 1 GiB.)
+    uint32_t kdone = 0, sdone = 0;
     auto prefix = [&](uint32_t t) -> uint32_t {
         const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
-        const uint32_t ng = (k + 63) / 64;
         for (;;) {
             const uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
             bool ok = (v & kStAgg) != 0;
-            uint32_t sum = (uint32_t) v;
-            for (uint32_t i = 0; i < ng; i++) {
-                const uint32_t j = lane + 64 * i;
+            uint32_t sg = 0;
+            for (uint32_t j0 = kdone; j0 < k; j0 += 64) {
+                const uint32_t j = j0 + lane;
                 const uint64_t g = j < k ? st_load(&w.fsuper[j]) : kGroupFull;
                 ok = ok && (g >> 56) == kSfxGroup;
-                sum += (uint32_t) g;
+                sg += j < k ? (uint32_t) g : 0u;
             }
-            if (__all(ok)) return wave_sum(sum);
+            if (__all(ok)) {
+                sdone += wave_sum(sg);
+                kdone = k;
+                return sdone + wave_sum((uint32_t) v);
+            }
             __builtin_amdgcn_s_sleep(2);
         }
     };
@@ -3009,6 +3021,9 @@ void k_decode_suffix_held(
         tA = tB;
         bA = bB;
         bB ^= 1u;
+        // (drawn right after the publish instead, its round trip under the
+        // stores: 762 against 730 us, profiles/r05_ab_sfx_early_draw.jsonl --
+        // the tile then starts later and its successors wait)
         if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
     }
     block_sync();
