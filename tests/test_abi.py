@@ -65,6 +65,21 @@ def test_product_has_no_variant_knobs():
     assert "b64x__test_range_chunks" in hooks
 
 
+def test_kernel_barriers_wait_for_lds():
+    """Every barrier in the kernels is block_sync() (an explicit
+    s_waitcnt lgkmcnt(0), then __syncthreads()): hipcc's barrier at the top
+    of the held suffix kernel's loop did not wait for thread 0's LDS write of
+    the next ticket, and a wave now and then decoded another tile (DESIGN.md
+    §5)."""
+    import re
+    src = open(os.path.join(ROOT, "async_amd", "csrc", "b64x_kernels.hip")).read()
+    code = re.sub(r"//[^\n]*", "", src)
+    a = code.index("DEV void block_sync()")
+    b = code.index("}", a) + 1
+    assert "s_waitcnt lgkmcnt(0)" in code[a:b] and "__syncthreads()" in code[a:b]
+    assert "__syncthreads()" not in code[:a] + code[b:]
+
+
 def test_every_environment_knob_is_documented():
     """Every ASYNC_B64_* variable the product libraries can read is in
     INTEGRATION.md's runtime-configuration table."""
