@@ -50,6 +50,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "b64x.h"
@@ -2955,8 +2956,10 @@ void k_decode_suffix_held(
     // stored after tile B is drawn, decoded and published, so that A's
     // predecessors have had a whole tile's time to publish.
     // (LA: the bytes after each held range, byte j for range j)
-    uint32_t HA[HP][6], LA = 0;
-    static_assert(HP <= 4, "one byte per held range in LA");
+    using LT = typename std::conditional<(HP > 4), uint64_t, uint32_t>::type;
+    uint32_t HA[HP][6];
+    LT LA = 0;
+    static_assert(HP <= 8, "one byte per held range in LA");
 #pragma unroll
     for (uint32_t j = 0; j < HP; j++) {
 #pragma unroll
@@ -2971,7 +2974,8 @@ void k_decode_suffix_held(
         const uint32_t tB = s_tile[bB];
         const bool haveB = tB < ntiles;
         if (!haveA && !haveB) break;
-        uint32_t HB[HP][6], LB = 0;
+        uint32_t HB[HP][6];
+        LT LB = 0;
         if (haveB) {
             const uint32_t rwB = r0 + tB * TILE + wv * HP;
             if (whole(rwB)) fetch(rwB, 0);
@@ -2979,7 +2983,7 @@ void k_decode_suffix_held(
             for (uint32_t j = 0; j < HP; j++) {
                 uint32_t lan;
                 decode_one(rwB, j, bB, HB[j], lan);
-                LB |= lan << (8 * j);
+                LB |= (LT) lan << (8 * j);
             }
         }
         block_sync();  // s_cnt[bB] complete
@@ -3000,7 +3004,7 @@ void k_decode_suffix_held(
             for (uint32_t j = 0; j < HP; j++) {
                 if (rwA + j < nranges) {
                     const uint32_t T = s_cnt[bA][wv * HP + j];
-                    store_one(rwA + j, Bp, T, HA[j], (LA >> (8 * j)) & 0xFFu);
+                    store_one(rwA + j, Bp, T, HA[j], (uint32_t) (LA >> (8 * j)) & 0xFFu);
                     Bp += T;
                 }
             }
