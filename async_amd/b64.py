@@ -207,10 +207,15 @@ def decode_batch(x: torch.Tensor, in_off: torch.Tensor, out: torch.Tensor,
 
 def release_stream(stream=None) -> None:
     """Hand back the library decode workspace bound to `stream`
-    (b64x_release_stream): call it before destroying a stream that decoded
-    without a workspace of its own, so the workspace is free at once instead
-    of when the least recently used one is taken over.  The next decode on
-    the stream binds one again; work already queued is not affected."""
+    (b64x_release_stream).  Required before the stream's handle is destroyed
+    if it decoded without a workspace of its own: a later takeover of the
+    workspace records an event on the handle it is bound to.  torch's own
+    streams (torch.cuda.Stream(), the default stream) come from pools that
+    live as long as the process, so this matters for handles wrapped with
+    torch.cuda.ExternalStream whose owner destroys them; for the others it
+    only frees the workspace at once instead of when the least recently used
+    one is taken over.  The next decode on the stream binds one again; work
+    already queued is not affected."""
     _lib.load().b64x_release_stream(_stream(stream))
 
 

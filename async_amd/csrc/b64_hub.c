@@ -271,24 +271,32 @@ static void batch_drop_after(b64_hub *h, b64_batch *b)
 }
 
 /* The pool ran dry: stock it, by one thread at a time and within the
- * pool's cap, up to the arenas the live hubs hold under their normal limit
- * (HUB_MAX_LIVE each), and past that by a quarter of the arenas in
- * existence (at least 2).  Demand grows a little at a time -- config 5 on 16
- * loops took one more arena than ever before in a pass now and then -- and
- * every arena allocated on demand is a pinned-memory call that stalls every
- * loop for milliseconds: with the pool filled only on demand, passes that
- * allocated ran 10.8-14.1 GiB/s against 16.2-16.5 for those that did not
- * (profiles/r05_cfg5_t16_pool128.jsonl, r05_cfg5_t16_stocked.jsonl). */
+ * pool's cap.  Demand grows a little at a time -- config 5 on 16 loops took
+ * one more arena than ever before in a pass now and then -- and every arena
+ * allocated on demand is a pinned-memory call that stalls every loop for
+ * milliseconds: with the pool filled only on demand, passes that allocated
+ * ran 10.8-14.1 GiB/s against 16.2-16.5 for those that did not
+ * (profiles/r05_cfg5_t16_pool128.jsonl, r05_cfg5_t16_stocked.jsonl).
+ *  - Several loops with GPU stages (nhubs > 1): up to the arenas the live
+ *    hubs hold under their normal limit (HUB_MAX_LIVE each).
+ *  - Otherwise, and past that: a quarter of the arenas in existence.  A
+ *    process with one loop that decodes one message allocates its one arena
+ *    and no more (round 5 stocked HUB_MAX_LIVE at once: ~330 MB pinned for
+ *    one message); one that keeps 4+ arenas busy grows by a
+ *    quarter each time the pool runs dry.
+ * The pool never holds more than ASYNC_B64_POOL_MAX idle arenas (256 by
+ * default, ~41 MB pinned each at the default ASYNC_B64_BATCH_BYTES: a
+ * ceiling of ~10.5 GB of idle pinned memory, reached only by a process whose
+ * peak held that many). */
 static void stock_pool(b64_hub *h)
 {
     bool idle = false;
     if (!atomic_compare_exchange_strong(&stocking, &idle, true))
         return;
     const unsigned total = atomic_load_explicit(&arenas_total, memory_order_relaxed);
-    const unsigned cover = atomic_load_explicit(&nhubs, memory_order_relaxed) * HUB_MAX_LIVE;
-    unsigned want = cover > total ? cover - total : total / 4;
-    if (want < 2)
-        want = 2;
+    const unsigned hubs = atomic_load_explicit(&nhubs, memory_order_relaxed);
+    const unsigned cover = hubs > 1 ? hubs * HUB_MAX_LIVE : 0;
+    const unsigned want = cover > total ? cover - total : total / 4;
     pthread_once(&pool_once, pool_init);
     for (unsigned i = 0; i < want; i++) {
         pthread_mutex_lock(&pool_lock);

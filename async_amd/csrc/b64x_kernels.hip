@@ -50,7 +50,6 @@
 
 #include <atomic>
 #include <mutex>
-#include <type_traits>
 #include <utility>
 
 #include "b64x.h"
@@ -862,18 +861,18 @@ DEV int fast_prefix(const LaneChunk &lc, bool hold, uint8_t *out)
 //   lfail   kFailWords words, kFailStride apart (one per 128-byte line):
 //           ~(first failing slot) of k_decode_lines, published by each wave
 //           into word (block mod kFailWords) so that failing waves do not all
-//           read one line; 0 = none (cleared by k_decode_suffix)
+//           read one line; 0 = none (cleared by k_decode_suffix_held)
 //   fail_any  nonzero when any failure word was published (set by the probe
 //           and by the first publisher into a word, which sees it zero;
-//           cleared by k_decode_suffix): the idle suffix kernel's one
+//           cleared by k_decode_suffix_held): the idle suffix kernel's one
 //           scalar load instead of a wave reading all 64 words per block
 //   model   the line model k_decode_probe found, for k_decode_lines and
-//           k_decode_suffix; model_n the length of the stream it was made for:
+//           k_decode_suffix_held; model_n the length of the stream it was made for:
 //           a call of the same length may reuse it without a probe
 //           (decode_dev_ws), and k_decode_lines checks that it does
-//   fticket, fstatus, fsuper, wdone  k_decode_suffix's tile ticket, tile
+//   fticket, fstatus, fsuper, wdone  k_decode_suffix_held's tile ticket, tile
 //           counts, group sums and count of blocks that have left
-//   sfx_start  where the last call's k_decode_suffix<false> started (its
+//   sfx_start  where the last call's k_decode_suffix_held<false> started (its
 //           first failing slot's span), ~0 when it had nothing to do; read
 //           by the tests only (clean and MIME input must never need it)
 // The regions that must be zero between calls (status, fstatus, fsuper, lfail,
@@ -895,50 +894,36 @@ static_assert(sizeof(LineModel) == 32, "the workspace header holds 32 bytes of m
 struct DecodeWs {
     uint64_t *lfail;     // kFailWords words, kFailStride apart
     uint64_t *fail_any;  // nonzero: some failure word was published (own line)
-    uint32_t *wdone;     // k_decode_suffix: blocks that have left (own line; zero between calls)
-    LineModel *model;    // k_decode_lines' model, for k_decode_suffix
+    uint32_t *wdone;     // k_decode_suffix_held: blocks that have left (own line; zero between calls)
+    LineModel *model;    // k_decode_lines' model, for k_decode_suffix_held
     uint64_t *model_n;   // the stream length the model was probed for (0: none yet)
     uint64_t *fd;
     uint64_t *fd_cur;
     uint32_t *ticket;
     uint32_t *fticket;   // the single-pass decode's tile ticket (zero between calls)
-    uint64_t *sfx_start; // where k_decode_suffix<false> started, ~0 = nothing to do
+    uint64_t *sfx_start; // where k_decode_suffix_held<false> started, ~0 = nothing to do
     uint32_t *counts;
     uint64_t *bases;
     uint64_t *status;
     uint64_t *fstatus;   // the single-pass decode's tile status words (zero between calls)
-    uint64_t *fsuper;    // k_decode_suffix's group sums: tiles counted << 56 | sum (zero between calls)
+    uint64_t *fsuper;    // k_decode_suffix_held's group sums: tiles counted << 56 | sum (zero between calls)
 };
 
 constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
-// Ranges per wave of a single-pass decode tile (k_decode_suffix): 8 (16
-// was 841 us, 8 766 us on 1 GiB at junk density 0.05, profiles/r03_ab_sfx_*;
-// 4 and 2: r04_g/r04_h, slower).
-constexpr uint32_t kFusePer = 8;
-constexpr uint32_t kFuseLoad = 4;  // of them loaded at once for counting
-constexpr uint32_t kFuseTile = kFusePer * kWavesPerBlock;  // ranges per block
-// k_decode_suffix_held: ranges per wave of a tile (held in VGPRs, decoded;
-// 4 with 5 waves per SIMD, see there)
-#ifndef B64X_SFX_HP
-#define B64X_SFX_HP 4
-#endif
-#ifndef B64X_SFX_WPE
-#define B64X_SFX_WPE 5
-#endif
-#ifndef B64X_SFX_HELD
-#define B64X_SFX_HELD 1  // k_decode_suffix_held (0: the counting form)
-#endif
-constexpr uint32_t kHeldPer = B64X_SFX_HP;
+// k_decode_suffix_held: ranges per wave of a tile (held in VGPRs; 4 at 5
+// waves per SIMD: 2, 3, 5-8 per wave and 4 or 6 waves per SIMD all measured
+// slower, profiles/r05_ab_sfx_held*.jsonl)
+constexpr uint32_t kHeldPer = 4;
+constexpr uint32_t kHeldWaves = 5;  // waves per SIMD (96 VGPRs: two tiles held)
 constexpr uint32_t kHeldTile = kHeldPer * kWavesPerBlock;
-constexpr uint32_t kSfxTileMin = kHeldTile < kFuseTile ? kHeldTile : kFuseTile;
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsModelN = 64;                                        // the model's stream length
 constexpr uint64_t kWsStatus = 128;                                       // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
-constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix: tiles per group sum
+constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix_held: tiles per group sum
 constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
-constexpr uint64_t kWsFSuper = kWsFStatus + (kMaxRanges / kSfxTileMin + 1) * 8;   // suffix group sums
-constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kSfxTileMin / kSfxGroup + 16) * 8;  // lines failures
+constexpr uint64_t kWsFSuper = kWsFStatus + (kMaxRanges / kHeldTile + 1) * 8;   // suffix group sums
+constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kHeldTile / kSfxGroup + 16) * 8;  // lines failures
 // failure words, fail_any, wdone: one 128-byte line each
 constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
@@ -1393,12 +1378,6 @@ DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
 }
 
 
-DEV uint32_t lane_valid_count(const uint32_t P[4])
-{
-    return 16u - __popc(P[0] & 0x80808080u) - __popc(P[1] & 0x80808080u) -
-           __popc(P[2] & 0x80808080u) - __popc(P[3] & 0x80808080u);
-}
-
 // One wave copies 64 x 16 bytes from gsrc (per lane) to LDS at lds_dst +
 // 16 x lane, straight into LDS (global_load_lds_dwordx4: no VGPR holds the
 // data).  Issued as inline asm so that the compiler does not track the copy:
@@ -1626,7 +1605,7 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
 // decoded exactly by the one wave that owns slot T, which also writes the
 // result record.  The first failing slot t_f (any other structure, junk,
 // '=' inside the stream) is published; everything before pos(16 t_f) is
-// final, and k_decode_suffix<false> decodes [pos(16 t_f), n) exactly.  The
+// final, and k_decode_suffix_held<false> decodes [pos(16 t_f), n) exactly.  The
 // model is probed from the first 256 bytes by one wave per block; the
 // decode never depends on it being right, only its speed does.
 //
@@ -1816,18 +1795,18 @@ DEV uint32_t tab_pack4(const uint8_t *tab, uint32_t x)
 // into the workspace, for k_decode_lines (every block reads them with one
 // scalar load instead of probing -- 175 K probes of the same 256 bytes cost
 // 7 % of a 1 GiB decode -- and of computing T and L's reciprocals: hundreds
-// of scalar instructions per wave) and k_decode_suffix.  n <= 2^31 (the
+// of scalar instructions per wave) and k_decode_suffix_held.  n <= 2^31 (the
 // launcher's bound), so sextet indices and positions fit in 32 bits.
 //
 // Wave 0 probes the model from the first 256 bytes.  Every thread also
 // checks 64 bytes sampled further in (half of them over the stream's first
 // sixteenth, half over all of it, spaced quadratically), against the model: where a sample breaks it, every slot
-// from there on is left to k_decode_suffix (T is cut there), so that junk
+// from there on is left to k_decode_suffix_held (T is cut there), so that junk
 // the first window did not show -- sparse junk, one character in a thousand
 // -- is not decoded twice, once by k_decode_lines until its slots fail and
-// again by k_decode_suffix from the first failure.  Where T falls never
+// again by k_decode_suffix_held from the first failure.  Where T falls never
 // matters for the result (k_decode_lines takes slots [0, T) exactly or
-// publishes their failure; k_decode_suffix takes the rest), only for speed.
+// publishes their failure; k_decode_suffix_held takes the rest), only for speed.
 constexpr uint32_t kProbeThreads = 256;
 
 // What the probe of the last call on a (workspace, input, length) saw, for
@@ -1835,7 +1814,7 @@ constexpr uint32_t kProbeThreads = 256;
 // host reads without a sync: a stale or torn hint only picks the slower
 // path).  junky: the probe cut the line model within the stream's first
 // sixteenth, so k_decode_lines would take almost nothing and the single
-// pass (k_decode_suffix<true>) is the faster exact decode.
+// pass (k_decode_suffix_held<true>) is the faster exact decode.
 struct DecodeHint {
     uint32_t key, junky;
 };
@@ -1886,7 +1865,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
                 // junk in the window that no line model explains (unstructured
                 // junk, a short first line): under the clean model the slot
                 // holding it fails, so k_decode_lines takes only the slots
-                // before it, and k_decode_suffix everything from there
+                // before it, and k_decode_suffix_held everything from there
                 m.T = pj / 16;
                 m.skip = 1;
             } else if (m.L == 0) {
@@ -1928,7 +1907,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
     const uint32_t pf = s_first;
     if (!mo.skip && pf != 0xFFFFFFFFu) {
         // the slot holding model position F(pf): every slot from there on is
-        // k_decode_suffix's
+        // k_decode_suffix_held's
         const uint32_t F = mo.L ? pf / mo.P * mo.L + (pf % mo.P < mo.L ? pf % mo.P : mo.L) : pf;
         if (F / 16 < mo.T) {
             mo.T = F / 16;
@@ -1991,7 +1970,7 @@ void k_decode_lines(
     // for this length, or a fresh one at a reused address): the clean model
     // of this length instead (L = 0, every slot, no cut) -- exact like any
     // model; clean input keeps the fast path and anything else fails a slot
-    // and goes to k_decode_suffix (which then asks for a probe).
+    // and goes to k_decode_suffix_held (which then asks for a probe).
     const bool mok = mn == n;
     const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : (uint32_t) n / 16u;
     // a block wholly past slot T (the probe cut the model's slots at junk)
@@ -2161,7 +2140,7 @@ void k_decode_lines(
     if (T >= t0 + kLinesSlots || m.skip) return;
     // This wave owns slot T: the < 16 + s bytes after the last interior
     // span, decoded exactly, and the result record (replaced by
-    // k_decode_suffix when a slot failed).
+    // k_decode_suffix_held when a slot failed).
     const uint64_t Q = line_pos(m, 16 * (uint64_t) T);
     const uint32_t tl = (uint32_t) (n - Q);  // < 16 + s <= 20
     const bool here = lane < tl;
@@ -2198,7 +2177,7 @@ void k_decode_lines(
         r.nchars = n;
         r.seq = seq;
         r.flags = hold ? 1u : 0u;
-        *res = r;  // provisional: k_decode_suffix mirrors it to the host or replaces it
+        *res = r;  // provisional: k_decode_suffix_held mirrors it to the host or replaces it
     }
 }
 
@@ -2268,7 +2247,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
     if (!last && T > 0 && (T & 3)) {
         // complete the range's last group from the characters after it:
         // given (la, la_ok), in LDS at la_lds (the next range, whole, copied
-        // there by k_decode_suffix while this range decoded: waited for
+        // there by k_decode_suffix_held while this range decoded: waited for
         // now), or read from `in` only now (la_late)
         bool ok = la_ok;
         if (la_lds) {
@@ -2409,36 +2388,33 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 
 // ---- single-pass exact decode of a suffix ---------------------------------
 //
-// Decodes characters [S, n) into out + O, S being a group boundary of the
-// whole stream (Vb = the alphabet characters before S, a multiple of 4, O =
-// 3 Vb / 4), and writes the result record for the whole stream.  WHOLE: S =
-// 0 (B64X_DEC_EXPECT_JUNK); else S, O, Vb come from the first failing slot
-// k_decode_lines published, and the kernel exits at once when there is none
-// (the common case: every block reads one word and returns).
+// k_decode_suffix_held decodes characters [S, n) into out + O, S being a
+// group boundary of the whole stream (Vb = the alphabet characters before S,
+// a multiple of 4, O = 3 Vb / 4), and writes the result record for the whole
+// stream.  WHOLE: S = 0 (B64X_DEC_EXPECT_JUNK, and the hinted single pass);
+// else S, O, Vb come from the first failing slot k_decode_lines published,
+// and the kernel exits at once when there is none (the common case: every
+// block reads one word and returns).
 //
 // Ranges are the pass-1 ranges of R = 2,048 characters, aligned to the
 // stream; the first one, r0 = S / R, starts at S.  Persistent blocks take
-// tiles of kFuseTile ranges (kFusePer per wave) from a ticket in the order
+// tiles of kHeldTile ranges (kHeldPer per wave) from a ticket in the order
 // they start, so a tile's predecessors are running or done whatever else
-// shares the GPU.  A block counts its tile and publishes the count, then
-// draws and counts its NEXT tile before it takes the first one's prefix, and
-// decodes the first one with decode_range (re-reading it).  The prefix is not
-// a chained look-back: it is the counts of the tiles before it in its group
-// of 64 tiles (one status word per lane) plus the sums of the earlier groups
-// (every tile adds its count into its group's word), all loaded at once, so
-// it takes one memory round trip at any depth and waits only for tiles drawn
-// before this one to be counted -- which, counted one tile ahead, they are.
-// (Round 2's chained look-back -- back over predecessors' aggregates 64 at a
-// time to the first inclusive prefix, right after the count, three waves
-// idle at a barrier -- cost 157 of 945 us on 1 GiB at junk density 0.05,
-// profiles/r03_ab_sfx_breakdown.jsonl.)  Every block counts itself out in
-// `wdone` when it leaves; the block that decodes the last tile writes the
-// record, waits until every block has left (so no prefix read is in
-// flight), then clears the status and group words, the ticket, `wdone` and
-// the failure words.
-// At least 6 waves per SIMD (80 VGPRs).
+// shares the GPU.  A tile's prefix is not a chained look-back: it is the
+// counts of the tiles before it in its group of 64 tiles (one status word
+// per lane) plus the sums of the earlier groups (every tile adds its count
+// into its group's word), loaded at once.  (Round 2's chained look-back --
+// back over predecessors' aggregates 64 at a time to the first inclusive
+// prefix, three waves idle at a barrier -- cost 157 of 945 us on 1 GiB at
+// junk density 0.05, profiles/r03_ab_sfx_breakdown.jsonl.)  Every block
+// counts itself out in `wdone` when it leaves; the block that decodes the
+// last tile writes the record, waits until every block has left (so no
+// prefix read is in flight), then clears the status and group words, the
+// ticket, `wdone` and the failure words.  Rounds 3-5 shipped a form that
+// counted each tile one tile ahead and re-read it to decode (FETCH 2.01x the
+// input); it was removed in round 6 (DESIGN.md §5 keeps its measurements).
 
-// The idle test of k_decode_suffix<false>: false when k_decode_lines took
+// The idle test of k_decode_suffix_held<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
 // done); else S, Vb of the first failing slot, and *reprobe (pinned, the
 // launcher's: the next call of this length on the workspace probes again
@@ -2484,249 +2460,45 @@ DEV bool suffix_start(DecodeWs w, uint64_t n, b64x_dec_result *res, b64x_dec_res
     return true;
 }
 
-template <bool WHOLE>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6)))
-void k_decode_suffix(
-    const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
-    DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
-    uint32_t seq, uint32_t *reprobe)
-{
-    constexpr uint64_t R = 2 * kChunk;
-    DecodeWs w = ws_view(ws, nranges);
-    uint64_t S = 0, Vb = 0;
-    if (!WHOLE && !suffix_start(w, n, res, hres, S, Vb, reprobe)) return;
-    uint8_t *base_out = out + Vb / 4 * 3;
-    const uint32_t r0 = (uint32_t) (S / R);
-    const uint32_t ntiles = (nranges - r0 + kFuseTile - 1) / kFuseTile;
-    if (!WHOLE && blockIdx.x == 0 && threadIdx.x == 0) *w.sfx_start = S;
-    const bool dma = (((uintptr_t) in) & 15) == 0;
-    __shared__ P2dSmem sm;
-    // per wave: two ranges read ahead (an LDS object of its own, so that the
-    // compiler sees table and window reads cannot alias the copies in flight)
-    __shared__ uint4 s_rng[kWavesPerBlock][2][128];
-    __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_cnt[2][kFuseTile];
-    __shared__ uint32_t s_excl;
-    build_dec_table(sm.tab, a);
-    build_compact_sel(sm.sel);
-    const uint32_t lane = lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint4 *bq = sm.bits[wv];
-
-    // Count tile t into s_cnt[b] (each wave its kFusePer ranges; every
-    // wave's loads issued before any is counted).  Block-uniform call.
-    auto count_tile = [&](uint32_t t, uint32_t b) {
-        const uint32_t rw = r0 + t * kFuseTile + wv * kFusePer;  // this wave's first range
-        for (uint32_t j0 = 0; j0 < kFusePer; j0 += kFuseLoad) {
-            uint4 c[kFuseLoad][2];
-            uint32_t nin[kFuseLoad][2];
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj++) {
-                const uint32_t r = rw + j0 + jj;
-                const uint64_t rb = (uint64_t) r * R;
-                const uint64_t beg = rb > S ? rb : S;
-                const uint64_t re = rb + R < n ? rb + R : n;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = beg + (uint64_t) h * kChunk + 16 * lane;
-                    nin[jj][h] = r >= nranges || p >= re
-                                     ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                    c[jj][h] = nin[jj][h] ? load_chars(in + p, nin[jj][h]) : make_uint4(0, 0, 0, 0);
-                }
-            }
-            // two ranges' counts (each <= 2,048) share one packed DPP scan
-            // (a shuffle reduction per range cost 25 VALU and 6 LDS ops)
-#pragma unroll
-            for (uint32_t jj = 0; jj < kFuseLoad; jj += 2) {
-                uint32_t cnt = 0;
-#pragma unroll
-                for (uint32_t e = 0; e < 2; e++) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        uint32_t P[4];
-                        lane_values(sm.tab, c[jj + e][h], nin[jj + e][h], P);
-                        cnt += lane_valid_count(P) << (16 * e);
-                    }
-                }
-                const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane(
-                    (int) wave_incl_scan_dpp(cnt), 63);
-                if (lane == 0) {
-                    s_cnt[b][wv * kFusePer + j0 + jj] = tot & 0xFFFFu;
-                    s_cnt[b][wv * kFusePer + j0 + jj + 1] = tot >> 16;
-                }
-            }
-        }
-    };
-    // Publish tile t's count (s_cnt[b] complete): its status word and its
-    // group's sum.  Thread 0.
-    auto publish = [&](uint32_t t, uint32_t b) {
-        uint32_t agg = 0;
-        for (uint32_t i = 0; i < kFuseTile; i++) agg += s_cnt[b][i];
-        st_store(&w.fstatus[t], kStAgg | agg);
-        __hip_atomic_fetch_add(&w.fsuper[t / kSfxGroup], (1ull << 56) | agg, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // The alphabet characters of the suffix before tile t.  Wave 0.
-    auto prefix = [&](uint32_t t) -> uint32_t {
-        const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
-        const uint32_t ng = (k + 63) / 64;  // group words per lane (uniform)
-        for (;;) {
-            const uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
-            bool ok = (v & kStAgg) != 0;
-            uint32_t sum = (uint32_t) v;
-            for (uint32_t i = 0; i < ng; i++) {
-                const uint32_t j = lane + 64 * i;
-                const uint64_t g = j < k ? st_load(&w.fsuper[j]) : kGroupFull;
-                ok = ok && (g >> 56) == kSfxGroup;
-                sum += (uint32_t) g;
-            }
-            if (__all(ok)) return wave_sum(sum);
-            __builtin_amdgcn_s_sleep(2);
-        }
-    };
-
-    block_sync();  // the tables
-    if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
-    block_sync();
-    uint32_t tA = s_tile[0], bA = 0;
-    if (tA < ntiles) {
-        count_tile(tA, 0);
-        block_sync();
-        if (threadIdx.x == 0) publish(tA, 0);
-    }
-    bool owner = false;  // this block decoded the last tile
-    uint32_t Vs = 0;     // then: the suffix's alphabet characters
-    while (tA < ntiles) {
-        const uint32_t bB = bA ^ 1u;
-        if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
-        block_sync();  // also: s_cnt[bB] of two tiles back is consumed
-        const uint32_t tB = s_tile[bB];
-        if (tB < ntiles) count_tile(tB, bB);
-        block_sync();
-        if (threadIdx.x == 0 && tB < ntiles) publish(tB, bB);
-        if (wv == 0) {
-            const uint32_t ex = tA ? prefix(tA) : 0u;
-            if (lane == 0) s_excl = ex;
-        }
-        block_sync();
-        uint32_t B = s_excl;  // alphabet characters of the suffix before this wave's ranges
-        for (uint32_t i = 0; i < wv * kFusePer; i++) B += s_cnt[bA][i];
-        const uint32_t rw = r0 + tA * kFuseTile + wv * kFusePer;
-        // A whole range (2,048 characters from its aligned start) of a
-        // 16-byte aligned input is read ahead into LDS by two direct
-        // global->LDS copies (no VGPRs held) while the range before it
-        // decodes; the others (the first, from S; the stream's last) load
-        // as they decode.
-        auto whole = [&](uint32_t r) {
-            return dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
-        };
-        auto fetch = [&](uint32_t r, uint32_t buf) {
-            const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
-            lds_dma16(src, &s_rng[wv][buf][0]);
-            lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
-        };
-        if (whole(rw)) fetch(rw, 0);
-        for (uint32_t j = 0; j < kFusePer && rw + j < nranges; j++) {
-            const uint32_t r = rw + j;
-            const uint64_t rb = (uint64_t) r * R;
-            const uint64_t re = rb + R < n ? rb + R : n;
-            const bool first = r == r0, last = r + 1 == nranges;
-            const uint64_t start = first ? S : rb;
-            const bool next_dma = j + 1 < kFusePer && whole(r + 1);
-            uint4 *buf = s_rng[wv][j & 1];
-            uint32_t nin[2] = {16u, 16u};
-            // Every range goes through the LDS buffer, so that one code path
-            // decodes them all: a joined path made the compiler wait for the
-            // register path's loads (vmcnt(0), draining the copy in flight)
-            // on the copied path too.  A whole range waits for its copy; any
-            // other is loaded here (and waited for) and written there.
-            if (whole(r)) {
-                vm_wait_all();
-            } else {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
-                    nin[h] = p >= re ? 0u : (re - p >= 16 ? 16u : (uint32_t) (re - p));
-                    buf[64 * h + lane] = nin[h] ? load_chars(in + p, nin[h]) : make_uint4(0, 0, 0, 0);
-                }
-            }
-            uint4 c[2];
-            c[0] = buf[lane];
-            c[1] = buf[64 + lane];
-            // then the next range's copy: in flight while this one decodes
-            // (no global load of the compiler's is outstanding from here on)
-            if (next_dma) fetch(r + 1, (j + 1) & 1);
-            decode_range(sm, bq, in, n, start, re, first ? 0 : range_skip(B),
-                         base_out + (B + 3) / 4 * 3, c, nin, 0u, !last, last, hold,
-                         next_dma ? (const uint8_t *) s_rng[wv][(j + 1) & 1] : nullptr, true);
-            B += s_cnt[bA][wv * kFusePer + j];
-        }
-        if (tA == ntiles - 1) {
-            owner = true;
-            Vs = s_excl;
-            for (uint32_t i = 0; i < kFuseTile; i++) Vs += s_cnt[bA][i];
-        }
-        tA = tB;
-        bA = bB;
-    }
-    // every prefix read of this block is over (relaxed: the loads have
-    // returned -- their values decided the loop -- and a release at agent
-    // scope would write back the L2)
-    block_sync();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!owner || wv != 0) return;
-    const uint64_t V = Vb + Vs;
-    if (lane == 0) write_result(res, hres, V, hold, n, seq);
-    find_tail_sextets(sm.tab, in, n, V, res, hres);
-    if (lane == 0) {
-        while (__hip_atomic_load(w.wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    for (uint32_t i = lane; i < ntiles; i += 64) st_store(&w.fstatus[i], 0);
-    for (uint32_t i = lane; i < (ntiles + kSfxGroup - 1) / kSfxGroup; i += 64) st_store(&w.fsuper[i], 0);
-    if (lane == 0) {
-        __hip_atomic_store(w.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(w.wdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // (WHOLE too: after a probe, the hinted single pass, decode_dev_ws)
-        for (uint32_t i = 0; i < kFailWords; i++) w.lfail[i * kFailStride] = 0;
-        *w.fail_any = 0;
-    }
-}
-
-// ---- single-pass exact decode, each range read and looked up once ----------
+// ---- each range read and looked up once -----------------------------------
 //
-// k_decode_suffix_held: the same contract, tiles, ticket, group sums and
-// result record as k_decode_suffix, but no counting pass.  A range is
-// decoded once, at relative bit 0 of the wave's window (its prefix is not
-// known yet), and the window -- the range's output bit stream, at most
-// 1,536 bytes -- is held in VGPRs (6 dwords per lane) while the tile is
-// published and the next tile is decoded; the range's count comes out of
+// A range is decoded once, at relative bit 0 of the wave's window (its
+// prefix is not known yet), and the window -- the range's output bit stream,
+// at most 1,536 bytes -- is held in VGPRs (6 dwords per lane) while the tile
+// is published and the next tile is decoded; the range's count comes out of
 // the decode.  A tile is stored one iteration later, when its prefix is
-// known (its predecessors have had a whole tile's time to publish): the
-// held dwords go back into the window, the range's last partial group is
+// known (its predecessors have had a whole tile's time to publish): the held
+// dwords go back into the window, the range's last partial group is
 // completed from the characters after it (their raw bytes loaded when the
-// range was decoded), and the window is copied to the output shifted by
-// the range's skip (0-3 sextets the range before it completed) and the
-// output's alignment.  Each input byte is read from HBM once (the counting
-// form reads every range twice) and looked up once.  Shipped (B64X_SFX_HELD
-// = 1).  On 1 GiB at junk density 0.05 (profiles/r05_pmc_sfx_held.txt,
-// r05_ab_sfx_held*.jsonl): FETCH 1.02x the input against 2.01x, VALU -10 %,
-// SALU -27 %, LDS instructions -20 %, and the same time (747.5 / 778.4 us
-// against 746.2 / 771.7 in two A/B runs): the kernel is bound by latency at
-// 5 waves per SIMD (96 VGPRs, two tiles held while the next decodes), not
-// by its bytes.  The prefix is 12 % of it (a pricing build without it: 658
-// us).  Tried and slower: a tile's ticket drawn one iteration ahead (940
-// us), storing range j of A right after decoding range j of B (A's prefix
-// then needed one range after B is drawn: 2.2-2.8 ms, tiles waiting on
-// their predecessors), 3 or 2 ranges per wave (810 / 1,156 us; with the
-// incremental prefix 815 / 1,153 against 725), 4 waves per SIMD without
-// spills (835 us).  The prefix loads only the groups completed since the
-// block's last tile (746.5 against 778.2 us, profiles/r05_ab_sfx_prefix_incremental.jsonl).  Its first form's barriers were hipcc's
-// __syncthreads(), and the one at the top of an iteration did not wait for
-// thread 0's write of the next ticket: now and then a wave decoded another
-// tile than its block (one repeated 1 GiB decode in five came out shifted;
-// block_sync()'s explicit lgkmcnt(0) fixed it: 96 + 96 stress decodes exact,
-// scripts/held_stress.py, profiles/r05_sfx_held_*.jsonl).
+// range was decoded), and the window is copied to the output shifted by the
+// range's skip (0-3 sextets the range before it completed) and the output's
+// alignment.  Each input byte is read from HBM once and looked up once.  On
+// 1 GiB at junk density 0.05 (profiles/r05_pmc_sfx_held.txt,
+// r05_ab_sfx_held*.jsonl): FETCH 1.02x the input against the count-ahead
+// form's 2.01x, VALU -10 %, SALU -27 %, LDS instructions -20 %, and the same
+// time: the kernel is bound by latency at 5 waves per SIMD (96 VGPRs, two
+// tiles held while the next decodes), not by its bytes.  Tried and slower: a
+// tile's ticket drawn one iteration ahead (940 us), storing range j of A
+// right after decoding range j of B (2.2-2.8 ms, tiles waiting on their
+// predecessors), 3 or 2 ranges per wave (815 / 1,153 against 725), 5-8
+// ranges per wave at 3-4 waves per SIMD (807-1,031), 4 waves per SIMD
+// without spills (835 us).  The prefix loads only the groups completed since
+// the block's last tile (746.5 against 778.2 us,
+// profiles/r05_ab_sfx_prefix_incremental.jsonl).
+//
+// Its first form's barriers were hipcc's __syncthreads(), and the one at the
+// top of an iteration did not wait for thread 0's write of the next ticket:
+// now and then a wave decoded another tile than its block (one repeated
+// 1 GiB decode in five came out shifted).  The ISA shows why
+// (profiles/r06_isa_barrier_evidence.txt): the fence of __syncthreads()
+// leaves a soft s_waitcnt lgkmcnt(0) before the s_barrier, and gfx950's
+// back-off barrier needs no wait of its own, so SIInsertWaitcnts may drop
+// the soft one -- and at this loop's header it did (present in the MIR
+// before the pass, gone after), although the back edge carries thread 0's
+// ds_write of the ticket.  block_sync()'s wait is inline asm, which the pass
+// cannot drop; tests/tools/isa_check.py walks the control-flow graph of
+// every kernel in the shipped code object and finds no barrier reached with
+// an LDS write in flight (test_abi.py::test_code_object_barriers_drain_lds).
 
 // The window dword a range's held dwords go back to, so that
 // store_window_bits reads aligned 16-byte groups: the range's bits start at
@@ -2787,7 +2559,7 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
 }
 
 template <bool WHOLE>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(B64X_SFX_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kHeldWaves)))
 void k_decode_suffix_held(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
@@ -2903,6 +2675,8 @@ void k_decode_suffix_held(
     };
     // Store range j of tile A (this wave's) from its held dwords: Bp = the
     // suffix's alphabet characters before it, T its own.
+    // the window holds dwords dl + [0, 384) (dl <= 3) and the 8 zeroed after
+    static_assert(kP2dBlocks * 4 >= 3 + 384 + 8, "held window fits the wave's LDS window");
     auto store_one = [&](uint32_t r, uint32_t Bp, uint32_t T, const uint32_t Hj[6], uint32_t la) {
         const uint64_t rb = (uint64_t) r * R;
         const uint64_t re = rb + R < n ? rb + R : n;
@@ -2956,10 +2730,9 @@ void k_decode_suffix_held(
     // stored after tile B is drawn, decoded and published, so that A's
     // predecessors have had a whole tile's time to publish.
     // (LA: the bytes after each held range, byte j for range j)
-    using LT = typename std::conditional<(HP > 4), uint64_t, uint32_t>::type;
     uint32_t HA[HP][6];
-    LT LA = 0;
-    static_assert(HP <= 8, "one byte per held range in LA");
+    uint32_t LA = 0;
+    static_assert(HP <= 4, "one byte per held range in LA");
 #pragma unroll
     for (uint32_t j = 0; j < HP; j++) {
 #pragma unroll
@@ -2975,7 +2748,7 @@ void k_decode_suffix_held(
         const bool haveB = tB < ntiles;
         if (!haveA && !haveB) break;
         uint32_t HB[HP][6];
-        LT LB = 0;
+        uint32_t LB = 0;
         if (haveB) {
             const uint32_t rwB = r0 + tB * TILE + wv * HP;
             if (whole(rwB)) fetch(rwB, 0);
@@ -2983,7 +2756,7 @@ void k_decode_suffix_held(
             for (uint32_t j = 0; j < HP; j++) {
                 uint32_t lan;
                 decode_one(rwB, j, bB, HB[j], lan);
-                LB |= (LT) lan << (8 * j);
+                LB |= lan << (8 * j);
             }
         }
         block_sync();  // s_cnt[bB] complete
@@ -4169,7 +3942,8 @@ struct RowsShape {
 
 struct WsEntry {
     int dev;
-    void *stream;       // bound stream; nullptr = idle (reusable)
+    bool bound;         // held by `stream` (which may be the NULL stream); else idle
+    void *stream;       // the stream it is bound to (meaningful only when bound)
     void *ws;           // nullptr: slot not allocated yet
     hipEvent_t last;    // recorded behind the last use when it left a stream
     bool recorded;      // `last` guards a use on a stream it has left
@@ -4430,7 +4204,7 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
         std::lock_guard<std::mutex> lk(g_ws_mu);
         for (int i = 0; i < kWsCache; i++) {
             WsEntry &e = g_ws[i];
-            if (e.ws && e.dev == dev && e.stream == stream && !e.release) {
+            if (e.ws && e.dev == dev && e.bound && e.stream == stream && !e.release) {
                 e.used = ++g_ws_tick;
                 e.pins++;
                 *slot = i;
@@ -4455,7 +4229,7 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
                     (v < 0 || e.used < g_ws[v].used))
                     v = i;
             }
-            if (v < 0 || !g_ws[v].stream || !capturing(g_ws[v].stream)) break;
+            if (v < 0 || !g_ws[v].bound || !capturing(g_ws[v].stream)) break;
             skip |= 1u << v;
         }
         if (v < 0)
@@ -4467,7 +4241,7 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
         }
         WsEntry &e = g_ws[v];
         fresh = !e.ws;
-        if (!fresh && e.stream) {
+        if (!fresh && e.bound) {
             // taken from a stream that still holds it: mark the end of
             // everything enqueued there so far, its last use included (an
             // enqueue, no wait; under the lock, so the owner cannot release
@@ -4482,6 +4256,7 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
         after = e.last;
         if (fresh) e = WsEntry{};
         e.dev = dev;
+        e.bound = true;
         e.stream = stream;
         e.used = ++g_ws_tick;
         e.pins = 1;  // reserved: nobody else takes this slot
@@ -4512,7 +4287,8 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
     }
     std::lock_guard<std::mutex> lk(g_ws_mu);
     if (rc) {
-        g_ws[v].stream = nullptr;  // idle again, its event still guards it
+        g_ws[v].bound = false;  // idle again, its event still guards it
+        g_ws[v].stream = nullptr;
         g_ws[v].pins = 0;
         *err = rc;
         return nullptr;
@@ -4527,10 +4303,11 @@ static void *library_workspace(void *stream, int *slot, int *err, RowsShape *row
 // the workspace's last use) with the entry's event.  Under g_ws_mu.
 static void ws_leave(WsEntry &e)
 {
-    if (e.stream && hipEventRecord(e.last, (hipStream_t) e.stream) == hipSuccess)
+    if (e.bound && hipEventRecord(e.last, (hipStream_t) e.stream) == hipSuccess)
         e.recorded = true;
-    else if (e.stream)
+    else if (e.bound)
         e.recorded = false;  // nothing to wait on; the caller owns the ordering
+    e.bound = false;
     e.stream = nullptr;
     e.release = false;
 }
@@ -4556,7 +4333,7 @@ void b64x_release_stream(void *stream)
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (int i = 0; i < kWsCache; i++) {
         WsEntry &e = g_ws[i];
-        if (!e.ws || e.dev != dev || e.stream != stream) continue;
+        if (!e.ws || e.dev != dev || !e.bound || e.stream != stream) continue;
         if (e.pins)
             e.release = true;  // the last unpin unbinds it
         else
@@ -4622,7 +4399,7 @@ static uint32_t *rows_stale(int slot)
 // Workspaces whose line model (k_decode_probe's, kept in the workspace with
 // the length it was made for) a call of the same length may reuse without a
 // probe: one entry per hash of the workspace, and a pinned flag beside it
-// that k_decode_suffix<false> raises when a call found anything to decode
+// that k_decode_suffix_held<false> raises when a call found anything to decode
 // past k_decode_lines (junk, another format, a cut model), so that the next
 // call probes again.  A wrong entry or a late flag only costs speed: any
 // model gives exact output, and k_decode_lines checks the model's length.
@@ -4676,15 +4453,6 @@ static uint32_t hint_key(const void *ws, const void *in, uint64_t n)
 }
 
 // decode_dev_impl's launches on a given workspace.
-// The single-pass suffix decode: the counting form or the held form
-// (B64X_SFX_HELD; same arguments, same workspace).
-extern "C++" {
-template <bool WHOLE>
-static auto sfx_kernel()
-{
-    return B64X_SFX_HELD ? k_decode_suffix_held<WHOLE> : k_decode_suffix<WHOLE>;
-}
-}  // extern "C++"
 
 static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
                          b64x_dec_result *d_res, b64x_dec_result *h_res,
@@ -4703,10 +4471,10 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         // of whatever suffix it could not take -- nothing, on clean and
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
-        static const int occ_sfx = occupancy_of(sfx_kernel<false>());
+        static const int occ_sfx = occupancy_of(k_decode_suffix_held<false>);
         const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
         if (flags & B64X_DEC_EXPECT_JUNK) {
-            hipLaunchKernelGGL(sfx_kernel<true>(), dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(k_decode_suffix_held<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
@@ -4745,7 +4513,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         }
         if (junky) {
             path_taken(kPathHinted);
-            hipLaunchKernelGGL(sfx_kernel<true>(), dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(k_decode_suffix_held<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
@@ -4755,7 +4523,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
                            dim3(kLinesTH), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
-        hipLaunchKernelGGL(sfx_kernel<false>(), dim3(sfx_grid), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(k_decode_suffix_held<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                            hold, d_res, h_res, seq, reprobe);
         return launch_status();
@@ -5831,11 +5599,7 @@ const char *b64x_build_info(void)
 #define B64X_STR(x) B64X_STR2(x)
     return "b64x abi=" B64X_STR(B64X_ABI_VERSION) " arch=gfx950 enc:quad12->16 lds-alphabet "
            "1 quad/lane; dec:probe+line-model single pass (4 slots/lane) + exact suffix "
-#if B64X_SFX_HELD
            "(decoded once, held until its prefix, group sums, LDS read-ahead); rows:line model in row "
-#else
-           "(count ahead, group sums, LDS read-ahead); rows:line model in row "
-#endif
            "bands; lanes:chained decoder blocks";
 }
 

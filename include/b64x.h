@@ -185,8 +185,13 @@ int b64x_decode_dev_seq(const void *d_in, uint64_t nchars, void *d_out,
 int b64x_result_check(const b64x_dec_result *res, uint64_t nchars, unsigned flags,
                       uint32_t seq);
 /* Unbind the library-owned decode workspace of `stream` on the current
- * device, if it has one, so another stream can take it; call it before
- * destroying a stream that decoded with d_workspace == NULL. */
+ * device, if it has one, so another stream can take it.  REQUIRED before
+ * destroying a stream that decoded with d_workspace == NULL: the workspace
+ * stays bound to the stream's handle, and a later call on another stream
+ * that takes it over records an event on that handle (and asks whether it
+ * is being captured) -- on a destroyed stream that is a dangling handle.
+ * Released here, the event is recorded while the stream is still alive.
+ * The NULL stream may hold a workspace like any other. */
 void b64x_release_stream(void *stream);
 
 /* ---- batches of independent buffers ----------------------------------- */

@@ -80,6 +80,97 @@ def test_kernel_barriers_wait_for_lds():
     assert "__syncthreads()" not in code[:a] + code[b:]
 
 
+def _isa():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "tools"))
+    import isa_check
+    return isa_check, isa_check.disassemble(_lib.LIB_PATH)
+
+
+# The kernels the product launches (b64x_kernels.hip); nothing else may be in
+# its code object: no A/B variant, no experiment, no test hook.
+SHIPPED_KERNELS = {
+    "k_encode", "k_encode_flat", "k_encode_tight2<2>", "k_encode_strided<2, true>",
+    "k_encode_ragged",
+    "k_decode_probe", "k_decode_lines", "k_decode_suffix_held<false>",
+    "k_decode_suffix_held<true>", "k_decode_pass1<2, true>", "k_decode_scan2",
+    "k_decode_pass2d",
+    "k_decode_slots<2>", "k_rows_prep", "k_decode_rows_lines<4, false>",
+    "k_decode_rows_lines<4, true>", "k_rows_finish", "k_decode_batch_fast<false>",
+    "k_decode_batch_fast<true>", "k_decode_batch_fix2<false>", "k_decode_batch_fix2<true>",
+    "k_batch_finish",
+    "k_result_zero", "k_stamp", "k_spell_head", "k_gather_host", "k_fill_splitmix64",
+}
+
+
+def test_code_object_holds_only_shipped_kernels():
+    """the experiments (the count-ahead suffix kernel, the
+    tile-shape knobs) are out of the product translation unit; the code
+    object's kernel symbols are exactly the kernels the library launches."""
+    isa, dis = _isa()
+    names = subprocess.run(["c++filt"], input="\n".join(sorted(isa.kernel_symbols(dis))),
+                           capture_output=True, text=True, check=True).stdout.split("\n")
+    got = set()
+    for n in names:
+        if not n:
+            continue
+        m = re.match(r"^(?:void )?(?:\(anonymous namespace\)::)?([\w]+(?:<[^>]*>)?)\(", n)
+        got.add(m.group(1) if m else n)
+    assert got == SHIPPED_KERNELS, (got - SHIPPED_KERNELS, SHIPPED_KERNELS - got)
+
+
+def test_code_object_barriers_drain_lds():
+    """On gfx950 the hardware barrier does not wait for LDS writes, and the
+    compiler may drop the soft lgkmcnt(0) that __syncthreads()'s fence leaves
+    before it (it did at k_decode_suffix_held's loop header in round 5:
+    profiles/r06_isa_barrier_evidence.txt).  Over the control-flow graph of
+    every kernel in the shipped code object, no s_barrier is reached with an
+    LDS write or a global -> LDS copy in flight; and in the kernels that copy
+    into LDS, the only LDS reads reached while a copy may be in flight are the
+    decode table's byte lookups (the copies' buffers are read after the
+    reader's own vmcnt(0))."""
+    isa, dis = _isa()
+    assert isa.barrier_count(dis) > 20
+    assert isa.barrier_report(dis) == []
+    reads = isa.dma_reads(dis)
+    assert reads, "k_decode_suffix_held copies its ranges into LDS"
+    for name, rows in reads.items():
+        kinds = {re.sub(r"\s+v\d+, v\d+", "", t) for _, t in rows}
+        assert len(kinds) <= 1 and all(k.startswith("ds_read_u8") for k in kinds), (name, kinds)
+
+
+def test_isa_check_finds_the_round5_race():
+    """The checker flags the pattern it is meant to catch: a loop whose
+    header barrier has no wait while its back edge carries an LDS write
+    (a hand-written listing in the disassembler's format)."""
+    sys_path = os.path.join(ROOT, "tests", "tools")
+    import sys
+    sys.path.insert(0, sys_path)
+    import isa_check
+    def listing(wait):
+        rows = ["0000000000001000 <k>:",
+                "\tv_mov_b32_e32 v2, 0 // 000000001000: 0",
+                "\tds_write_b32 v2, v1 offset:64 // 000000001004: 0",
+                "\ts_waitcnt lgkmcnt(0) // 000000001008: 0",
+                "\ts_barrier // 00000000100C: 0",
+                "\tv_lshlrev_b32_e32 v3, 2, v61 // 000000001010: 0"]
+        if wait:
+            rows.append("\ts_waitcnt lgkmcnt(0) // 000000001014: 0")
+        else:
+            rows.append("\ts_nop 0 // 000000001014: 0")
+        rows += ["\ts_barrier // 000000001018: 0",
+                 "\tds_read_b32 v3, v3 offset:64 // 00000000101C: 0",
+                 "\ts_waitcnt lgkmcnt(0) // 000000001020: 0",
+                 "\tds_write_b32 v6, v4 offset:64 // 000000001024: 0",
+                 "\ts_cbranch_vccz 1 // 000000001028: 0 <k+0x30>",
+                 "\ts_branch 65528 // 00000000102C: 0 <k+0x10>",
+                 "\ts_endpgm // 000000001030: 0"]
+        return "\n".join(rows)
+    assert isa_check.barrier_report(listing(True)) == []
+    bad = isa_check.barrier_report(listing(False))
+    assert [(r[1], r[2]) for r in bad] == [(0x18, "lds")]
+
+
 def test_every_environment_knob_is_documented():
     """Every ASYNC_B64_* variable the product libraries can read is in
     INTEGRATION.md's runtime-configuration table."""

@@ -1295,6 +1295,67 @@ def test_workspace_taken_over_while_its_stream_is_busy():
         lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
 
 
+def test_workspace_taken_over_from_the_null_stream():
+    """the NULL stream (torch's default stream, cuda_stream == 0)
+    holds a library workspace like any other stream.  Its handle is 0, which
+    the workspace cache once also used to mean "idle": a side stream taking
+    the NULL stream's workspace over then recorded no event on it and did not
+    wait for the NULL stream's queued decode, so two junk-laden decodes ran
+    on one set of tickets and tile words at once.  Here the NULL stream's
+    decode is queued behind a GPU sleep, the side stream's behind one as long,
+    and the side stream takes the NULL stream's workspace over (it is the
+    least recently used); both outputs must be exact."""
+    import ctypes
+
+    from async_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(1234)
+    a = b64._abc(None)
+
+    def job(n, seed):
+        raw = np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+        text = _junk(rng, orc.encode(raw), 0.05)
+        x = dev(text)
+        out = torch.zeros(b64.decoded_cap(len(text)) + 8, dtype=torch.uint8, device=DEV)
+        res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
+        return raw, x, out, res
+
+    def decode(j, st, flags=0):
+        raw, x, out, res = j
+        assert lib.b64x_decode_dev(ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                   ctypes.byref(a), flags, None,
+                                   ctypes.c_void_p(st)) == 0
+
+    side = [torch.cuda.Stream() for _ in range(8)]
+    small = job(50_000, 1)
+    big0 = job(48 << 20, 2)
+    big1 = job(48 << 20, 3)
+    torch.cuda.synchronize()
+    for st in side:  # start from no side stream holding a workspace
+        lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
+    lib.b64x_release_stream(ctypes.c_void_p(0))
+    decode(small, 0)                       # the NULL stream binds one
+    for st in side[:7]:                    # seven more, used after it
+        decode(small, st.cuda_stream)
+    torch.cuda.synchronize()
+    cur = torch.cuda.current_stream()
+    assert cur.cuda_stream == 0, "torch's default stream is the NULL stream"
+    torch.cuda._sleep(40_000_000)          # ~20 ms on the NULL stream
+    decode(big0, 0, b64.EXPECT_JUNK)       # queued behind it
+    for st in side[:7]:                    # the seven become more recent
+        decode(small, st.cuda_stream)
+    with torch.cuda.stream(side[7]):
+        torch.cuda._sleep(40_000_000)      # as long on the taking stream
+    decode(big1, side[7].cuda_stream, b64.EXPECT_JUNK)  # takes the NULL stream's over
+    torch.cuda.synchronize()
+    for raw, x, out, res in (small, big0, big1):
+        assert np.array_equal(out[:raw.size].cpu().numpy(), raw)
+    for st in side:
+        lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
+    lib.b64x_release_stream(ctypes.c_void_p(0))
+
+
 def test_library_workspace_is_bounded():
     """Decodes with d_workspace == NULL on 100 fresh streams keep at most 8
     library workspaces (~12.7 MiB of HBM each), not one per stream forever;
