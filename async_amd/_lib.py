@@ -113,6 +113,8 @@ SIGNATURES = {
     "b64x_diag_paths": (None, [ctypes.POINTER(_u64)]),
     "b64x_fill_splitmix64": (_int, [_vp, _u64, _u64, _vp]),
     "b64x_device_check": (_int, []),
+    "b64x_device_numa_node": (_int, [_int]),
+    "b64x_bind_thread": (_int, [_int]),
     "b64x_build_info": (ctypes.c_char_p, []),
     "b64x_strerror": (ctypes.c_char_p, [_int]),
 }

@@ -228,6 +228,19 @@ def fill_splitmix64(x: torch.Tensor, seed: int, stream=None) -> torch.Tensor:
     return x
 
 
+def device_numa_node(device: int = -1) -> int:
+    """The NUMA node the GPU hangs off (b64x_device_numa_node); negative
+    errno when unknown."""
+    return _lib.load().b64x_device_numa_node(device)
+
+
+def bind_thread(device: int = -1) -> int:
+    """Bind the calling thread to the GPU's NUMA node (b64x_bind_thread):
+    threads it starts afterwards inherit the mask.  Returns the node or a
+    negative errno (the thread unchanged)."""
+    return _lib.load().b64x_bind_thread(device)
+
+
 def device_check() -> None:
     """Raise unless a gfx950 device is usable by the library."""
     _lib.check("b64x_device_check", _lib.load().b64x_device_check())

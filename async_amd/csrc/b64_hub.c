@@ -647,6 +647,10 @@ b64_hub *b64_hub_acquire(async_t *async)
         errno = e;
         return NULL;
     }
+    /* the loop's thread onto the GPU's NUMA node (b64x_bind_thread): its
+     * copies into pinned arenas and out of them are the loop's work */
+    if (env_bytes("ASYNC_B64_BIND", 1, 0) != 0)
+        (void) b64x_bind_thread(-1);
     h->users = 1;
     h->next_hub = registry;
     registry = h;

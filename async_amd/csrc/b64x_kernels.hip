@@ -43,10 +43,13 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <mutex>
@@ -4081,6 +4084,93 @@ uint64_t b64x_decode_workspace_size(uint64_t nchars)
 }
 
 int b64x_device_check(void) { return device_info() ? 0 : -ENODEV; }
+
+// ---- host placement (sysfs; no libnuma in the image) ----------------------
+
+static bool read_small(const char *path, char *buf, size_t cap)
+{
+    FILE *f = fopen(path, "r");
+    if (!f) return false;
+    const size_t n = fread(buf, 1, cap - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    return n > 0;
+}
+
+int b64x_device_numa_node(int device)
+{
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return -ENODEV;
+    char bus[64];
+    if (hipDeviceGetPCIBusId(bus, (int) sizeof bus, device) != hipSuccess) return -ENODEV;
+    for (char *c = bus; *c; c++)
+        if (*c >= 'A' && *c <= 'F') *c = (char) (*c - 'A' + 'a');
+    char path[160], v[32];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (!read_small(path, v, sizeof v)) return -ENOENT;
+    const int node = atoi(v);
+    return node >= 0 ? node : -ENOENT;
+}
+
+// "0-63,128-191" -> set
+static bool parse_cpulist(const char *s, cpu_set_t *set)
+{
+    CPU_ZERO(set);
+    bool any = false;
+    while (*s) {
+        char *e = nullptr;
+        long a = strtol(s, &e, 10);
+        if (e == s) break;
+        long b = a;
+        s = e;
+        if (*s == '-') {
+            b = strtol(s + 1, &e, 10);
+            s = e;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++) {
+            CPU_SET((int) c, set);
+            any = true;
+        }
+        while (*s == ',' || *s == '\n' || *s == ' ') s++;
+    }
+    return any;
+}
+
+int b64x_bind_thread(int device)
+{
+    const int node = b64x_device_numa_node(device);
+    if (node < 0) return node;
+    char path[96], list[4096];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    cpu_set_t on_node, mine, both;
+    if (!read_small(path, list, sizeof list) || !parse_cpulist(list, &on_node)) return -ENOENT;
+    if (sched_getaffinity(0, sizeof mine, &mine) != 0) return -errno;
+    CPU_AND(&both, &on_node, &mine);
+    if (CPU_COUNT(&both) == 0) return -ENOENT;  // the thread may not run there
+    if (CPU_EQUAL(&both, &mine)) return node;   // already inside the node
+    // a mask inside another single node: the application placed the thread
+    bool one_node = true;
+    int first = -1;
+    for (int c = 0; c < CPU_SETSIZE && one_node; c++) {
+        if (!CPU_ISSET(c, &mine)) continue;
+        char np[96];
+        int n = -1;
+        for (int k = 0; k < 64 && n < 0; k++) {
+            snprintf(np, sizeof np, "/sys/devices/system/cpu/cpu%d/node%d", c, k);
+            if (access(np, F_OK) == 0) n = k;
+        }
+        if (first < 0) first = n;
+        else if (n != first) one_node = false;
+    }
+    if (one_node) return first;
+    if (sched_setaffinity(0, sizeof both, &both) != 0) return -errno;
+    // prefer the node for the pages this thread faults in from now on
+    unsigned long mask[16] = {0};
+    if (node < 64 * 16) {
+        mask[node / 64] = 1ul << (node % 64);
+        (void) syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, (unsigned long) 64 * 16);
+    }
+    return node;
+}
 
 int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
                     const b64x_alphabet *abc, void *stream)

@@ -176,6 +176,27 @@ def preheat(ms: float = PREHEAT_MS):
         a[0].copy_(a[1])
 
 
+def bench_placement(b64):
+    """Put this rank's host side on its GPU's NUMA node and say where it is.
+    The main thread is bound (b64x_bind_thread) before anything else runs,
+    so the buffers it fills and every thread it starts (the CPU baseline's,
+    the harness's loops) live on the GPU's node; each loop's hub binds its
+    thread again (ASYNC_B64_BIND).  One loop of config 5 ran 6.1-6.2 GiB/s
+    on the GPU's node and 4.4-4.5 on the other socket of the same box: the
+    scheduler's choice was round 5's box-to-box spread
+    (profiles/r06_numa_probe.jsonl)."""
+    from async_amd import placement as pl
+    dev = torch.cuda.current_device()
+    node = b64.bind_thread(dev)
+    topo = pl.topology(dev)
+    cpus = sorted(os.sched_getaffinity(0))
+    return {"gpu_node": topo["gpu_node"], "gpu_pci": topo["gpu_pci"], "link": topo["link"],
+            "numa_nodes": topo["nodes"], "main_thread_node": node,
+            "main_thread_cpus": pl.cpulist(cpus),
+            "loops": "bound to the GPU's node by their hub" if
+                     os.environ.get("ASYNC_B64_BIND", "1") != "0" else "unbound (ASYNC_B64_BIND=0)"}
+
+
 def bench_single(args, world, rank, b64):
     N = args.size
     E = b64.encoded_len(N)
@@ -1111,6 +1132,7 @@ def main():
     from async_amd import b64
 
     b64.device_check()
+    placement = bench_placement(b64)
     r = bench_single(args, world, rank, b64)
     ceiling = copy_ceilings(r["N"], r["E"]) if rank == 0 else None
     batch = None if args.no_batch else bench_batch(args, world, rank, b64)
@@ -1213,6 +1235,7 @@ def main():
             "root_scatter": scatter,
             "mime_decode": mime,
             "cfg5_egress": cfg5,
+            "placement": placement,
             "process_group": {"backend": dist.get_backend() if world > 1 else None,
                               "world_size": dist.get_world_size() if world > 1 else 1},
         }

@@ -411,6 +411,24 @@ int b64x_fill_splitmix64(void *d_out, uint64_t n, uint64_t seed,
 
 /* 0 if a gfx950 device is usable, -ENODEV otherwise. */
 int b64x_device_check(void);
+
+/* ---- host placement ------------------------------------------------------ */
+
+/* The NUMA node the GPU `device` (-1: the current device) hangs off, from
+ * sysfs; -ENOENT when unknown (no NUMA, a virtual device).  */
+int b64x_device_numa_node(int device);
+/* Bind the calling thread to the CPUs of `device`'s NUMA node (-1: the
+ * current device) that its affinity mask allows, and prefer that node for
+ * the pages it faults in.  Event loops that feed a GPU spend their time
+ * copying messages into pinned arenas and reading frames back: one loop ran
+ * config 5 at 6.1-6.2 GiB/s on the GPU's node and 4.4-4.5 on the other
+ * socket of the same box (profiles/r06_numa_probe.jsonl).  A thread whose
+ * mask already lies inside one node (the application placed it) is left as
+ * it is.  Returns the node the thread runs on afterwards, or a negative errno
+ * (-ENOENT: the node or its CPUs are unknown; the thread is unchanged).  The
+ * batching hub calls it on a loop's thread when the loop gets its first GPU
+ * stage, unless ASYNC_B64_BIND=0. */
+int b64x_bind_thread(int device);
 /* Static description of the compiled kernels (for logs). */
 const char *b64x_build_info(void);
 const char *b64x_strerror(int err);

@@ -365,6 +365,13 @@ int b64x_device_check(void)
     return 0;
 }
 
+/* No device, no node: the hub's binding leaves the thread as it is. */
+int b64x_bind_thread(int device)
+{
+    (void) device;
+    return -ENOENT;
+}
+
 /* Pinned buffers stand-in: the allocation ends (64-byte aligned) right
  * before an inaccessible page, so that a write past a buffer's end faults
  * here as it does against the real pinned mappings (calloc'd buffers let

@@ -171,6 +171,33 @@ def test_isa_check_finds_the_round5_race():
     assert [(r[1], r[2]) for r in bad] == [(0x18, "lds")]
 
 
+def test_bind_thread_without_a_gpu_leaves_the_thread():
+    """b64x_bind_thread (and the hub's call of it) is a no-op that reports an
+    error when there is no device: the thread's CPU mask is unchanged."""
+    import threading
+    lib = _lib.load()
+    out = {}
+
+    def run():
+        before = os.sched_getaffinity(0)
+        out["rc"] = lib.b64x_bind_thread(-1)
+        out["same"] = os.sched_getaffinity(0) == before
+        out["node"] = lib.b64x_device_numa_node(-1)
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    assert out["rc"] < 0 and out["same"] and out["node"] < 0
+
+
+def test_placement_helpers():
+    from async_amd import placement as pl
+    assert pl.parse_cpulist("0-3,7,9-10") == {0, 1, 2, 3, 7, 9, 10}
+    assert pl.cpulist({0, 1, 2, 3, 7, 9, 10}) == "0-3,7,9-10"
+    cpus = os.sched_getaffinity(0)
+    assert pl.cpu_node(min(cpus)) >= 0 or not os.path.isdir("/sys/devices/system/node/node0")
+    assert isinstance(pl.pages_by_node(1 << 20), dict)
+
+
 def test_every_environment_knob_is_documented():
     """Every ASYNC_B64_* variable the product libraries can read is in
     INTEGRATION.md's runtime-configuration table."""

@@ -7,6 +7,8 @@ properties (digests recorded from the reference, round trips, lengths).
 """
 import hashlib
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -1354,6 +1356,45 @@ def test_workspace_taken_over_from_the_null_stream():
     for st in side:
         lib.b64x_release_stream(ctypes.c_void_p(st.cuda_stream))
     lib.b64x_release_stream(ctypes.c_void_p(0))
+
+
+def test_bind_thread_puts_the_thread_on_the_gpus_node():
+    """b64x_bind_thread: the calling thread's CPU mask afterwards lies inside
+    the GPU's NUMA node (sysfs), within what it was allowed before; a thread
+    already inside one node is left as it is.  Run on threads of their own,
+    so the test process keeps its mask."""
+    import threading
+
+    from async_amd import placement as pl
+    node = b64.device_numa_node(0)
+    if node < 0:
+        pytest.skip("no NUMA node for the GPU on this box")
+    on_node = pl.node_cpus(node)
+    out = {}
+
+    def run():
+        before = os.sched_getaffinity(0)
+        out["rc"] = b64.bind_thread(0)
+        out["after"] = os.sched_getaffinity(0)
+        out["before"] = before
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    if not (out["before"] & on_node):
+        assert out["rc"] < 0 and out["after"] == out["before"]
+        return
+    assert out["rc"] == node
+    assert out["after"] <= on_node and out["after"] <= out["before"]
+    other = out["before"] - on_node
+    if other:
+        def run2():
+            os.sched_setaffinity(0, other)
+            out["rc2"] = b64.bind_thread(0)
+            out["after2"] = os.sched_getaffinity(0)
+        t = threading.Thread(target=run2)
+        t.start()
+        t.join()
+        assert out["after2"] == other and out["rc2"] != node
 
 
 def test_library_workspace_is_bounded():
