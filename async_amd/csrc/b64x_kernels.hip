@@ -1956,6 +1956,57 @@ DEV void lines_first_fail(uint32_t badm, uint32_t &fail_u, uint32_t &fail_lane)
     }
 }
 
+// k_decode_lines' hot path for line-structured text (a full wave, aligned
+// buffers, every window inside the input): lane slot t0 + 64 u + lane for u
+// < kLinesU; returns the lane's failed-slot bits.  A4: L % 4 == 0 (RFC
+// 2045's 76, PEM's 64), where a line end falls on a dword of the slot.
+template <bool A4>
+DEV uint32_t lines_hot(const uint8_t *tab, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                       const LineModel &m, uint32_t line0, uint32_t col0, uint32_t t0,
+                       uint32_t lane)
+{
+    const uint32_t L = m.L, s = m.s, P = m.P;
+    uint4 win[kLinesU];
+    uint2 wx[kLinesU];
+    uint32_t oo[kLinesU], cc[kLinesU];
+    bool hs[kLinesU];
+    const uint32_t pos0 = line0 * P;  // wave-uniform
+#pragma unroll
+    for (uint32_t u = 0; u < kLinesU; u++) {
+        // rel < L + 4,096 and rcp < 2^16: 24-bit products (full rate;
+        // a 32-bit multiply issues at a quarter of it), exact
+        const uint32_t rel = col0 + 16 * (u * 64 + lane);
+        const uint32_t dl = __umul24(rel, m.rcp) >> 20;
+        const uint32_t col = rel - __umul24(dl, L);
+        const uint32_t pos = pos0 + __umul24(dl, P) + col;
+        hs[u] = L - col <= 16;  // a line ends in (or right after) the slot
+        cc[u] = hs[u] ? L - col : 16u;
+        oo[u] = pos & 3u;
+        const uint8_t *ab = in + (pos & ~3u);
+        win[u] = ld16<false>(ab);  // (non-temporal: neutral, r02_ab_lines_ntl.jsonl)
+        const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
+        wx[u] = make_uint2(v.x, v.y);
+    }
+    const uint32_t need = sep_need(s);
+    uint32_t badm = 0;  // bit u: this lane's slot u failed
+#pragma unroll
+    for (uint32_t u = 0; u < kLinesU; u++) {
+        const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
+        uint32_t sep, G[4], bad;
+        const uint4 d = A4 ? slot_chars4(w6, oo[u], cc[u] >> 2, s, &sep)
+                           : slot_chars(w6, oo[u], cc[u], s, &sep);
+        map_fast(tab, d, 16, G, bad);
+        // the separator bytes of a line that ends here must all be
+        // outside the alphabet (looked up by every lane, kept by those)
+        // (no branch: the bytes required are zero where no line ends)
+        const uint32_t nd = hs[u] ? need : 0u;
+        if ((sep_nonalpha(tab, sep) & nd) != nd) bad |= 0x100u;
+        badm |= bad ? 1u << u : 0u;
+        emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
+    }
+    return badm;
+}
+
 __global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
@@ -2033,46 +2084,15 @@ void k_decode_lines(
         lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns && L != 0 && full && oal && ial && safe) {
         // The hot path of line-structured text: 32-bit offsets from the
-        // input's base, unguarded window loads, non-temporal stores.
-        const bool a4 = (L & 3) == 0;
-        uint4 win[kLinesU];
-        uint2 wx[kLinesU];
-        uint32_t oo[kLinesU], cc[kLinesU];
-        bool hs[kLinesU];
-        const uint32_t pos0 = line0 * P;  // wave-uniform
-#pragma unroll
-        for (uint32_t u = 0; u < kLinesU; u++) {
-            // rel < L + 4,096 and rcp < 2^16: 24-bit products (full rate;
-            // a 32-bit multiply issues at a quarter of it), exact
-            const uint32_t rel = col0 + 16 * (u * 64 + lane);
-            const uint32_t dl = __umul24(rel, m.rcp) >> 20;
-            const uint32_t col = rel - __umul24(dl, L);
-            const uint32_t pos = pos0 + __umul24(dl, P) + col;
-            hs[u] = L - col <= 16;  // a line ends in (or right after) the slot
-            cc[u] = hs[u] ? L - col : 16u;
-            oo[u] = pos & 3u;
-            const uint8_t *ab = in + (pos & ~3u);
-            win[u] = ld16<false>(ab);  // (non-temporal: neutral, r02_ab_lines_ntl.jsonl)
-            const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
-            wx[u] = make_uint2(v.x, v.y);
-        }
-        const uint32_t need = sep_need(s);
-        uint32_t badm = 0;  // bit u: this lane's slot u failed
-#pragma unroll
-        for (uint32_t u = 0; u < kLinesU; u++) {
-            const uint32_t w6[6] = {win[u].x, win[u].y, win[u].z, win[u].w, wx[u].x, wx[u].y};
-            uint32_t sep, G[4], bad;
-            const uint4 d = a4 ? slot_chars4(w6, oo[u], cc[u] >> 2, s, &sep)
-                               : slot_chars(w6, oo[u], cc[u], s, &sep);
-            map_fast(tab, d, 16, G, bad);
-            // the separator bytes of a line that ends here must all be
-            // outside the alphabet (looked up by every lane, kept by those)
-            // (no branch: the bytes required are zero where no line ends)
-            const uint32_t nd = hs[u] ? need : 0u;
-            if ((sep_nonalpha(tab, sep) & nd) != nd) bad |= 0x100u;
-            badm |= bad ? 1u << u : 0u;
-            emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
-        }
+        // input's base, unguarded window loads, non-temporal stores.  Two
+        // instances, one per line-length class, behind a wave-uniform branch:
+        // written as `a4 ? slot_chars4(..) : slot_chars(..)` the compiler
+        // computed both forms for every slot and selected (692 VALU for a
+        // wave's 4 slots in the listing, ~250 of them the general form that
+        // CRLF-76 never uses).
+        const uint32_t badm = (L & 3) == 0
+            ? lines_hot<true>(tab, in, out, m, line0, col0, t0, lane)
+            : lines_hot<false>(tab, in, out, m, line0, col0, t0, lane);
         lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns) {
         // Everything else (a partial wave, the input's end, misaligned
