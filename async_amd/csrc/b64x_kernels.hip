@@ -53,6 +53,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "b64x.h"
@@ -919,14 +920,20 @@ constexpr uint32_t kScanTile = 1024;  // ranges per scan tile: 256 threads x 4
 constexpr uint32_t kHeldPer = 4;
 constexpr uint32_t kHeldWaves = 5;  // waves per SIMD (96 VGPRs: two tiles held)
 constexpr uint32_t kHeldTile = kHeldPer * kWavesPerBlock;
+// Inputs up to kLinesMaxChars characters (8 Gi: 6 GiB of payload) take the
+// probe / lines / held-suffix decode with 2,048-character ranges -- up to
+// kLinesMaxRanges of them, whose tile words the workspace's fixed regions
+// hold; larger ones pass 1, the scan and pass 2 (kMaxRanges longer ranges).
+constexpr uint64_t kLinesMaxChars = 1ull << 33;
+constexpr uint32_t kLinesMaxRanges = (uint32_t) (kLinesMaxChars / (2 * kChunk));
 constexpr uint32_t kFailWords = 64, kFailStride = 16;
 constexpr uint64_t kWsModelN = 64;                                        // the model's stream length
 constexpr uint64_t kWsStatus = 128;                                       // scan tile status
 constexpr uint64_t kWsFStatus = kWsStatus + kMaxRanges / kScanTile * 8;   // suffix tile status
 constexpr uint32_t kSfxGroup = 64;  // k_decode_suffix_held: tiles per group sum
 constexpr uint64_t kGroupFull = (uint64_t) kSfxGroup << 56;
-constexpr uint64_t kWsFSuper = kWsFStatus + (kMaxRanges / kHeldTile + 1) * 8;   // suffix group sums
-constexpr uint64_t kWsFail = kWsFSuper + (kMaxRanges / kHeldTile / kSfxGroup + 16) * 8;  // lines failures
+constexpr uint64_t kWsFSuper = kWsFStatus + (kLinesMaxRanges / kHeldTile + 1) * 8;   // suffix group sums
+constexpr uint64_t kWsFail = kWsFSuper + (kLinesMaxRanges / kHeldTile / kSfxGroup + 16) * 8;  // lines failures
 // failure words, fail_any, wdone: one 128-byte line each
 constexpr uint64_t kWsScratch = kWsFail + (kFailWords + 2) * kFailStride * 8;  // counts, bases
 
@@ -963,6 +970,13 @@ DEV DecodeWs ws_view(void *ws, uint32_t nranges)
 }
 
 DEV uint32_t wave_sum(uint32_t x)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+DEV uint64_t wave_sum64(uint64_t x)
 {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
@@ -1798,8 +1812,10 @@ DEV uint32_t tab_pack4(const uint8_t *tab, uint32_t x)
 // into the workspace, for k_decode_lines (every block reads them with one
 // scalar load instead of probing -- 175 K probes of the same 256 bytes cost
 // 7 % of a 1 GiB decode -- and of computing T and L's reciprocals: hundreds
-// of scalar instructions per wave) and k_decode_suffix_held.  n <= 2^31 (the
-// launcher's bound), so sextet indices and positions fit in 32 bits.
+// of scalar instructions per wave) and k_decode_suffix_held.  n <= 2^33 (the
+// launcher's bound, kLinesMaxChars): positions are 64-bit, slot indices
+// (< 2^29) 32-bit; the division constants m, k serve sextet indices below
+// 2^31, and k_decode_lines divides larger ones in 64 bits.
 //
 // Wave 0 probes the model from the first 256 bytes.  Every thread also
 // checks 64 bytes sampled further in (half of them over the stream's first
@@ -1832,12 +1848,12 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
 {
     __shared__ uint8_t tab[256];
     __shared__ LineModel s_m;
-    __shared__ uint32_t s_first;
+    __shared__ unsigned long long s_first;
     // the samples' loads are issued first: they overlap the table build and
     // the window probe
     const bool sample = n >= kProbeSampleMin && threadIdx.x < kProbeNS;
     uint32_t sw[16];
-    uint32_t q = 0;
+    uint64_t q = 0;
     if (sample) {
         // half the samples over the first 1/16 of the stream, half over all
         // of it, each half at quadratically growing distances
@@ -1846,7 +1862,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
         const uint64_t i = threadIdx.x % (kProbeNS / 2) + 1;
         const uint64_t raw = 256 + span * i * i / ((uint64_t) kProbeNS * kProbeNS / 4);
         const uint8_t *pa = (const uint8_t *) ((uintptr_t) (in + raw) & ~(uintptr_t) 15);
-        q = (uint32_t) (pa - in);
+        q = (uint64_t) (pa - in);
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) {
             const uint4 x = *(const uint4 *) (pa + 16 * k);
@@ -1857,13 +1873,12 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
         }
     }
     build_dec_table(tab, a);
-    if (threadIdx.x == 0) s_first = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) s_first = ~0ull;
     block_sync();
     if (threadIdx.x < 64) {
         uint32_t pj = 0xFFFFFFFFu;
         LineModel m = probe_lines(tab, in, n, &pj);
         if (threadIdx.x == 0) {
-            const uint32_t n32 = (uint32_t) n;
             if (m.L == 0 && pj != 0xFFFFFFFFu) {
                 // junk in the window that no line model explains (unstructured
                 // junk, a short first line): under the clean model the slot
@@ -1872,16 +1887,17 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
                 m.T = pj / 16;
                 m.skip = 1;
             } else if (m.L == 0) {
-                m.T = n32 / 16;
+                m.T = (uint32_t) (n / 16);
             } else {
                 m.P = m.L + m.s;
                 // T: the slots whose spans lie wholly inside the input -- those
                 // whose 16 characters are model positions below n, less the
                 // last one if a line ends right after it and its separator is
                 // cut off
-                const uint32_t F = n32 / m.P * m.L + (n32 % m.P < m.L ? n32 % m.P : m.L);
-                m.T = F / 16;
-                if (m.T && (16 * m.T) % m.L == 0 && (16 * m.T) / m.L * m.P > n32) m.T--;
+                const uint64_t F = n / m.P * m.L + (n % m.P < m.L ? n % m.P : m.L);
+                m.T = (uint32_t) (F / 16);
+                const uint64_t i = 16ull * m.T;
+                if (m.T && i % m.L == 0 && i / m.L * m.P > n) m.T--;
                 m.k = 32 - __builtin_clz(m.L - 1);  // ceil(log2 L)
                 m.m = (uint32_t) ((((uint64_t) 1 << (31 + m.k)) + m.L - 1) / m.L);
                 m.rcp = ((1u << 20) + m.L - 1) / m.L;
@@ -1894,26 +1910,27 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
     if (sample && !m.skip) {
         // the first sampled byte the model gets wrong: outside the alphabet
         // where a line character belongs, or inside it where a separator does
-        uint32_t r = m.L ? q % m.P : 0u, first = 0xFFFFFFFFu;
+        uint32_t r = m.L ? (uint32_t) (q % m.P) : 0u;
+        uint64_t first = ~0ull;
 #pragma unroll
         for (uint32_t j = 0; j < 64; j++) {
             const bool al = tab[(sw[j >> 2] >> (8 * (j & 3))) & 0xFFu] < 64u;
             const bool want = m.L == 0 || r < m.L;
-            if (al != want && first == 0xFFFFFFFFu) first = q + j;
+            if (al != want && first == ~0ull) first = q + j;
             if (m.L && ++r == m.P) r = 0;
         }
-        if (first != 0xFFFFFFFFu) atomicMin(&s_first, first);
+        if (first != ~0ull) atomicMin(&s_first, (unsigned long long) first);
     }
     block_sync();
     if (threadIdx.x != 0) return;
     LineModel mo = m;
-    const uint32_t pf = s_first;
-    if (!mo.skip && pf != 0xFFFFFFFFu) {
+    const uint64_t pf = s_first;
+    if (!mo.skip && pf != ~0ull) {
         // the slot holding model position F(pf): every slot from there on is
         // k_decode_suffix_held's
-        const uint32_t F = mo.L ? pf / mo.P * mo.L + (pf % mo.P < mo.L ? pf % mo.P : mo.L) : pf;
+        const uint64_t F = mo.L ? pf / mo.P * mo.L + (pf % mo.P < mo.L ? pf % mo.P : mo.L) : pf;
         if (F / 16 < mo.T) {
-            mo.T = F / 16;
+            mo.T = (uint32_t) (F / 16);
             mo.skip = 1;
         }
     }
@@ -1958,19 +1975,22 @@ DEV void lines_first_fail(uint32_t badm, uint32_t &fail_u, uint32_t &fail_lane)
 
 // k_decode_lines' hot path for line-structured text (a full wave, aligned
 // buffers, every window inside the input): lane slot t0 + 64 u + lane for u
-// < kLinesU; returns the lane's failed-slot bits.  A4: L % 4 == 0 (RFC
+// < kLinesU; returns the lane's failed-slot bits.  inw: the input at the
+// dword below the wave's first line start, pos0 (0..3) that line start's
+// offset from it (BIG; else inw = in and pos0 the line start's position);
+// the output of slot t0 is outw + obase (BIG: obase 0, outw 64-bit; else
+// outw = out), so lane offsets stay 32-bit at any stream length.  A4: L % 4 == 0 (RFC
 // 2045's 76, PEM's 64), where a line end falls on a dword of the slot.
 template <bool A4>
-DEV uint32_t lines_hot(const uint8_t *tab, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
-                       const LineModel &m, uint32_t line0, uint32_t col0, uint32_t t0,
-                       uint32_t lane)
+DEV uint32_t lines_hot(const uint8_t *tab, const uint8_t *__restrict__ inw, uint32_t pos0,
+                       uint8_t *__restrict__ outw, uint32_t obase, const LineModel &m,
+                       uint32_t col0, uint32_t lane)
 {
     const uint32_t L = m.L, s = m.s, P = m.P;
     uint4 win[kLinesU];
     uint2 wx[kLinesU];
     uint32_t oo[kLinesU], cc[kLinesU];
     bool hs[kLinesU];
-    const uint32_t pos0 = line0 * P;  // wave-uniform
 #pragma unroll
     for (uint32_t u = 0; u < kLinesU; u++) {
         // rel < L + 4,096 and rcp < 2^16: 24-bit products (full rate;
@@ -1982,8 +2002,10 @@ DEV uint32_t lines_hot(const uint8_t *tab, const uint8_t *__restrict__ in, uint8
         hs[u] = L - col <= 16;  // a line ends in (or right after) the slot
         cc[u] = hs[u] ? L - col : 16u;
         oo[u] = pos & 3u;
-        const uint8_t *ab = in + (pos & ~3u);
-        win[u] = ld16<false>(ab);  // (non-temporal: neutral, r02_ab_lines_ntl.jsonl)
+        const uint8_t *ab = inw + (pos & ~3u);
+        // (non-temporal: neutral, r02_ab_lines_ntl.jsonl; with the 8-byte
+        // load too, 443 -> 476 us, r06_e_ab.jsonl)
+        win[u] = ld16<false>(ab);
         const u32x2a4 v = *(const u32x2a4 *) (ab + 16);
         wx[u] = make_uint2(v.x, v.y);
     }
@@ -2002,11 +2024,16 @@ DEV uint32_t lines_hot(const uint8_t *tab, const uint8_t *__restrict__ in, uint8
         const uint32_t nd = hs[u] ? need : 0u;
         if ((sep_nonalpha(tab, sep) & nd) != nd) bad |= 0x100u;
         badm |= bad ? 1u << u : 0u;
-        emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
+        emit_full_off<true>(G, outw, obase + 12 * (u * 64 + lane));
     }
     return badm;
 }
 
+// BIG: n > 2^31 (up to kLinesMaxChars): sextet indices and positions of a
+// wave's first slot are 64-bit, divided by L in 64 bits, and the wave's loads
+// and stores go through 64-bit wave bases; below, the 32-bit forms of rounds
+// 2-5 (the 64-bit bases cost the clean decode 1.5 %, r06_h_ab.jsonl).
+template <bool BIG>
 __global__ __launch_bounds__(kLinesTH) __attribute__((amdgpu_waves_per_eu(6)))
 void k_decode_lines(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
@@ -2026,7 +2053,7 @@ void k_decode_lines(
     // model; clean input keeps the fast path and anything else fails a slot
     // and goes to k_decode_suffix_held (which then asks for a probe).
     const bool mok = mn == n;
-    const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : (uint32_t) n / 16u;
+    const uint32_t T = mok ? (uint32_t) (mw1 >> 32) : (uint32_t) (n / 16);
     // a block wholly past slot T (the probe cut the model's slots at junk)
     // leaves before the barrier: on junk-laden input nearly every block of
     // this launch does.  (Tested before the table build, the model's load
@@ -2055,14 +2082,21 @@ void k_decode_lines(
     const bool oal = (((uintptr_t) out) & 3) == 0;
     const bool ial = (((uintptr_t) in) & 3) == 0;
     uint32_t fail_u = kLinesU, fail_lane = 0;  // the wave's first failing slot
-    // line coordinates of the wave's first sextet
-    const uint32_t i0 = 16 * t0;
-    const uint32_t line0 = L ? line_div(m, i0) : 0;
-    const uint32_t col0 = i0 - line0 * L;
+    // line coordinates of the wave's first sextet (scalar; BIG: a 64-bit
+    // division, once per wave)
+    const uint64_t i0 = 16ull * t0;
+    const uint32_t line0 = !L ? 0u : !BIG ? line_div(m, (uint32_t) i0) : (uint32_t) (i0 / L);
+    const uint32_t col0 = (uint32_t) (i0 - (uint64_t) line0 * L);
     // the wave's windows all end inside the input (24 bytes from a dword at
     // or below each span's start)
-    const uint32_t ie = i0 + 16 * ns, le = L ? line_div(m, ie) : 0;
-    const bool safe = (uint64_t) (L ? le * P + (ie - le * L) : ie) + 24 <= n;
+    const uint64_t ie = i0 + 16 * ns;
+    const uint32_t le = !L ? 0u : !BIG ? line_div(m, (uint32_t) ie) : (uint32_t) (ie / L);
+    const bool safe = (L ? (uint64_t) le * P + (ie - (uint64_t) le * L) : ie) + 24 <= n;
+    // the wave's first line start and its output: BIG, 64-bit bases and
+    // 32-bit offsets from them; else 32-bit offsets from in and out
+    const uint64_t pos0 = (uint64_t) line0 * P;
+    uint8_t *const outw = BIG ? out + 12ull * t0 : out;
+    const uint32_t obase = BIG ? 0u : 12 * t0;
     if (ns && L == 0 && full && oal && ial) {
         // The hot path (clean input, a full wave, aligned buffers): lane t's
         // 16 characters are one non-temporal dwordx4 at 16t, its 12 bytes one
@@ -2071,28 +2105,32 @@ void k_decode_lines(
         // here is exec-masked (a masked form also lost the nt bit and waited
         // on every load at once: 7 % slower).
         uint4 c[kLinesU];
+        const uint8_t *const inw = BIG ? in + 16ull * t0 : in;
+        const uint32_t ibase = BIG ? 0u : 16 * t0;
 #pragma unroll
-        for (uint32_t u = 0; u < kLinesU; u++) c[u] = ld16<true>(in + 16 * (t0 + u * 64 + lane));
+        for (uint32_t u = 0; u < kLinesU; u++) c[u] = ld16<true>(inw + (ibase + 16 * (u * 64 + lane)));
         uint32_t badm = 0;  // bit u: this lane's slot u failed
 #pragma unroll
         for (uint32_t u = 0; u < kLinesU; u++) {
             uint32_t G[4], bad;
             map_fast(tab, c[u], 16, G, bad);
             badm |= bad ? 1u << u : 0u;
-            emit_full_off<true>(G, out, 12 * (t0 + u * 64 + lane));  // < 2^31: n <= 2^31
+            emit_full_off<true>(G, outw, obase + 12 * (u * 64 + lane));
         }
         lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns && L != 0 && full && oal && ial && safe) {
         // The hot path of line-structured text: 32-bit offsets from the
-        // input's base, unguarded window loads, non-temporal stores.  Two
+        // wave's bases, unguarded window loads, non-temporal stores.  Two
         // instances, one per line-length class, behind a wave-uniform branch:
         // written as `a4 ? slot_chars4(..) : slot_chars(..)` the compiler
         // computed both forms for every slot and selected (692 VALU for a
         // wave's 4 slots in the listing, ~250 of them the general form that
         // CRLF-76 never uses).
+        const uint8_t *const inw = BIG ? in + (pos0 & ~3ull) : in;
+        const uint32_t p0 = (uint32_t) (BIG ? pos0 & 3u : pos0);
         const uint32_t badm = (L & 3) == 0
-            ? lines_hot<true>(tab, in, out, m, line0, col0, t0, lane)
-            : lines_hot<false>(tab, in, out, m, line0, col0, t0, lane);
+            ? lines_hot<true>(tab, inw, p0, outw, obase, m, col0, lane)
+            : lines_hot<false>(tab, inw, p0, outw, obase, m, col0, lane);
         lines_first_fail(badm, fail_u, fail_lane);
     } else if (ns) {
         // Everything else (a partial wave, the input's end, misaligned
@@ -2108,7 +2146,7 @@ void k_decode_lines(
             const uint32_t rel = col0 + 16 * (u * 64 + lane);
             const uint32_t dl = L ? (rel * m.rcp) >> 20 : 0;
             const uint32_t col = rel - dl * L;
-            const uint32_t pos = L ? (line0 + dl) * P + col : i0 + 16 * (u * 64 + lane);
+            const uint64_t pos = L ? (uint64_t) (line0 + dl) * P + col : i0 + 16 * (u * 64 + lane);
             hs[u] = L && L - col <= 16;
             cc[u] = hs[u] ? L - col : 16u;
             const uint8_t *ap = in + pos;
@@ -2581,7 +2619,10 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
     }
 }
 
-template <bool WHOLE>
+// BIG: n > 2^31 (up to kLinesMaxChars): a tile's prefix -- alphabet
+// characters of the suffix before it -- in 64 bits (in 32 below: the 64-bit
+// sums cost 7 % at junk density 0.05, r06_h_ab.jsonl).
+template <bool WHOLE, bool BIG>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kHeldWaves)))
 void k_decode_suffix_held(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
@@ -2601,8 +2642,9 @@ void k_decode_suffix_held(
     __shared__ P2dSmem sm;
     __shared__ uint4 s_rng[kWavesPerBlock][2][128];
     __shared__ uint32_t s_tile[2];
+    using Cnt = typename std::conditional<BIG, uint64_t, uint32_t>::type;
     __shared__ uint32_t s_cnt[2][TILE];
-    __shared__ uint32_t s_excl;
+    __shared__ Cnt s_excl;
     build_dec_table(sm.tab, a);
     build_compact_sel(sm.sel);
     const uint32_t lane = lane_id();
@@ -2623,8 +2665,11 @@ void k_decode_suffix_held(
     // one round trip.  (Loading every earlier group, 64 per lane-pass, took
     // one round trip per pass, each waited for before the next: 6 on average
     // on 1 GiB.)
-    uint32_t kdone = 0, sdone = 0;
-    auto prefix = [&](uint32_t t) -> uint32_t {
+    // (64-bit sums: a suffix of a stream past 2^32 characters, up to
+    // kLinesMaxChars)
+    uint32_t kdone = 0;
+    Cnt sdone = 0;
+    auto prefix = [&](uint32_t t) -> Cnt {
         const uint32_t k = t / kSfxGroup, own = t - k * kSfxGroup;
         for (;;) {
             const uint64_t v = lane < own ? st_load(&w.fstatus[k * kSfxGroup + lane]) : kStAgg;
@@ -2637,7 +2682,7 @@ void k_decode_suffix_held(
                 sg += j < k ? (uint32_t) g : 0u;
             }
             if (__all(ok)) {
-                sdone += wave_sum(sg);
+                sdone += BIG ? (Cnt) wave_sum64(sg) : (Cnt) wave_sum(sg);
                 kdone = k;
                 return sdone + wave_sum((uint32_t) v);
             }
@@ -2700,11 +2745,11 @@ void k_decode_suffix_held(
     // suffix's alphabet characters before it, T its own.
     // the window holds dwords dl + [0, 384) (dl <= 3) and the 8 zeroed after
     static_assert(kP2dBlocks * 4 >= 3 + 384 + 8, "held window fits the wave's LDS window");
-    auto store_one = [&](uint32_t r, uint32_t Bp, uint32_t T, const uint32_t Hj[6], uint32_t la) {
+    auto store_one = [&](uint32_t r, Cnt Bp, uint32_t T, const uint32_t Hj[6], uint32_t la) {
         const uint64_t rb = (uint64_t) r * R;
         const uint64_t re = rb + R < n ? rb + R : n;
         const bool last = r + 1 == nranges;
-        const uint32_t k = (4u - (Bp & 3u)) & 3u;  // sextets the range before took
+        const uint32_t k = (4u - ((uint32_t) Bp & 3u)) & 3u;  // sextets the range before took
         uint8_t *dst = base_out + (uint64_t) (Bp + k) / 4 * 3;
         const uint32_t dl = window_delta(6 * k, dst);  // the held dwords go to dl..
 #pragma unroll
@@ -2713,7 +2758,7 @@ void k_decode_suffix_held(
         wave_lds_order();
         uint32_t Tc = T;
         bool at_end = last;
-        if (!last && ((Bp + T) & 3u)) {
+        if (!last && (((uint32_t) Bp + T) & 3u)) {
             // complete the range's last group from the characters after it
             bool ok = re + lane < n;
             for (uint64_t q = re;;) {
@@ -2722,7 +2767,7 @@ void k_decode_suffix_held(
                 const uint64_t m = __ballot(v);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                const uint32_t need = 4u - ((Bp + Tc) & 3u);
+                const uint32_t need = 4u - (((uint32_t) Bp + Tc) & 3u);
                 if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 18);
                 const uint32_t got = (uint32_t) __popcll(m);
                 if (got >= need) {
@@ -2763,7 +2808,8 @@ void k_decode_suffix_held(
     }
     block_sync();  // the tables
     bool haveA = false, owner = false;
-    uint32_t tA = 0, bA = 1, bB = 0, Vs = 0;
+    uint32_t tA = 0, bA = 1, bB = 0;
+    Cnt Vs = 0;
     if (threadIdx.x == 0) s_tile[0] = atomicAdd(w.fticket, 1u);
     for (;;) {
         block_sync();  // the ticket; s_cnt[bB] (two tiles back) consumed
@@ -2788,12 +2834,12 @@ void k_decode_suffix_held(
             // (every wave taking the prefix itself, no barrier: 841 against
             // 780 us, profiles/r05_ab_sfx_held_wavepfx.jsonl)
             if (wv == 0) {
-                const uint32_t ex = tA ? prefix(tA) : 0u;
+                const Cnt ex = tA ? prefix(tA) : (Cnt) 0;
                 if (lane == 0) s_excl = ex;
             }
             block_sync();
-            const uint32_t exw = s_excl;
-            uint32_t Bp = exw;
+            const Cnt exw = s_excl;
+            Cnt Bp = exw;
             for (uint32_t i = 0; i < wv * HP; i++) Bp += s_cnt[bA][i];
             const uint32_t rwA = r0 + tA * TILE + wv * HP;
 #pragma unroll
@@ -4055,7 +4101,9 @@ RangePlan plan_ranges(uint64_t n)
     if (g_test_range_chunks) chunks = g_test_range_chunks;
 #endif
     uint64_t R = chunks * kChunk;
-    if ((n + R - 1) / R > kMaxRanges) {
+    // up to kLinesMaxChars: 2,048-character ranges for the lines path, past
+    // kMaxRanges too (its kernels use no per-range scratch)
+    if ((n + R - 1) / R > kMaxRanges && !(chunks == kRangeChunks && n <= kLinesMaxChars)) {
         R = (n + kMaxRanges - 1) / kMaxRanges;
         R = (R + kChunk - 1) / kChunk * kChunk;
     }
@@ -4581,10 +4629,17 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         // of whatever suffix it could not take -- nothing, on clean and
         // MIME-formatted text: each block of that launch reads one word and
         // returns.  EXPECT_JUNK skips the first.
-        static const int occ_sfx = occupancy_of(k_decode_suffix_held<false>);
+        // BIG instances past 2^31 characters (64-bit positions and prefixes)
+        const bool big = nchars > (1ull << 31);
+        static const int occ_small = occupancy_of(k_decode_suffix_held<false, false>);
+        static const int occ_big = occupancy_of(k_decode_suffix_held<false, true>);
+        const int occ_sfx = big ? occ_big : occ_small;
+        auto *const k_whole = big ? k_decode_suffix_held<true, true> : k_decode_suffix_held<true, false>;
+        auto *const k_sfx = big ? k_decode_suffix_held<false, true> : k_decode_suffix_held<false, false>;
+        auto *const k_lines = big ? k_decode_lines<true> : k_decode_lines<false>;
         const uint32_t sfx_grid = (uint32_t) d->cus * occ_sfx;
         if (flags & B64X_DEC_EXPECT_JUNK) {
-            hipLaunchKernelGGL(k_decode_suffix_held<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
@@ -4623,17 +4678,17 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         }
         if (junky) {
             path_taken(kPathHinted);
-            hipLaunchKernelGGL(k_decode_suffix_held<true>, dim3(sfx_grid), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                                hold, d_res, h_res, seq, nullptr);
             return launch_status();
         }
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
-        hipLaunchKernelGGL(k_decode_lines, dim3((uint32_t) ((waves + kLinesWaves - 1) / kLinesWaves)),
+        hipLaunchKernelGGL(k_lines, dim3((uint32_t) ((waves + kLinesWaves - 1) / kLinesWaves)),
                            dim3(kLinesTH), 0, s, (const uint8_t *) d_in, nchars, (uint8_t *) d_out,
                            p.nranges, a, ws, hold, d_res, seq);
         if ((err = launch_status())) return err;
-        hipLaunchKernelGGL(k_decode_suffix_held<false>, dim3(sfx_grid), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(k_sfx, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
                            hold, d_res, h_res, seq, reprobe);
         return launch_status();

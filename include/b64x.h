@@ -159,7 +159,7 @@ int b64x_encode_dev(const void *d_in, uint64_t n, void *d_out,
  * may reuse it and skip the probe; one workspace per stream), or NULL to use
  * a library-owned one
  * per (device, stream).  The library keeps at most 8 such workspaces
- * (about 12.7 MiB of HBM each), allocated on first need and never freed: a
+ * (about 14 MiB of HBM each), allocated on first need and never freed: a
  * call on a stream without one takes an idle one (its stream made to wait
  * on the device for the workspace's last use), or -EBUSY if all eight are
  * in use by calls being enqueued right then.  A stream being captured into

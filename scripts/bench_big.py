@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Past 2^31 characters (DESIGN.md §5 "Larger inputs"): the clean decode of
-one buffer of 3 x 2^30 characters (2.25 GiB of payload) takes pass 1, the
-scan and pass 2 (the range count is capped, so ranges grow past 2,048
-characters) instead of the probe / lines / suffix pipeline.  Encode and
-decode timed with HIP events (median of 10 after 2 warm-ups), bit-checked,
-one JSON line; the 1 GiB decode beside it for comparison.
+one buffer of 3 x 2^30 characters (2.25 GiB of payload) and of 4.5 GiB of
+payload (6 x 2^30 characters, past 2^32).  Since round 6 both take the probe
+/ lines / suffix pipeline (up to 2^33 characters); rounds 1-5 sent anything
+past 2^31 to pass 1, the scan and pass 2.  Encode and decode timed with HIP
+events (median of 10 after 2 warm-ups), bit-checked, one JSON line; the
+1 GiB decode beside it for comparison.
 
     python scripts/bench_big.py
 """
@@ -36,7 +37,7 @@ def timed(fn, steps=10):
 
 def main():
     out = {}
-    for name, n in (("1GiB", 1 << 30), ("2.25GiB", 9 << 28)):
+    for name, n in (("1GiB", 1 << 30), ("2.25GiB", 9 << 28), ("4.5GiB", 9 << 29)):
         x = torch.empty(n, dtype=torch.uint8, device="cuda")
         b64.fill_splitmix64(x, 0x5EED)
         enc = b64.encode(x)

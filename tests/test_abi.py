@@ -92,8 +92,10 @@ def _isa():
 SHIPPED_KERNELS = {
     "k_encode", "k_encode_flat", "k_encode_tight2<2>", "k_encode_strided<2, true>",
     "k_encode_ragged",
-    "k_decode_probe", "k_decode_lines", "k_decode_suffix_held<false>",
-    "k_decode_suffix_held<true>", "k_decode_pass1<2, true>", "k_decode_scan2",
+    "k_decode_probe", "k_decode_lines<false>", "k_decode_lines<true>",
+    "k_decode_suffix_held<false, false>", "k_decode_suffix_held<true, false>",
+    "k_decode_suffix_held<false, true>", "k_decode_suffix_held<true, true>",
+    "k_decode_pass1<2, true>", "k_decode_scan2",
     "k_decode_pass2d",
     "k_decode_slots<2>", "k_rows_prep", "k_decode_rows_lines<4, false>",
     "k_decode_rows_lines<4, true>", "k_rows_finish", "k_decode_batch_fast<false>",
