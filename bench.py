@@ -68,7 +68,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s base64 encode+decode, device-resident, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ROUND = "r05"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
+ROUND = "r06"  # the committed PMC summary (profiles/pmc_<ROUND>.json) used for `traffic`
 
 
 def parse():

@@ -37,7 +37,7 @@ for k, v in vals.items():
                   "raw_FETCH_SIZE_KiB": v["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": v["WRITE_SIZE"]}
 # short aliases for the config-2 kernels bench.py names
 for alias in ("k_encode_flat", "k_decode_pass1", "k_decode_lines", "k_decode_probe",
-              "k_decode_suffix", "k_encode_tight2", "k_decode_rows_lines", "k_rows_prep"):
+              "k_decode_suffix_held", "k_encode_tight2", "k_decode_rows_lines", "k_rows_prep"):
     cands = sorted((k for k in kernels if k.startswith(alias + "@")),
                    key=lambda k: -kernels[k]["hbm_bytes_per_launch"])
     if cands:
