@@ -549,6 +549,54 @@ def test_beyond_32bit_sizes():
     assert torch.equal(dd.out[:n], x)
 
 
+def _gpu_lines(chars: torch.Tensor, L: int, sep: bytes) -> torch.Tensor:
+    """chars in lines of L characters, each followed by `sep` (the last
+    line short, with its separator), built on the GPU (no boolean masks:
+    torch's mask indexing fails past 2^31 elements)."""
+    n = chars.numel()
+    full = n // L
+    sp = torch.tensor(list(sep), dtype=torch.uint8, device=chars.device)
+    body = torch.cat([chars[:full * L].view(full, L), sp.expand(full, len(sep))], dim=1).reshape(-1)
+    if n % L:
+        body = torch.cat([body, chars[full * L:], sp])
+    return body.contiguous()
+
+
+@pytest.mark.parametrize("L,sep", [(76, b"\r\n"), (70, b"\n")])
+def test_beyond_31bit_lines(L, sep):
+    """MIME-formatted text past 2^31 characters (round 6: the lines path's
+    64-bit wave bases, k_decode_lines<true>, both slot forms: L % 4 == 0 and
+    not): 1.6 GiB of payload in lines, decoded whole, then with a junk byte
+    near the end (the suffix from there, 64-bit prefix); windows across 2^31
+    and 2^32 characters against the oracle's decode of the same text."""
+    n = 1717986918  # 1.6 GiB: 2.29 G characters, 2.35-2.36 G bytes with separators
+    x = torch.empty(n, dtype=torch.uint8, device=DEV)
+    b64.fill_splitmix64(x, 0x11E5 + L)
+    enc = b64.encode(x)
+    text = _gpu_lines(enc, L, sep)
+    del enc
+    assert text.numel() > (1 << 31)
+    dd = b64.decode(text)
+    assert dd.info().out_len == n
+    assert torch.equal(dd.out[:n], x)
+    del dd
+    # the oracle on 40-line windows that start on (even) line boundaries,
+    # across 2^31 and 2^32 bytes of text
+    W = L + len(sep)
+    for at in ((1 << 31) - 5000, (1 << 31) + 77, text.numel() - 3 * W * 40):
+        a = at // (2 * W) * (2 * W)
+        want = orc.decode(text[a:a + 40 * W].cpu().numpy().tobytes())
+        o = a // W * L // 4 * 3
+        assert x[o:o + len(want)].cpu().numpy().tobytes() == want, at
+    # one junk byte inserted late in the stream: the lines pass stops there
+    # and the suffix decodes the rest
+    k = text.numel() - 1000
+    text = torch.cat([text[:k], torch.tensor([ord("*")], dtype=torch.uint8, device=DEV), text[k:]])
+    dd = b64.decode(text)
+    assert dd.info().out_len == n
+    assert torch.equal(dd.out[:n], x)
+
+
 @pytest.mark.slow
 def test_beyond_32bit_strided_batch():
     """A batch whose total input and output pass 4 GiB: 4,194,307 rows of
