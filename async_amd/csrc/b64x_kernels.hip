@@ -2584,22 +2584,34 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
     const uint32_t a = (uint32_t) ((uintptr_t) dst & 15);
     // block m of the aligned grid covers bytes [16 m - a, 16 m - a + 16)
     const uint32_t m0 = a ? 1u : 0u, mend = (nb + a) >> 4;
-    const uint32_t sh = (s + 128 * m0 - 8 * a) & 31;  // the same for every block
+    const uint32_t b0 = s + 128 * m0 - 8 * a;
+    const uint32_t i0 = b0 >> 5, sh = b0 & 31;  // block m0's first window dword (a multiple of 4)
+    const uint32_t nblk = mend > m0 ? mend - m0 : 0u;
+    uint8_t *const base = dst - a + 16 * m0;     // 16-byte aligned, wave-uniform
     const uint4 *win4 = (const uint4 *) win;
-    for (uint32_t m0l = m0; m0l < mend; m0l += 64) {
-        const uint32_t m = m0l + lane;
-        const uint32_t i = (s + 128 * m - 8 * a) >> 5;  // a multiple of 4
-        uint4 g = make_uint4(0, 0, 0, 0);
-        if (m < mend) g = win4[i >> 2];
-        uint32_t w4 = (uint32_t) __shfl_down((int) g.x, 1, 64);
-        if (m < mend && (lane == 63 || m + 1 >= mend)) w4 = win[i + 4];
-        auto f = [sh](uint32_t hi, uint32_t lo) {
-            return (uint32_t) ((((uint64_t) hi << 32) | lo) >> (32 - sh));
-        };
-        if (m < mend)
-            __builtin_nontemporal_store(u32x4a16{bswap32(f(g.x, g.y)), bswap32(f(g.y, g.z)),
-                                                 bswap32(f(g.z, g.w)), bswap32(f(g.w, w4))},
-                                        (u32x4a16 *) (dst - a + 16 * (uint64_t) m));
+    // Every lane reads its group and the next dword (no shuffle, no masked
+    // read: an index clamped inside the window for lanes past the end), the
+    // funnel shift is one v_alignbit per dword (sh = 0, wave-uniform: none),
+    // and only the store is masked (round 5: a masked read, a shuffle and a
+    // masked read of the next dword, each waited for, and 64-bit shifts).
+    constexpr uint32_t kLast = kP2dBlocks * 4 - 8;  // the last group read in full
+    for (uint32_t k0 = 0; k0 < nblk; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint32_t ik = i0 + 4 * k;
+        const uint32_t i = ik < kLast ? ik : kLast;
+        const uint4 g = win4[i >> 2];
+        const uint32_t w4 = win[i + 4];
+        uint32_t o0 = g.x, o1 = g.y, o2 = g.z, o3 = g.w;
+        if (sh) {
+            const uint32_t r = 32u - sh;
+            o0 = __builtin_amdgcn_alignbit(g.x, g.y, r);
+            o1 = __builtin_amdgcn_alignbit(g.y, g.z, r);
+            o2 = __builtin_amdgcn_alignbit(g.z, g.w, r);
+            o3 = __builtin_amdgcn_alignbit(g.w, w4, r);
+        }
+        if (k < nblk)
+            __builtin_nontemporal_store(u32x4a16{bswap32(o0), bswap32(o1), bswap32(o2), bswap32(o3)},
+                                        (u32x4a16 *) (base + 16 * k));
     }
     const uint32_t hend = a ? (16 - a < nb ? 16 - a : nb) : 0u;  // head bytes [0, hend)
     const uint32_t tb = mend > m0 ? 16 * mend - a : hend;          // tail bytes [tb, nb)
