@@ -2711,8 +2711,9 @@ void k_decode_suffix_held(
     };
 
     // Decode range j of tile t (this wave's) into the window; hold its
-    // dwords [6 lane, 6 lane + 6) in Hn and the byte after its end at lane
-    // offset in lan (the completion's first look); count into s_cnt[b].
+    // dwords [6 lane, 6 lane + 6) in Hn and, in lan, the table value of the
+    // byte at lane offset after its end (the completion's first look, looked
+    // up here: the load has landed by the range's wait); count into s_cnt[b].
     auto decode_one = [&](uint32_t rw, uint32_t j, uint32_t b, uint32_t Hn[6], uint32_t &lan) {
         const uint32_t r = rw + j;
         uint32_t T = 0;
@@ -2749,6 +2750,7 @@ void k_decode_suffix_held(
             wave_lds_order();
 #pragma unroll
             for (int i = 0; i < 6; i++) Hn[i] = bits[lane + 64 * i];  // consecutive lanes
+            lan = re + lane < n ? (uint32_t) sm.tab[lan] : 0xFFu;
             wave_lds_order();
         }
         if (lane == 0) s_cnt[b][wv * HP + j] = T;
@@ -2774,7 +2776,7 @@ void k_decode_suffix_held(
             // complete the range's last group from the characters after it
             bool ok = re + lane < n;
             for (uint64_t q = re;;) {
-                const uint32_t t = ok ? sm.tab[la] : 0xFFu;
+                const uint32_t t = ok ? la : 0xFFu;  // a table value
                 const bool v = t < 64u;
                 const uint64_t m = __ballot(v);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -2793,7 +2795,7 @@ void k_decode_suffix_held(
                     break;
                 }
                 ok = q + lane < n;
-                la = ok ? in[q + lane] : 0u;
+                la = ok ? sm.tab[in[q + lane]] : 0xFFu;
             }
             wave_lds_order();
         }
