@@ -2589,12 +2589,21 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
     const uint32_t nblk = mend > m0 ? mend - m0 : 0u;
     uint8_t *const base = dst - a + 16 * m0;     // 16-byte aligned, wave-uniform
     const uint4 *win4 = (const uint4 *) win;
+    constexpr uint32_t kLast = kP2dBlocks * 4 - 8;  // the last group read in full
+    // The partial blocks' bytes (head [0, hend), tail [tb, nb); at most 15
+    // each, one per lane of lanes 0-31): their two window dwords are read
+    // first, so that one wait covers them and the first groups.
+    const uint32_t hend = a ? (16 - a < nb ? 16 - a : nb) : 0u;
+    const uint32_t tb = mend > m0 ? 16 * mend - a : hend;
+    const uint32_t bi = lane < 16 ? lane : (tb > hend ? tb : hend) + (lane - 16);
+    const bool act = lane < 16 ? bi < hend : lane < 32 && bi < nb;
+    const uint32_t X = s + 8 * bi, xi = (X >> 5) < kLast ? X >> 5 : kLast;
+    const uint32_t x0 = win[xi], x1 = win[xi + 1];
     // Every lane reads its group and the next dword (no shuffle, no masked
     // read: an index clamped inside the window for lanes past the end), the
     // funnel shift is one v_alignbit per dword (sh = 0, wave-uniform: none),
     // and only the store is masked (round 5: a masked read, a shuffle and a
     // masked read of the next dword, each waited for, and 64-bit shifts).
-    constexpr uint32_t kLast = kP2dBlocks * 4 - 8;  // the last group read in full
     for (uint32_t k0 = 0; k0 < nblk; k0 += 64) {
         const uint32_t k = k0 + lane;
         const uint32_t ik = i0 + 4 * k;
@@ -2613,22 +2622,7 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
             __builtin_nontemporal_store(u32x4a16{bswap32(o0), bswap32(o1), bswap32(o2), bswap32(o3)},
                                         (u32x4a16 *) (base + 16 * k));
     }
-    const uint32_t hend = a ? (16 - a < nb ? 16 - a : nb) : 0u;  // head bytes [0, hend)
-    const uint32_t tb = mend > m0 ? 16 * mend - a : hend;          // tail bytes [tb, nb)
-    uint32_t bi = 0;
-    bool act = false;
-    if (lane < 16) {
-        bi = lane;
-        act = bi < hend;
-    } else if (lane < 32) {
-        bi = (tb > hend ? tb : hend) + (lane - 16);
-        act = bi < nb;
-    }
-    if (act) {
-        const uint32_t X = s + 8 * bi;
-        const uint64_t W = ((uint64_t) win[X >> 5] << 32) | win[(X >> 5) + 1];
-        dst[bi] = (uint8_t) (W >> (56 - (X & 31)));
-    }
+    if (act) dst[bi] = (uint8_t) ((((uint64_t) x0 << 32) | x1) >> (56 - (X & 31)));
 }
 
 // BIG: n > 2^31 (up to kLinesMaxChars): a tile's prefix -- alphabet
