@@ -2708,10 +2708,15 @@ void k_decode_suffix_held(
     // dwords [6 lane, 6 lane + 6) in Hn and, in lan, the table value of the
     // byte at lane offset after its end (the completion's first look, looked
     // up here: the load has landed by the range's wait); count into s_cnt[b].
-    auto decode_one = [&](uint32_t rw, uint32_t j, uint32_t b, uint32_t Hn[6], uint32_t &lan) {
+    auto la_load = [&](uint32_t r) -> uint32_t {
+        if (r >= nranges) return 0u;
+        const uint64_t re = (uint64_t) r * R + R < n ? (uint64_t) r * R + R : n;
+        return re + lane < n ? (uint32_t) in[re + lane] : 0u;
+    };
+    auto decode_one = [&](uint32_t rw, uint32_t j, uint32_t b, uint32_t Hn[6], uint32_t &lan,
+                          uint32_t &lan_next) {
         const uint32_t r = rw + j;
         uint32_t T = 0;
-        lan = 0;
 #pragma unroll
         for (int i = 0; i < 6; i++) Hn[i] = 0;
         if (r < nranges) {
@@ -2721,7 +2726,6 @@ void k_decode_suffix_held(
             const bool next_dma = j + 1 < HP && whole(r + 1);
             uint4 *buf = s_rng[wv][j & 1];
             uint32_t nin[2] = {16u, 16u};
-            lan = re + lane < n ? (uint32_t) in[re + lane] : 0u;
             if (whole(r)) {
                 vm_wait_all();
             } else {
@@ -2736,6 +2740,7 @@ void k_decode_suffix_held(
             c[0] = buf[lane];
             c[1] = buf[64 + lane];
             if (next_dma) fetch(r + 1, (j + 1) & 1);
+            if (j + 1 < HP) lan_next = la_load(r + 1);
             wave_lds_order();
             bq[lane] = make_uint4(0, 0, 0, 0);
             if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
@@ -2746,6 +2751,8 @@ void k_decode_suffix_held(
             for (int i = 0; i < 6; i++) Hn[i] = bits[lane + 64 * i];  // consecutive lanes
             lan = re + lane < n ? (uint32_t) sm.tab[lan] : 0xFFu;
             wave_lds_order();
+        } else {
+            lan = 0;
         }
         if (lane == 0) s_cnt[b][wv * HP + j] = T;
     };
@@ -2829,11 +2836,13 @@ void k_decode_suffix_held(
         if (haveB) {
             const uint32_t rwB = r0 + tB * TILE + wv * HP;
             if (whole(rwB)) fetch(rwB, 0);
+            uint32_t lan = la_load(rwB);
 #pragma unroll
             for (uint32_t j = 0; j < HP; j++) {
-                uint32_t lan;
-                decode_one(rwB, j, bB, HB[j], lan);
+                uint32_t lan_next = 0;
+                decode_one(rwB, j, bB, HB[j], lan, lan_next);
                 LB |= lan << (8 * j);
+                lan = lan_next;
             }
         }
         block_sync();  // s_cnt[bB] complete
