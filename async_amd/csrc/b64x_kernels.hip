@@ -1569,20 +1569,23 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
     // invalid-byte pattern, via v_dot4 of the bit-7s) and 6 x the count of
     // non-alphabet bytes; the scan runs over the lanes' BIT counts (both
     // chunks packed in one DPP scan), so positions need no multiply
-    uint32_t P[2][4], sel[2][4], six[2][4], cnt = 0;
+    // acc[h][g]: -6 x the non-alphabet bytes of chunk h before group g, a
+    // running signed v_dot4 (group g's field sits 24 g + acc[h][g] bits into
+    // the lane's share of the chunk)
+    uint32_t P[2][4], sel[2][4], cnt = 0;
+    int acc[2][5];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         lane_values(sm.tab, c[h], nin[h], P[h]);
-        uint32_t nb6 = 0;
+        acc[h][0] = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
             const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
             sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-            six[h][g] = __builtin_amdgcn_udot4(iv, 0x06060606u, 0u, false);
-            nb6 += six[h][g];
+            acc[h][g + 1] = __builtin_amdgcn_sdot4((int) iv, (int) 0xFAFAFAFAu, acc[h][g], false);
         }
-        cnt |= (96u - nb6) << (16 * h);  // the lane's output bits in chunk h (<= 96)
+        cnt |= (uint32_t) (96 + acc[h][4]) << (16 * h);  // the lane's output bits in chunk h (<= 96)
     }
     const uint32_t incl = wave_incl_scan_dpp(cnt);  // halves <= 6,144
     const uint32_t ex = incl - cnt;
@@ -1590,12 +1593,12 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t before = h ? tot & 0xFFFFu : 0u;
-        uint32_t p = (uint32_t) bit0 + before + ((ex >> (16 * h)) & 0xFFFFu);
+        const uint32_t p = (uint32_t) bit0 + before + ((ex >> (16 * h)) & 0xFFFFu);
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
-            or_field<BE>(bits, p, group_dot(D));  // absent sextets are zero bytes
-            p += 24u - six[h][g];
+            // absent sextets are zero bytes
+            or_field<BE>(bits, p + 24u * g + (uint32_t) acc[h][g], group_dot(D));
         }
     }
     return ((tot & 0xFFFFu) + (tot >> 16)) / 6u;  // alphabet characters (scalar)
