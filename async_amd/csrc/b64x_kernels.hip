@@ -2722,6 +2722,7 @@ void k_decode_suffix_held(
         uint32_t T = 0;
 #pragma unroll
         for (int i = 0; i < 6; i++) Hn[i] = 0;
+        vm_wait_all();
         if (r < nranges) {
             const uint64_t rb = (uint64_t) r * R;
             const uint64_t re = rb + R < n ? rb + R : n;
@@ -2729,9 +2730,7 @@ void k_decode_suffix_held(
             const bool next_dma = j + 1 < HP && whole(r + 1);
             uint4 *buf = s_rng[wv][j & 1];
             uint32_t nin[2] = {16u, 16u};
-            if (whole(r)) {
-                vm_wait_all();
-            } else {
+            if (!whole(r)) {
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const uint64_t p = start + (uint64_t) h * kChunk + 16 * lane;
