@@ -2722,6 +2722,11 @@ void k_decode_suffix_held(
         uint32_t T = 0;
 #pragma unroll
         for (int i = 0; i < 6; i++) Hn[i] = 0;
+        // this range's copy (issued by the range before, or for the tile's
+        // first) has landed: waited for on every path, so that no path of
+        // the listing reaches a barrier with a copy in flight
+        // (tests/tools/isa_check.py; under `if (whole(r))` the checker saw
+        // the infeasible path that skips it)
         vm_wait_all();
         if (r < nranges) {
             const uint64_t rb = (uint64_t) r * R;
