@@ -1383,7 +1383,9 @@ DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
         const uint32_t t1 = tab[(dw[g] >> 8) & 0xFFu];
         const uint32_t t2 = tab[(dw[g] >> 16) & 0xFFu];
         const uint32_t t3 = tab[dw[g] >> 24];
-        P[g] = t0 | (t1 << 8) | (t2 << 16) | (t3 << 24);
+        // two byte pairs and an OR (written as shifts, the compiler made it
+        // three shifts and a three-way OR)
+        P[g] = __builtin_amdgcn_perm(t1, t0, 0x0C0C0400u) | __builtin_amdgcn_perm(t3, t2, 0x04000C0Cu);
     }
     if (nin < 16) {
 #pragma unroll
@@ -1402,13 +1404,18 @@ DEV void lane_values(const uint8_t *tab, uint4 w, uint32_t nin, uint32_t P[4])
 // (the window's atomic ORs go through a pointer) and waited for every copy
 // in flight (vmcnt(0)) at the first of them, right after the copy was
 // issued.  The reader waits itself (vm_wait_all) before it reads the copy.
-DEV void lds_dma16(const void *gsrc, void *lds_dst)
+// The source is a wave-uniform base (SGPRs) plus 16 x lane: with a per-lane
+// 64-bit address the compiler hoisted `in + 16 lane` out of the tile loop
+// and spilled it, and its reload before each copy waited (vmcnt(0)) for the
+// stores of the tile before.
+DEV void lds_dma16(const uint8_t *gbase, void *lds_dst)
 {
     const uint32_t l = (uint32_t) (uintptr_t) (__attribute__((address_space(3))) void *) lds_dst;
+    const uint32_t voff = 16u * lane_id();
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(gbase), "s"(l) : "memory");
 }
 
 DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -1452,30 +1459,33 @@ DEV void build_compact_sel(uint32_t *sel)
 
 DEV uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
 
-// OR a left-aligned field (bits 23..24-w of F; the rest zero) into the
+// OR a field left-aligned in G (bits 31..32-w; the rest zero) into the
 // big-endian bit stream held in `bits` (dwords), its first bit at stream
 // bit p.  BE: the dwords hold the stream big-endian (the reader swaps each
 // dword once when it stores: decode_range's 16-byte blocks), else
 // little-endian per byte, the output bytes as they are (decode_buf_bits).
+// The two dwords are G >> o and the bits shifted out of it (v_lshrrev,
+// v_alignbit: both take the shift's low 5 bits, so p goes in as it is), the
+// dword index one v_bfe (round 5: a 64-bit shift of a zero-extended 24-bit
+// field by 40 - o, and a shift, mask and add for the address).
 template <bool BE = false>
-DEV void or_field(uint32_t *bits, uint32_t p, uint32_t F)
+DEV void or_field(uint32_t *bits, uint32_t p, uint32_t G)
 {
     const uint32_t o = p & 31u;
-    const uint64_t W = (uint64_t) F << (40u - o);
-    uint32_t *q = (uint32_t *) ((uint8_t *) bits + ((p >> 3) & ~3u));
-    const uint32_t hi = (uint32_t) (W >> 32), lo = (uint32_t) W;
+    const uint32_t hi = G >> o, lo = __builtin_amdgcn_alignbit(G, 0u, o);
+    uint32_t *q = bits + __builtin_amdgcn_ubfe(p, 5, 27);
     __hip_atomic_fetch_or(q, BE ? hi : bswap32(hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(q + 1, BE ? lo : bswap32(lo), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // Sextets in bytes 0..3 of D (stream order; absent ones zero) -> the
-// 24-bit group s0 s1 s2 s3.
+// group s0 s1 s2 s3 left-aligned in 32 bits (bits 31..8).
 DEV uint32_t group_dot(uint32_t D)
 {
     const uint32_t x = __builtin_amdgcn_udot4(D, 0x00000140u, 0u, false);  // s0*64 + s1
     const uint32_t y = __builtin_amdgcn_udot4(D, 0x01400000u, 0u, false);  // s2*64 + s3
-    return (x << 12) | y;
+    return (x << 20) | (y << 8);
 }
 
 // Copy LDS bytes [lo, hi) of `b` (a wave's buffer) to dst0 + [lo, hi),
@@ -2330,7 +2340,7 @@ DEV void decode_range(const P2dSmem &sm, uint4 *bq, const uint8_t *__restrict__ 
                 (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
             const int need = 4 - (T & 3);
             if (v && (int) rank < need)
-                or_field<true>(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 18);
+                or_field<true>(bits, (uint32_t) (pb0 + 6 * (T + (int) rank)), t << 26);
             const int got = __popcll(m);
             if (got >= need) {
                 T += need;
@@ -2598,7 +2608,10 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
     // first, so that one wait covers them and the first groups.
     const uint32_t hend = a ? (16 - a < nb ? 16 - a : nb) : 0u;
     const uint32_t tb = mend > m0 ? 16 * mend - a : hend;
-    const uint32_t bi = lane < 16 ? lane : (tb > hend ? tb : hend) + (lane - 16);
+    // (lane + a scalar: written as lane - 16 + ..., the loop-invariant
+    // lane - 16 was hoisted out of the tile loop and spilled, and its reload
+    // in every range waited for the previous range's stores)
+    const uint32_t bi = lane + (lane < 16 ? 0u : (tb > hend ? tb : hend) - 16u);
     const bool act = lane < 16 ? bi < hend : lane < 32 && bi < nb;
     const uint32_t X = s + 8 * bi, xi = (X >> 5) < kLast ? X >> 5 : kLast;
     const uint32_t x0 = win[xi], x1 = win[xi + 1];
@@ -2702,7 +2715,7 @@ void k_decode_suffix_held(
         return dma && r < nranges && r != r0 && (uint64_t) (r + 1) * R <= n;
     };
     auto fetch = [&](uint32_t r, uint32_t buf) {
-        const uint8_t *src = in + (uint64_t) r * R + 16 * lane;
+        const uint8_t *src = in + (uint64_t) r * R;  // wave-uniform
         lds_dma16(src, &s_rng[wv][buf][0]);
         lds_dma16(src + kChunk, &s_rng[wv][buf][64]);
     };
@@ -2752,7 +2765,9 @@ void k_decode_suffix_held(
             bq[lane] = make_uint4(0, 0, 0, 0);
             if (lane + 64 < kP2dBlocks) bq[lane + 64] = make_uint4(0, 0, 0, 0);
             wave_lds_order();
-            T = bits_step<true>(sm, bits, c, nin, 0);
+            // the wave's window as bits past sm.bits[0]: the ORs' addresses
+            // are then a constant plus (p >> 3) & ~3, no per-wave base added
+            T = bits_step<true>(sm, (uint32_t *) sm.bits[0], c, nin, (int) (wv * kP2dBlocks * 128));
             wave_lds_order();
 #pragma unroll
             for (int i = 0; i < 6; i++) Hn[i] = bits[lane + 64 * i];  // consecutive lanes
@@ -2790,7 +2805,7 @@ void k_decode_suffix_held(
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
                 const uint32_t need = 4u - (((uint32_t) Bp + Tc) & 3u);
-                if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 18);
+                if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 26);
                 const uint32_t got = (uint32_t) __popcll(m);
                 if (got >= need) {
                     Tc += need;
