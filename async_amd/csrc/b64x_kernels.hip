@@ -2591,9 +2591,17 @@ DEV uint32_t window_delta(uint32_t s, const uint8_t *dst)
 // plus the next group's first dword from the next lane, funnel-shifted by
 // the same amount for every block; the partial blocks at both ends one byte
 // per lane.
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const v4u32 lds_v4u32;
+
 DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t *dst)
 {
     const uint32_t lane = lane_id();
+    // wave-uniform arguments, made visibly so (read back from LDS counts, the
+    // compiler kept them and everything derived from them in VGPRs: the
+    // shift's test an exec-mask branch, the block loop's bounds vector)
+    s = (uint32_t) __builtin_amdgcn_readfirstlane((int) s);
+    nb = (uint32_t) __builtin_amdgcn_readfirstlane((int) nb);
     const uint32_t a = (uint32_t) ((uintptr_t) dst & 15);
     // block m of the aligned grid covers bytes [16 m - a, 16 m - a + 16)
     const uint32_t m0 = a ? 1u : 0u, mend = (nb + a) >> 4;
@@ -2601,7 +2609,6 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
     const uint32_t i0 = b0 >> 5, sh = b0 & 31;  // block m0's first window dword (a multiple of 4)
     const uint32_t nblk = mend > m0 ? mend - m0 : 0u;
     uint8_t *const base = dst - a + 16 * m0;     // 16-byte aligned, wave-uniform
-    const uint4 *win4 = (const uint4 *) win;
     constexpr uint32_t kLast = kP2dBlocks * 4 - 8;  // the last group read in full
     // The partial blocks' bytes (head [0, hend), tail [tb, nb); at most 15
     // each, one per lane of lanes 0-31): their two window dwords are read
@@ -2624,7 +2631,11 @@ DEV void store_window_bits(const uint32_t *win, uint32_t s, uint32_t nb, uint8_t
         const uint32_t k = k0 + lane;
         const uint32_t ik = i0 + 4 * k;
         const uint32_t i = ik < kLast ? ik : kLast;
-        const uint4 g = win4[i >> 2];
+        // one ds_read_b128 (a plain uint4 read was split into five reads
+        // of overlapping dword pairs, each waited for: the non-temporal form
+        // keeps it whole; LDS has no temporal hint to take)
+        const v4u32 g4 = __builtin_nontemporal_load((const lds_v4u32 *) (win + i));
+        const uint4 g = make_uint4(g4.x, g4.y, g4.z, g4.w);
         const uint32_t w4 = win[i + 4];
         uint32_t o0 = g.x, o1 = g.y, o2 = g.z, o3 = g.w;
         if (sh) {
