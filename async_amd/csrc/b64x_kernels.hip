@@ -120,6 +120,17 @@ DEV void build_dec_table(uint8_t *tab, const DecAlpha &a)
         tab[c] = (uint8_t) dec_value(c, a);
 }
 
+// The bit-stream decode's form (k_decode_suffix_held): sextet v as 4 v, 0xFF
+// for "not in the alphabet" -- the flag in bit 0, so a dword's four flags
+// are one AND, and the sextets still pack by v_dot4 (weights 64, 1).
+DEV void build_dec_table_lo(uint8_t *tab, const DecAlpha &a)
+{
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) {
+        const uint32_t v = dec_value(c, a);
+        tab[c] = (uint8_t) (v < 64 ? v << 2 : 0xFFu);
+    }
+}
+
 // ------------------------------------------------------- memory helpers --
 
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
@@ -1148,6 +1159,7 @@ void k_decode_pass1(
 
 // The stream's last V mod 4 alphabet characters (as sextets) into
 // res->tail, scanning backwards from the end; one wave.
+template <bool LO = false>  // LO: a build_dec_table_lo table
 DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, uint64_t V,
                            b64x_dec_result *res, b64x_dec_result *hres)
 {
@@ -1159,6 +1171,7 @@ DEV void find_tail_sextets(const uint8_t *tab, const uint8_t *in, uint64_t n, ui
         uint64_t beg = end >= 64 ? end - 64 : 0;
         uint64_t p = beg + lane;
         uint32_t t = p < end ? tab[in[p]] : 0xFFu;
+        if (LO) t = t & 3u ? 0xFFu : t >> 2;
         uint64_t bm = __ballot(t < 64u);
         while (need > 0 && bm) {
             int hi = 63 - __clzll(bm);
@@ -1479,13 +1492,14 @@ DEV void or_field(uint32_t *bits, uint32_t p, uint32_t G)
                           __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// Sextets in bytes 0..3 of D (stream order; absent ones zero) -> the
-// group s0 s1 s2 s3 left-aligned in 32 bits (bits 31..8).
+// Sextets in bytes 0..3 of D (stream order; absent ones zero; LO: as 4 s)
+// -> the group s0 s1 s2 s3 left-aligned in 32 bits (bits 31..8).
+template <bool LO = false>
 DEV uint32_t group_dot(uint32_t D)
 {
     const uint32_t x = __builtin_amdgcn_udot4(D, 0x00000140u, 0u, false);  // s0*64 + s1
     const uint32_t y = __builtin_amdgcn_udot4(D, 0x01400000u, 0u, false);  // s2*64 + s3
-    return (x << 20) | (y << 8);
+    return LO ? (x << 18) | (y << 6) : (x << 20) | (y << 8);
 }
 
 // Copy LDS bytes [lo, hi) of `b` (a wave's buffer) to dst0 + [lo, hi),
@@ -1571,7 +1585,7 @@ DEV uint32_t wave_incl_scan_dpp(uint32_t x)
 // sextet fields OR-ed into `bits` from window bit `bit0` on (bit0 may sit
 // up to 18 bits past the window's byte 4: skipped sextets land in its
 // head).  Returns the step's alphabet characters.
-template <bool BE = false, class SM = P2dSmem>
+template <bool BE = false, class SM = P2dSmem, bool LO = false>  // LO: build_dec_table_lo
 DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
                        const uint32_t nin[2], int bit0)
 {
@@ -1590,7 +1604,7 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
         acc[h][0] = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const uint32_t iv = (P[h][g] >> 7) & 0x01010101u;
+            const uint32_t iv = LO ? P[h][g] & 0x01010101u : (P[h][g] >> 7) & 0x01010101u;
             const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
             sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
             acc[h][g + 1] = __builtin_amdgcn_sdot4((int) iv, (int) 0xFAFAFAFAu, acc[h][g], false);
@@ -1608,7 +1622,7 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
             // absent sextets are zero bytes
-            or_field<BE>(bits, p + 24u * g + (uint32_t) acc[h][g], group_dot(D));
+            or_field<BE>(bits, p + 24u * g + (uint32_t) acc[h][g], group_dot<LO>(D));
         }
     }
     return ((tot & 0xFFFFu) + (tot >> 16)) / 6u;  // alphabet characters (scalar)
@@ -2678,7 +2692,7 @@ void k_decode_suffix_held(
     using Cnt = typename std::conditional<BIG, uint64_t, uint32_t>::type;
     __shared__ uint32_t s_cnt[2][TILE];
     __shared__ Cnt s_excl;
-    build_dec_table(sm.tab, a);
+    build_dec_table_lo(sm.tab, a);  // the bit-stream form: sextets as 4 v, flag in bit 0
     build_compact_sel(sm.sel);
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2778,7 +2792,7 @@ void k_decode_suffix_held(
             wave_lds_order();
             // the wave's window as bits past sm.bits[0]: the ORs' addresses
             // are then a constant plus (p >> 3) & ~3, no per-wave base added
-            T = bits_step<true>(sm, (uint32_t *) sm.bits[0], c, nin, (int) (wv * kP2dBlocks * 128));
+            T = bits_step<true, P2dSmem, true>(sm, (uint32_t *) sm.bits[0], c, nin, (int) (wv * kP2dBlocks * 128));
             wave_lds_order();
 #pragma unroll
             for (int i = 0; i < 6; i++) Hn[i] = bits[lane + 64 * i];  // consecutive lanes
@@ -2810,13 +2824,13 @@ void k_decode_suffix_held(
             // complete the range's last group from the characters after it
             bool ok = re + lane < n;
             for (uint64_t q = re;;) {
-                const uint32_t t = ok ? la : 0xFFu;  // a table value
-                const bool v = t < 64u;
+                const uint32_t t = ok ? la : 0xFFu;  // a table value (4 v, or 0xFF)
+                const bool v = (t & 3u) == 0;
                 const uint64_t m = __ballot(v);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
                 const uint32_t need = 4u - (((uint32_t) Bp + Tc) & 3u);
-                if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 26);
+                if (v && rank < need) or_field<true>(bits, 32 * dl + 6 * (Tc + rank), t << 24);
                 const uint32_t got = (uint32_t) __popcll(m);
                 if (got >= need) {
                     Tc += need;
@@ -2927,7 +2941,7 @@ void k_decode_suffix_held(
     if (!owner || wv != 0) return;
     const uint64_t V = Vb + Vs;
     if (lane == 0) write_result(res, hres, V, hold, n, seq);
-    find_tail_sextets(sm.tab, in, n, V, res, hres);
+    find_tail_sextets<true>(sm.tab, in, n, V, res, hres);
     if (lane == 0) {
         while (__hip_atomic_load(w.wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x)
             __builtin_amdgcn_s_sleep(1);
