@@ -1457,12 +1457,14 @@ struct __attribute__((aligned(16))) P2dSmem {
 
 // sel[m]: the v_perm selector that packs a dword's bytes whose bit j of m
 // is clear (the alphabet ones) into its low bytes, zeros above.
+// KEEP_SET: indexed by the alphabet bytes' mask instead (bit j set: keep).
+template <bool KEEP_SET = false>
 DEV void build_compact_sel(uint32_t *sel)
 {
     if (threadIdx.x < 16) {
         uint32_t v = 0x0C0C0C0Cu, k = 0;
         for (uint32_t j = 0; j < 4; j++)
-            if (!((threadIdx.x >> j) & 1u)) {
+            if (((threadIdx.x >> j) & 1u) == (KEEP_SET ? 1u : 0u)) {
                 v = (v & ~(0xFFu << (8 * k))) | (j << (8 * k));
                 k++;
             }
@@ -1595,21 +1597,27 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
     // chunks packed in one DPP scan), so positions need no multiply
     // acc[h][g]: -6 x the non-alphabet bytes of chunk h before group g, a
     // running signed v_dot4 (group g's field sits 24 g + acc[h][g] bits into
-    // the lane's share of the chunk)
+    // the lane's share of the chunk).  LO: the alphabet bytes' flags (one
+    // v_bitop3 of the table values), the selectors indexed by them
+    // (build_compact_sel<true>), and acc[h][g] the bits before group g, a
+    // running unsigned v_dot4 (its own destination: the signed one
+    // accumulates in place, a v_mov per group to keep each sum)
     uint32_t P[2][4], sel[2][4], cnt = 0;
-    int acc[2][5];
+    uint32_t acc[2][5];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         lane_values(sm.tab, c[h], nin[h], P[h]);
         acc[h][0] = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const uint32_t iv = LO ? P[h][g] & 0x01010101u : (P[h][g] >> 7) & 0x01010101u;
+            const uint32_t iv = LO ? ~P[h][g] & 0x01010101u : (P[h][g] >> 7) & 0x01010101u;
             const uint32_t off = __builtin_amdgcn_udot4(iv, 0x20100804u, 0u, false);
             sel[h][g] = *(const uint32_t *) ((const uint8_t *) sm.sel + off);
-            acc[h][g + 1] = __builtin_amdgcn_sdot4((int) iv, (int) 0xFAFAFAFAu, acc[h][g], false);
+            acc[h][g + 1] = LO ? __builtin_amdgcn_udot4(iv, 0x06060606u, acc[h][g], false)
+                               : (uint32_t) __builtin_amdgcn_sdot4((int) iv, (int) 0xFAFAFAFAu,
+                                                                  (int) acc[h][g], false);
         }
-        cnt |= (uint32_t) (96 + acc[h][4]) << (16 * h);  // the lane's output bits in chunk h (<= 96)
+        cnt |= (LO ? acc[h][4] : 96u + acc[h][4]) << (16 * h);  // the lane's output bits in chunk h (<= 96)
     }
     const uint32_t incl = wave_incl_scan_dpp(cnt);  // halves <= 6,144
     const uint32_t ex = incl - cnt;
@@ -1622,7 +1630,7 @@ DEV uint32_t bits_step(const SM &sm, uint32_t *bits, const uint4 c[2],
         for (int g = 0; g < 4; g++) {
             const uint32_t D = __builtin_amdgcn_perm(0u, P[h][g], sel[h][g]);
             // absent sextets are zero bytes
-            or_field<BE>(bits, p + 24u * g + (uint32_t) acc[h][g], group_dot<LO>(D));
+            or_field<BE>(bits, p + (LO ? 0u : 24u * g) + acc[h][g], group_dot<LO>(D));
         }
     }
     return ((tot & 0xFFFFu) + (tot >> 16)) / 6u;  // alphabet characters (scalar)
@@ -2693,7 +2701,7 @@ void k_decode_suffix_held(
     __shared__ uint32_t s_cnt[2][TILE];
     __shared__ Cnt s_excl;
     build_dec_table_lo(sm.tab, a);  // the bit-stream form: sextets as 4 v, flag in bit 0
-    build_compact_sel(sm.sel);
+    build_compact_sel<true>(sm.sel);  // indexed by the alphabet bytes (bits_step<..., true>)
     const uint32_t lane = lane_id();
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 *bq = sm.bits[wv];
