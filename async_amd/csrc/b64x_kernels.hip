@@ -2610,9 +2610,10 @@ DEV uint32_t window_delta(uint32_t s, const uint8_t *dst)
 // dwords, or_field<true>; s placed by window_delta): aligned 16-byte
 // blocks of dst, each four window dwords read as one aligned 16-byte LDS
 // read (consecutive lanes, consecutive 16-byte groups: no bank conflicts)
-// plus the next group's first dword from the next lane, funnel-shifted by
-// the same amount for every block; the partial blocks at both ends one byte
-// per lane.
+// plus, when the shift is not 0, the next group's first dword (a
+// ds_read_b32 four ways conflicted; taking it from the next lane by DPP
+// cost more VALU than the conflicts), funnel-shifted by the same
+// amount for every block; the partial blocks at both ends one byte per lane.
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4u32 lds_v4u32;
 
