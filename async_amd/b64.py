@@ -56,7 +56,14 @@ def workspace_size(nchars: int = 0) -> int:
     return int(_lib.load().b64x_decode_workspace_size(nchars))
 
 
+_DEFAULT_ABC: list = []  # the reference's alphabet, built once (read-only to the library)
+
+
 def _abc(abc) -> _lib.Alphabet:
+    if abc is None:
+        if not _DEFAULT_ABC:
+            _DEFAULT_ABC.append(alphabet())
+        return _DEFAULT_ABC[0]
     return abc if isinstance(abc, _lib.Alphabet) else alphabet(*abc) if abc else alphabet()
 
 
@@ -133,12 +140,14 @@ def decode(x: torch.Tensor, out: torch.Tensor | None = None, abc=None,
         workspace = torch.zeros(workspace_size(n), dtype=torch.uint8, device=x.device)
     flags = (HOLD_TAIL if hold_tail else 0) | (EXPECT_JUNK if expect_junk else 0)
     seq = ctypes.c_uint32(0)
+    # the stream looked up once (torch.cuda.current_stream() costs ~3 us of
+    # the call's host time, and a junk-laden or small decode is timed with it)
+    s = stream if stream is not None else torch.cuda.current_stream()
     _lib.check("b64x_decode_dev_seq", lib.b64x_decode_dev_seq(
         _ptr(x), n, _ptr(out), _ptr(result), ctypes.byref(a), flags,
-        _ptr(workspace) if workspace is not None else None, _stream(stream),
+        _ptr(workspace) if workspace is not None else None, s.cuda_stream,
         ctypes.byref(seq)))
-    return Decoded(out, result, n, flags & HOLD_TAIL, seq.value,
-                   stream if stream is not None else torch.cuda.current_stream())
+    return Decoded(out, result, n, flags & HOLD_TAIL, seq.value, s)
 
 
 def encode_strided(x: torch.Tensor, in_stride: int, length: int, nbuf: int,
