@@ -4875,7 +4875,7 @@ int b64x_decode_strided(const void *d_in, uint64_t in_stride, uint64_t len,
     if (nbuf > 1 && (in_stride < len || out_stride < b64x_decoded_cap(len))) return -EINVAL;
     const uint64_t S = (len + 15) / 16;
     const uint64_t slots = S * nbuf;
-    BatchLayout L{nullptr, nullptr, in_stride, out_stride, len};
+    BatchLayout L{nullptr, nullptr, in_stride, out_stride, len, 0, nullptr};
     if (slots > 0xFFFFFFFFull - 4096 || len > 0xFFFFFFFFull)
         return launch_batch_decode(d_in, L, nbuf, d_out, d_outlen, abc, stream);
     const DeviceInfo *d = device_info();
@@ -4985,7 +4985,7 @@ int b64x_decode_batch(const void *d_in, const uint64_t *d_in_off, uint32_t nbuf,
 {
     if (nbuf == 0) return 0;
     if (!d_in || !d_in_off || !d_out || !d_out_off || !d_outlen) return -EINVAL;
-    BatchLayout L{d_in_off, d_out_off, 0, 0, 0};
+    BatchLayout L{d_in_off, d_out_off, 0, 0, 0, 0, nullptr};
     return launch_batch_decode(d_in, L, nbuf, d_out, d_outlen, abc, stream);
 }
 
