@@ -1877,9 +1877,16 @@ constexpr uint64_t kProbeSampleMin = 1u << 18;  // shorter streams: the first wi
 constexpr uint32_t kProbeNS = 256;              // sampling threads
 constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
 
+// One block of kProbeThreads threads; tab/s_m/s_first in LDS.  publish:
+// also publish a cut model's slot T as failing (lfail, fail_any) for the
+// k_decode_lines and k_decode_suffix_held<false> launches that follow it.
+// The hinted single pass runs its probe after itself with publish 0: the
+// probe then only renews the hint and the model for the next call, and a
+// call that reuses that model has k_decode_lines publish the cut itself.
 __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
                                                                 DecAlpha a, void *ws, uint32_t nranges,
-                                                                DecodeHint *hint, uint32_t key)
+                                                                DecodeHint *hint, uint32_t key,
+                                                                uint32_t publish)
 {
     __shared__ uint8_t tab[256];
     __shared__ LineModel s_m;
@@ -1969,7 +1976,7 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
             mo.skip = 1;
         }
     }
-    if (mo.skip) {
+    if (mo.skip && publish) {
         *ws_view(ws, nranges).lfail = ~(uint64_t) mo.T;
         *ws_view(ws, nranges).fail_any = 1;
     }
@@ -4719,9 +4726,12 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         }
         // The probe of the last call on the same workspace, input and length
         // cut the line model near the start (junk throughout): this call
-        // takes the single pass after its own probe (which renews the hint)
-        // and skips k_decode_lines' launch of blocks that would all leave
-        // at once.  Same bytes either way; only the path differs.
+        // takes the single pass, then its own probe (which renews the hint
+        // and the model for the next call; launched second, it runs behind
+        // the decode instead of in front of it, and the gap the host's
+        // second launch left between the two kernels is gone), and skips
+        // k_decode_lines' launch of blocks that would all leave at once.
+        // Same bytes either way; only the path differs.
         DecodeHint *hints = decode_hints();
         const uint32_t key = hint_key(ws, d_in, nchars);
         DecodeHint *hint = hints ? hints + (key % kDecodeHints) : nullptr;
@@ -4738,23 +4748,31 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
             reuse = g_held[hs].ws == ws && g_held[hs].n == nchars &&
                     !*(volatile uint32_t *) reprobe;
         }
+        if (junky) {
+            path_taken(kPathHinted);
+            if (reprobe) *(volatile uint32_t *) reprobe = 0;
+            hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
+                               (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
+                               hold, d_res, h_res, seq, nullptr);
+            if ((err = launch_status())) return err;
+            hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
+                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key, 0u);
+            if ((err = launch_status())) return err;
+            path_taken(kPathProbe);
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            g_held[hs] = HeldModel{ws, nchars};
+            return 0;
+        }
         if (!reuse) {
             if (reprobe) *(volatile uint32_t *) reprobe = 0;
             hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
-                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key);
+                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key, 1u);
             if ((err = launch_status())) return err;
             path_taken(kPathProbe);
             std::lock_guard<std::mutex> lk(g_held_mu);
             g_held[hs] = HeldModel{ws, nchars};
         } else {
             path_taken(kPathHeld);
-        }
-        if (junky) {
-            path_taken(kPathHinted);
-            hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
-                               (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res, seq, nullptr);
-            return launch_status();
         }
         const uint64_t waves = (nchars / 16 + 1 + kLinesSlots - 1) / kLinesSlots;
         hipLaunchKernelGGL(k_lines, dim3((uint32_t) ((waves + kLinesWaves - 1) / kLinesWaves)),

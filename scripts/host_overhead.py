@@ -36,14 +36,14 @@ legs = {
     "clean": lambda: b64.decode(enc, out=out, workspace=ws, result=rr),
 }
 # ORDER=ej,hinted,... runs the legs in that order, twice (the first leg after
-# the setup may run on a GPU whose clocks are still ramping)
+# the setup may run on a GPU whose clocks are still ramping); REPS calls a leg
 order = os.environ.get("ORDER", "junk_hinted,junk_ej,clean").split(",")
 for name in order:
     fn = legs[name]
     fn()
     torch.cuda.synchronize()
     host, gpu = [], []
-    for _ in range(20):
+    for _ in range(int(os.environ.get("REPS", "20"))):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         t0 = time.perf_counter()
