@@ -856,7 +856,7 @@ def test_decode_lines_takes_clean_and_mime_whole(aligned):
 def test_repeat_junk_decode_takes_the_hinted_single_pass():
     """A call whose probe cut the line model near the start leaves a hint
     for the next call on the same workspace, input and length: that one
-    takes the single pass (no k_decode_lines launch) after its own probe.
+    takes the single pass (no k_decode_lines launch), then its own probe.
     Every call is exact; a clean stream in the same buffer goes back to the
     lines pass on the call after the one that finds it clean."""
     rng = np.random.default_rng(47)
@@ -1206,6 +1206,10 @@ def test_new_content_at_a_held_address_and_length():
     # a 5 %-junk text, and what they decode to
     junky = [_junk(rng, c, 0.05)[:m] for c in clean]
     want_j = [orc.decode(t) for t in junky]
+    # clean for its first half, 5 % junk after: a probe cuts its model past
+    # the stream's first sixteenth (no hint)
+    mid = (clean[0][:m // 2] + _junk(rng, clean[0][m // 2:], 0.05))[:m]
+    want_mid = orc.decode(mid)
     x = torch.empty(m, dtype=torch.uint8, device=DEV)
     out = torch.zeros(b64.decoded_cap(m) + 8, dtype=torch.uint8, device=DEV)
     res = torch.zeros(b64.RES_BYTES, dtype=torch.uint8, device=DEV)
@@ -1248,6 +1252,18 @@ def test_new_content_at_a_held_address_and_length():
         run(clean[2], raw[2].tobytes(), [1, 0, 1])
         # then the lines pass on the held clean model, no probe
         run(clean[3], raw[3].tobytes(), [0, 1, 0])
+        # junk under the held clean model, then the probe that sets the hint
+        run(junky[2], want_j[2], [0, 1, 0])
+        run(junky[2], want_j[2], [1, 0, 0])
+        # the hinted single pass on content the probe behind it cuts past the
+        # first sixteenth: the hint turns clean and the cut model is held,
+        # its cut not published (that probe runs after the decode)...
+        run(mid, want_mid, [1, 0, 1])
+        # ...so the next call takes the held cut model without a probe and
+        # k_decode_lines publishes the cut itself; the suffix had work, so
+        # the call after that probes again
+        run(mid, want_mid, [0, 1, 0])
+        run(mid, want_mid, [1, 0, 0])
         if ws is None:
             import ctypes
 
