@@ -1877,20 +1877,25 @@ constexpr uint64_t kProbeSampleMin = 1u << 18;  // shorter streams: the first wi
 constexpr uint32_t kProbeNS = 256;              // sampling threads
 constexpr uint64_t kProbeTailKeep = 4096;       // samples avoid the stream's end (padding, a short last line)
 
-// One block of kProbeThreads threads; tab/s_m/s_first in LDS.  publish:
-// also publish a cut model's slot T as failing (lfail, fail_any) for the
-// k_decode_lines and k_decode_suffix_held<false> launches that follow it.
-// The hinted single pass runs its probe after itself with publish 0: the
-// probe then only renews the hint and the model for the next call, and a
-// call that reuses that model has k_decode_lines publish the cut itself.
-__global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
-                                                                DecAlpha a, void *ws, uint32_t nranges,
-                                                                DecodeHint *hint, uint32_t key,
-                                                                uint32_t publish)
+struct ProbeSmem {
+    uint8_t tab[256];
+    LineModel m;
+    unsigned long long first;
+};
+
+// The probe, run by one block of kProbeThreads threads (all of them call
+// it).  publish: also publish a cut model's slot T as failing (lfail,
+// fail_any) for the k_decode_lines and k_decode_suffix_held<false> launches
+// that follow it.  The hinted single pass runs it itself, in the first
+// block that finds no tile left, with publish 0: it then only renews the
+// hint and the model for the next call, and a call that reuses that model
+// has k_decode_lines publish the cut itself.
+DEV void probe_stream(ProbeSmem &ps, const uint8_t *__restrict__ in, uint64_t n, DecAlpha a,
+                      void *ws, uint32_t nranges, DecodeHint *hint, uint32_t key, uint32_t publish)
 {
-    __shared__ uint8_t tab[256];
-    __shared__ LineModel s_m;
-    __shared__ unsigned long long s_first;
+    uint8_t *const tab = ps.tab;
+    LineModel &s_m = ps.m;
+    unsigned long long &s_first = ps.first;
     // the samples' loads are issued first: they overlap the table build and
     // the window probe
     const bool sample = n >= kProbeSampleMin && threadIdx.x < kProbeNS;
@@ -1987,6 +1992,14 @@ __global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *_
         h->junky = mo.skip && 256 * (uint64_t) mo.T < n ? 1u : 0u;  // 16 T < n / 16
         h->key = key;
     }
+}
+
+__global__ void __launch_bounds__(kProbeThreads) k_decode_probe(const uint8_t *__restrict__ in, uint64_t n,
+                                                                DecAlpha a, void *ws, uint32_t nranges,
+                                                                DecodeHint *hint, uint32_t key)
+{
+    __shared__ ProbeSmem ps;
+    probe_stream(ps, in, n, a, ws, nranges, hint, key, 1u);
 }
 
 // At least 6 waves per SIMD (80 VGPRs): unconstrained, the rarely taken
@@ -2690,7 +2703,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kHeldW
 void k_decode_suffix_held(
     const uint8_t *__restrict__ in, uint64_t n, uint8_t *__restrict__ out, uint32_t nranges,
     DecAlpha a, void *ws, uint32_t hold, b64x_dec_result *res, b64x_dec_result *hres,
-    uint32_t seq, uint32_t *reprobe)
+    uint32_t seq, uint32_t *reprobe, DecodeHint *hint, uint32_t key)
 {
     constexpr uint64_t R = 2 * kChunk;
     constexpr uint32_t HP = kHeldPer, TILE = kHeldTile;
@@ -2951,6 +2964,15 @@ void k_decode_suffix_held(
         // stores: 762 against 730 us, profiles/r05_ab_sfx_early_draw.jsonl --
         // the tile then starts later and its successors wait)
         if (threadIdx.x == 0) s_tile[bB] = atomicAdd(w.fticket, 1u);
+    }
+    // (s_tile[bB]: the block's last ticket, read at the loop's last pass)
+    if (WHOLE && hint && s_tile[bB] == ntiles) {
+        // the hinted single pass's probe, in the first block that drew no
+        // tile (ticket ntiles: exactly one block), while the others finish
+        // theirs -- not a launch of its own after the decode (3.7 us and a
+        // kernel boundary on every hinted call)
+        __shared__ ProbeSmem ps;
+        probe_stream(ps, in, n, a, ws, nranges, hint, key, 0u);
     }
     block_sync();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w.wdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4721,15 +4743,14 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         if (flags & B64X_DEC_EXPECT_JUNK) {
             hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res, seq, nullptr);
+                               hold, d_res, h_res, seq, nullptr, nullptr, 0u);
             return launch_status();
         }
         // The probe of the last call on the same workspace, input and length
         // cut the line model near the start (junk throughout): this call
-        // takes the single pass, then its own probe (which renews the hint
-        // and the model for the next call; launched second, it runs behind
-        // the decode instead of in front of it, and the gap the host's
-        // second launch left between the two kernels is gone), and skips
+        // takes the single pass, which runs the probe itself (renewing the
+        // hint and the model for the next call) in its first block to run
+        // out of tiles, while the others finish theirs, and skips
         // k_decode_lines' launch of blocks that would all leave at once.
         // Same bytes either way; only the path differs.
         DecodeHint *hints = decode_hints();
@@ -4753,10 +4774,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
             if (reprobe) *(volatile uint32_t *) reprobe = 0;
             hipLaunchKernelGGL(k_whole, dim3(sfx_grid), dim3(kThreads), 0, s,
                                (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                               hold, d_res, h_res, seq, nullptr);
-            if ((err = launch_status())) return err;
-            hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
-                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key, 0u);
+                               hold, d_res, h_res, seq, nullptr, hint, key);
             if ((err = launch_status())) return err;
             path_taken(kPathProbe);
             std::lock_guard<std::mutex> lk(g_held_mu);
@@ -4766,7 +4784,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         if (!reuse) {
             if (reprobe) *(volatile uint32_t *) reprobe = 0;
             hipLaunchKernelGGL(k_decode_probe, dim3(1), dim3(kProbeThreads), 0, s,
-                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key, 1u);
+                               (const uint8_t *) d_in, nchars, a, ws, p.nranges, hint, key);
             if ((err = launch_status())) return err;
             path_taken(kPathProbe);
             std::lock_guard<std::mutex> lk(g_held_mu);
@@ -4781,7 +4799,7 @@ static int decode_dev_ws(const void *d_in, uint64_t nchars, void *d_out,
         if ((err = launch_status())) return err;
         hipLaunchKernelGGL(k_sfx, dim3(sfx_grid), dim3(kThreads), 0, s,
                            (const uint8_t *) d_in, nchars, (uint8_t *) d_out, p.nranges, a, ws,
-                           hold, d_res, h_res, seq, reprobe);
+                           hold, d_res, h_res, seq, reprobe, nullptr, 0u);
         return launch_status();
     }
     // Larger inputs (ranges longer than 2,048 characters): pass 1, the scan,
