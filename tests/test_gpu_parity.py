@@ -856,7 +856,8 @@ def test_decode_lines_takes_clean_and_mime_whole(aligned):
 def test_repeat_junk_decode_takes_the_hinted_single_pass():
     """A call whose probe cut the line model near the start leaves a hint
     for the next call on the same workspace, input and length: that one
-    takes the single pass (no k_decode_lines launch), then its own probe.
+    takes the single pass (no k_decode_lines launch), which runs the probe
+    itself in its first block left without a tile.
     Every call is exact; a clean stream in the same buffer goes back to the
     lines pass on the call after the one that finds it clean."""
     rng = np.random.default_rng(47)
@@ -1255,9 +1256,9 @@ def test_new_content_at_a_held_address_and_length():
         # junk under the held clean model, then the probe that sets the hint
         run(junky[2], want_j[2], [0, 1, 0])
         run(junky[2], want_j[2], [1, 0, 0])
-        # the hinted single pass on content the probe behind it cuts past the
-        # first sixteenth: the hint turns clean and the cut model is held,
-        # its cut not published (that probe runs after the decode)...
+        # the hinted single pass on content its probe (run inside it) cuts
+        # past the first sixteenth: the hint turns clean and the cut model is
+        # held, its cut not published (that probe runs with the decode)...
         run(mid, want_mid, [1, 0, 1])
         # ...so the next call takes the held cut model without a probe and
         # k_decode_lines publishes the cut itself; the suffix had work, so
