@@ -2529,6 +2529,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_pass2d(
 // ticket, `wdone` and the failure words.  Rounds 3-5 shipped a form that
 // counted each tile one tile ahead and re-read it to decode (FETCH 2.01x the
 // input); it was removed in round 6 (DESIGN.md §5 keeps its measurements).
+// hint (the hinted single pass only; else null): the block that draws
+// ticket ntiles -- the first with no tile left -- runs the probe
+// (probe_stream, publish 0) for the next call while the others finish.
 
 // The idle test of k_decode_suffix_held<false>: false when k_decode_lines took
 // everything (its record is then mirrored to the host and the call is
